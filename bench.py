@@ -1,0 +1,326 @@
+"""EfficientDet-D0 bf16 train-step throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 32] [--dtype bf16]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = one full EfficientDet-D0 train step (forward, fused focal+Huber loss, backward,
+gradient all-reduce when N>1, L2 + clip + SGD-momentum + EMA, BN moving statistics) over one
+synthetic 512x512 batch of 32 images per GPU (weak scaling).  Inputs and targets are resident
+in HBM before the timed region.  The step is captured once in a HIP graph and replayed.
+
+Prints ONE JSON line on rank 0 with value = images/s over all ranks, plus
+  roofline     : dominant kernel's algorithmic bytes / its average launch duration (HIP
+                 events around each launch of an instrumented eager step) vs 8 TB/s HBM
+  cpu_baseline : the oracle's fp32 train step (torch-CPU restatement of the reference
+                 semantics, not TF) on the host cores, bounded sample, rank 0 at N=1 only
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def synthetic_batch(anchors, B, size, seed, device, dtype):
+    """x ~ U[0,1); 7 GT boxes/image, size log-uniform 16..400 px, aspect U[0.5,2], class U{1..80}."""
+    rng = np.random.default_rng(seed)
+    x = torch.tensor(rng.random((B, size, size, 3), dtype=np.float32), device=device).to(dtype)
+    G = 7
+    boxes = np.zeros((B, G, 4), np.float32)
+    cls = rng.integers(1, 81, (B, G)).astype(np.int32)
+    for b in range(B):
+        for k in range(G):
+            s = np.exp(rng.uniform(np.log(16), np.log(400)))
+            ar = rng.uniform(0.5, 2.0)
+            h, w = s * np.sqrt(ar), s / np.sqrt(ar)
+            cy, cx = rng.uniform(0, size, 2)
+            boxes[b, k] = [cy - h / 2, cx - w / 2, cy + h / 2, cx + w / 2]
+    t = anchors.generate_targets_batched(torch.tensor(boxes), torch.tensor(cls), torch.full((B,), G, dtype=torch.int32))
+    return x, t
+
+
+# ---------------------------------------------------------------- per-kernel instrumentation
+def algorithmic_bytes(name, args, es):
+    """Minimum HBM bytes of one launch: every operand read once, every output written once."""
+    from tf2mv_amd import _lib as L
+
+    def rows(p):
+        p = getattr(p, "_obj", p)
+        return sum(p.batch * p.H[i] * p.W[i] for i in range(p.nseg))
+
+    if name == "edet_conv1x1_fwd":
+        p, K, N = args[2], args[3], args[5]
+        return rows(p) * (K + N) * es + K * N * es
+    if name == "edet_conv1x1_dgrad":
+        p, N, K, acc = args[3], args[4], args[6], args[9]
+        return rows(p) * (N + K * (1 + acc)) * es + K * N * es
+    if name == "edet_conv1x1_wgrad":
+        p, K, N = args[2], args[3], args[6]
+        return rows(p) * (K + N) * es
+    if name in ("edet_dwconv_fwd", "edet_dwconv_wgrad"):
+        pin, C, pout = args[2], args[3], args[8]
+        return (rows(pin) + rows(pout)) * C * es
+    if name == "edet_dwconv_dgrad":
+        pout, C, pin, acc = args[2], args[3], args[8], args[9]
+        return (rows(pout) + rows(pin) * (1 + acc)) * C * es
+    if name == "edet_lazy_bwd_reduce":
+        return 2 * rows(args[2]) * args[3] * es
+    if name == "edet_lazy_bwd_apply":
+        return (3 + args[9]) * rows(args[2]) * args[3] * es
+    if name == "edet_detection_loss":
+        p, A, NC = args[5], args[6], args[7]
+        return rows(p) * A * (2 * NC * es + 2 * 4 * es + 4 + 16)
+    if name == "edet_stem_fwd":
+        B, H, W, Co = args[2], args[3], args[4], args[6]
+        return B * H * W * 3 * es + B * ((H + 1) // 2) * ((W + 1) // 2) * Co * es
+    if name == "edet_stem_wgrad":
+        B, H, W, Co = args[2], args[3], args[4], args[6]
+        return B * H * W * 3 * es + B * ((H + 1) // 2) * ((W + 1) // 2) * Co * es
+    return None
+
+
+class KernelTimer:
+    """Wraps _lib.call: HIP events on the launch stream around every libedet kernel call."""
+
+    def __init__(self, es):
+        from tf2mv_amd import _lib as L
+        self.L, self.es = L, es
+        self.rec = []
+        self.orig = L.call
+
+    def __enter__(self):
+        L = self.L
+
+        def timed(name, *args):
+            if name in ("edet_memset_async", "edet_memcpy_async"):
+                return self.orig(name, *args)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = self.orig(name, *args)
+            e.record()
+            self.rec.append((name, s, e, algorithmic_bytes(name, args, self.es)))
+            return r
+
+        L.call = timed
+        import tf2mv_amd.ops, tf2mv_amd.model, tf2mv_amd.runtime, tf2mv_amd.anchors  # noqa
+        for mod in (tf2mv_amd.ops, tf2mv_amd.model, tf2mv_amd.runtime, tf2mv_amd.anchors):
+            mod.L.call = timed  # modules hold the _lib module object; patching it once suffices
+        return self
+
+    def __exit__(self, *exc):
+        self.L.call = self.orig
+
+    def summary(self):
+        torch.cuda.synchronize()
+        agg = {}
+        for name, s, e, b in self.rec:
+            ms = s.elapsed_time(e)
+            a = agg.setdefault(name, [0, 0.0, 0.0, True])
+            a[0] += 1
+            a[1] += ms
+            if b is None:
+                a[3] = False
+            else:
+                a[2] += b
+        return agg
+
+
+def cpu_baseline(model, seconds=12.0):
+    """Oracle fp32 train step (forward + loss + backward) on the host cores, 1 image/iteration."""
+    from oracle.ref_model import RefEfficientDet
+    threads = len(os.sched_getaffinity(0))
+    torch.set_num_threads(threads)
+    ref = RefEfficientDet(model, model.state_dict(), dtype=torch.float32)
+    train_keys = [k for k in ref.p if not k.endswith(("moving_mean", "moving_variance"))]
+    for k in train_keys:
+        ref.p[k].requires_grad_(True)
+    S = model.cfg.image_size
+    rng = np.random.default_rng(0)
+    x = rng.random((1, S, S, 3), dtype=np.float32)
+    shapes = [(1,) + model.level_hw[l] + (9,) for l in model.levels]
+    yb = [np.zeros(s + (4,), np.float32) for s in shapes]
+    yc = [np.eye(model.NC, dtype=np.float32)[np.zeros(s, np.int64)] for s in shapes]
+    ym = [np.zeros(s + (1,), bool) for s in shapes]
+    n, t0 = 0, time.perf_counter()
+    while True:
+        box, cls = ref.forward(x, True)
+        loss, _ = ref.detection_loss(box, cls, yb, yc, ym)
+        torch.autograd.grad(loss, [ref.p[k] for k in train_keys], allow_unused=True)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 50:
+            break
+    return {"value": n / el, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} x 1-image 512x512 fp32 train steps (forward+loss+backward) of the oracle "
+                      f"(torch-CPU restatement of the reference TF2 semantics), {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--model", default="efficientdet-d0")
+    ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--kernel-timing", type=int, default=1)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from tf2mv_amd.anchors import Anchors
+    from tf2mv_amd.config import efficientnet_b0_blocks, get_efficientdet_config
+    from tf2mv_amd.model import EfficientDetNetTrain
+
+    cfg = get_efficientdet_config(args.model)
+    S, B = cfg.image_size, args.batch
+    anchors = Anchors(cfg.min_level, cfg.max_level, (S, S), cfg.num_scales, cfg.aspect_ratios, cfg.anchor_scale, device=dev)
+    ar = (lambda t: dist.all_reduce(t)) if world > 1 else None
+    model = EfficientDetNetTrain(efficientnet_b0_blocks(), cfg, anchors, dtype=args.dtype, device=dev, seed=0,
+                                 world_size=world, grad_allreduce=ar, npos_allreduce=ar,
+                                 lr_schedule={"warmup_steps": 100, "total_steps": 10000,
+                                              "adjusted_lr": 0.08 * B * world / 64})
+    x, t = synthetic_batch(anchors, B, S, 1000 + rank, dev, model.eng.tdtype)
+    data = (x, t)
+    log(f"[bench] {args.model} B={B}/gpu world={world} dtype={args.dtype} params={model.P.n_trainable}")
+
+    # eager warm-up (allocates persistent buffers), then capture
+    for _ in range(2):
+        model.train_step(data)
+    torch.cuda.synchronize()
+    log(f"[bench] eager warm-up ok, loss={float(model.scalars[0]):.4f} gnorm={float(model.scalars[3]):.4f}")
+
+    step = lambda: model.train_step(data)  # noqa: E731
+    if args.graph:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        if world == 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                model.train_step(data)
+            step = g.replay
+        else:
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            model.grad_allreduce = None
+            model.npos_allreduce = None
+            with torch.cuda.graph(g1):
+                model.forward_backward(data)
+            with torch.cuda.graph(g2):
+                model.apply_gradients()
+
+            def step():
+                g1.replay()
+                dist.all_reduce(model.P.g)
+                g2.replay()
+        torch.cuda.synchronize()
+        log("[bench] graph captured")
+
+    for i in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([el], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    value = world * B * args.steps / el
+    loss = float(model.scalars[0])
+    gnorm = float(model.scalars[3])
+    log(f"[bench] {args.steps} steps in {el:.3f}s -> {value:.1f} img/s  loss={loss:.4f} gnorm={gnorm:.4f}")
+
+    roofline = None
+    kernels = None
+    if args.kernel_timing and rank == 0:
+        es = 2 if args.dtype == "bf16" else 4
+        if dist:
+            model.grad_allreduce = None
+        with KernelTimer(es) as kt:
+            model.train_step(data)
+        agg = kt.summary()
+        total_ms = sum(a[1] for a in agg.values())
+        top = sorted(agg.items(), key=lambda kv: -kv[1][1])
+        kernels = {k: {"calls": a[0], "ms": round(a[1], 4), "GBps": (round(a[2] / (a[1] * 1e6), 1) if a[3] and a[1] > 0 else None)}
+                   for k, a in top[:12]}
+        log(f"[bench] instrumented eager step: {total_ms:.2f} ms of kernel time")
+        for k, a in top[:12]:
+            log(f"   {k:28s} calls={a[0]:4d} ms={a[1]:8.3f} share={a[1] / total_ms * 100:5.1f}%"
+                + (f" {a[2] / (a[1] * 1e6):8.1f} GB/s" if a[3] else ""))
+        dom = next((kv for kv in top if kv[1][3]), None)
+        if dom is not None:
+            name, (calls, ms, byts, _) = dom
+            ach = byts / (ms * 1e6)
+            roofline = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "bytes_per_launch": round(byts / calls), "avg_launch_us": round(ms / calls * 1e3, 2)}
+
+    cpu = None
+    if args.cpu_baseline and rank == 0 and world == 1:
+        log("[bench] cpu baseline (oracle, fp32) ...")
+        cpu = cpu_baseline(model)
+        log(f"[bench] cpu baseline {cpu['value']:.3f} img/s on {cpu['cores']} threads")
+
+    if rank == 0:
+        out = {
+            "metric": "EfficientDet-D0 bf16 train-step images/sec",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic",
+            "config": {"workload": f"{args.model} full train step 512x512, B={B}/GPU, focal+Huber loss, SGD+EMA",
+                       "model": args.model, "global_batch": B * world, "image_size": S,
+                       "parallelism": f"dp{world}", "graph": bool(args.graph)},
+            "loss": round(loss, 5),
+            "gnorm": round(gnorm, 5),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernels": kernels,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,244 @@
+/*
+ * edet.h — C-ABI of libedet.so, the MI355X (gfx950) kernels behind the EfficientDet
+ * call()/train_step() hot path of tfwcn/tensorflow2-machine-vision.
+ *
+ * Boundary rules
+ *   - plain pointers, sizes and POD descriptors only; no torch / HIP C++ types;
+ *   - every entry point returns 0 on success or a negative EDET_E* code, and
+ *     edet_last_error() returns a thread-local message describing the last failure;
+ *   - the library never allocates or frees device memory: every buffer (activations,
+ *     fp32 statistic / gradient accumulators, workspaces) is caller-owned;
+ *   - every kernel is enqueued on the caller's HIP stream (`stream`, a hipStream_t
+ *     passed as void*), is graph-capturable (no allocation, no host sync) and is
+ *     re-entrant (no mutable global state);
+ *   - activations are NHWC, row-major [rows][ld] with rows = batch*H*W;
+ *     `dtype` selects the storage type: EDET_F32 or EDET_BF16; accumulation is fp32;
+ *   - *_accumulate* outputs: 0 = overwrite, 1 = add into the existing contents;
+ *     weight-gradient and statistic outputs are fp32 and always accumulated
+ *     (atomics) into caller-zeroed buffers.
+ *
+ * Reference interfaces each group replaces (paths relative to
+ * AIServer/ai_api/ai_models/ of the reference):
+ *   stem            layers/stem.py:37-38            (Conv2D 3x3 s2 SAME + BN + swish)
+ *   conv1x1         layers/mb_conv_block.py:143-154 (expand / project Conv2D 1x1),
+ *                   layers/resample_feature_map.py:24-27, layers/bifpn.py:16-21,
+ *                   layers/class_net.py:54-76, layers/box_net.py:49-78 (pointwise halves)
+ *   dwconv          layers/mb_conv_block.py:85-91,147 (DepthwiseConv2D k3/k5 s1/s2 SAME),
+ *                   SeparableConv2D depthwise halves (bifpn.py:16, class_net.py:46, box_net.py:52)
+ *   lazy BN/act     every BatchNormalization(training=True) + tf.nn.swish;
+ *                   the normalisation is applied in the consumer's load path
+ *   se              layers/se.py:35-39
+ *   maxpool/fuse    layers/resample_feature_map.py:35-51, layers/bifpn.py:59-66
+ *   residual        layers/class_net.py:93-96, layers/box_net.py:93-95 + utils/drop_connect.py:4-18
+ *   loss            losses/focal_loss.py:26-52, losses/box_loss.py:21-30,
+ *                   efficientnet/efficientdet_net_train.py:41-52
+ *   optimizer       efficientdet_net_train.py:21-28,129-131, efficientnet/train.py:35-63,114-120
+ *   anchors         efficientnet/utils/anchors.py:47-84 (_generate_boxes), :91-138
+ *                   (generate_targets + iou.py:27-69), :245-274 (_boxes_decoder)
+ */
+#ifndef EDET_H_
+#define EDET_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* edet_stream_t; /* hipStream_t */
+
+enum { EDET_F32 = 0, EDET_BF16 = 1 };
+enum { EDET_ACT_NONE = 0, EDET_ACT_SWISH = 1 };
+enum { EDET_MODE_SAME = 0, EDET_MODE_UPSAMPLE = 1, EDET_MODE_MAXPOOL = 2 };
+enum { EDET_OK = 0, EDET_EINVAL = -1, EDET_EUNSUPPORTED = -2, EDET_EHIP = -3 };
+
+#define EDET_MAX_SEG 5
+
+/* Row layout of a (possibly multi-level) NHWC activation buffer.  Segment s holds
+ * batch*H[s]*W[s] rows starting at row_off[s] (a multiple of 128).  A plain tensor
+ * is one segment at offset 0.  The feature pyramid P3..P7 is five segments. */
+typedef struct edet_pyramid {
+  int32_t nseg;
+  int32_t batch;
+  int32_t row_off[EDET_MAX_SEG];
+  int32_t H[EDET_MAX_SEG];
+  int32_t W[EDET_MAX_SEG];
+} edet_pyramid;
+
+/* Training-mode batch normalisation of a raw tensor (per segment). sum/sq are the fp32
+ * per-channel sums of x and x^2 over the segment's rows, produced by the tensor's
+ * producer kernel.  y = (x - mean) * rsqrt(var + eps) * gamma + beta, var biased. */
+typedef struct edet_bn {
+  const float* sum[EDET_MAX_SEG];
+  const float* sq[EDET_MAX_SEG];
+  const float* gamma[EDET_MAX_SEG];
+  const float* beta[EDET_MAX_SEG];
+  float eps;
+  int32_t enabled;
+} edet_bn;
+
+/* A value that is stored raw and materialised on load:
+ *   v = act(bn(x)) * gate[image][c]        (bn / act / gate each optional) */
+typedef struct edet_lazy {
+  const void* x;        /* raw [rows][ld] in `dtype` */
+  const float* gate;    /* [batch][C] SE gate or NULL */
+  edet_bn bn;
+  int32_t ld;
+  int32_t act;
+} edet_lazy;
+
+/* per-segment fp32 outputs (statistics: sum / sum of squares, or BN gamma/beta grads) */
+typedef struct edet_segout {
+  float* a[EDET_MAX_SEG];
+  float* b[EDET_MAX_SEG];
+} edet_segout;
+
+typedef struct edet_fuse_input {
+  edet_lazy v;          /* input value (lazy BN of a resampled conv, or a node output) */
+  void* dx;             /* backward: gradient w.r.t. the input value (same layout) */
+  int32_t H, W;         /* input spatial size */
+  int32_t mode;         /* EDET_MODE_* : same / nearest upsample / maxpool 3x3 s2 SAME */
+  int32_t accumulate;   /* backward: accumulate into dx */
+} edet_fuse_input;
+
+typedef struct edet_sched {
+  float adjusted_lr, warmup_init;
+  int32_t warmup_steps, total_steps;
+  float momentum, ema_decay, clip_norm, l2_weight;
+  float fixed_lr;       /* >0: constant learning rate instead of the cosine schedule */
+  int32_t pad;
+} edet_sched;
+
+/* ---- library ---- */
+const char* edet_last_error(void);
+int edet_abi_version(void);
+int edet_memset_async(void* p, int value, size_t bytes, edet_stream_t stream);
+int edet_memcpy_async(void* dst, const void* src, size_t bytes, edet_stream_t stream);
+
+/* ---- pointwise (1x1) convolution: y[m][n] = sum_k v(a)[m][k] * wt[n][k] + bias[n] ----
+ * wt is [N][K] in `dtype`.  `stats` (nullable) receives per-segment column sums of y. */
+int edet_conv1x1_fwd(int dtype, const edet_lazy* a, const edet_pyramid* rows, int K,
+                     const void* wt, int N, const float* bias, void* y, int ldy,
+                     int accumulate, const edet_segout* stats, edet_stream_t stream);
+/* dx[m][k] = sum_n dy[m][n] * wt[n][k] */
+int edet_conv1x1_dgrad(int dtype, const void* dy, int lddy, const edet_pyramid* rows, int N,
+                       const void* wt, int K, void* dx, int lddx, int accumulate,
+                       edet_stream_t stream);
+/* dwt[n][k] += sum_m dy[m][n] * v(a)[m][k];  dbias[n] += sum_m dy[m][n]  (valid rows only) */
+int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, int K,
+                       const void* dy, int lddy, int N, float* dwt, float* dbias,
+                       edet_stream_t stream);
+
+/* ---- depthwise k x k, stride s, TF 'SAME' padding; w is [k*k][C] in `dtype` ---- */
+int edet_dwconv_fwd(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
+                    int stride, const void* w, void* y, const edet_pyramid* pout,
+                    const edet_segout* stats, edet_stream_t stream);
+int edet_dwconv_dgrad(int dtype, const void* dy, const edet_pyramid* pout, int C, int k,
+                      int stride, const void* w, void* dx, const edet_pyramid* pin,
+                      int accumulate, edet_stream_t stream);
+int edet_dwconv_wgrad(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
+                      int stride, const void* dy, const edet_pyramid* pout, float* dw,
+                      edet_stream_t stream);
+
+/* ---- stem: 3x3 s2 SAME, Cin = 3, no bias; w is [3][3][3][Cout] in `dtype` ---- */
+int edet_stem_fwd(int dtype, const void* x, int B, int H, int W, const void* w, int Cout,
+                  void* y, float* sum, float* sq, edet_stream_t stream);
+int edet_stem_wgrad(int dtype, const void* x, int B, int H, int W, const void* dy, int Cout,
+                    float* dw, edet_stream_t stream);
+
+/* ---- lazy-value backward: dx = d v / d x  (BN training backward, swish', SE gate) ----
+ * dv_scale [nseg][batch] (nullable) multiplies dv per image (drop-connect);
+ * dsq [batch][C] (nullable) is added to d(pre-gate value) (SE squeeze path, already / HW).
+ * reduce: grads->a[s] += sum du * xhat (dgamma), grads->b[s] += sum du (dbeta)
+ * apply : dx = scale * (du - dbeta/M - xhat * dgamma/M)   (or du when BN is off) */
+int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, int C,
+                         const void* dv, const float* dv_scale, const float* dsq,
+                         const edet_segout* grads, edet_stream_t stream);
+int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, int C,
+                        const void* dv, const float* dv_scale, const float* dsq,
+                        const edet_segout* grads, void* dx, int accumulate,
+                        edet_stream_t stream);
+
+/* ---- squeeze-excitation ---- */
+int edet_se_squeeze(int dtype, const edet_lazy* x, int B, int HW, int C, float* s,
+                    edet_stream_t stream);            /* s += mean_hw v(x)  (zeroed s) */
+int edet_se_fwd(int B, int C, int R, const float* s, const float* w1, const float* b1,
+                const float* w2, const float* b2, float* z1, float* gate, edet_stream_t stream);
+int edet_gate_grad(int dtype, const edet_lazy* x, int B, int HW, int C, const void* dv,
+                   float* dgate, edet_stream_t stream); /* dgate += sum_hw dv * v(x) */
+int edet_se_bwd(int B, int C, int R, int HW, const float* s, const float* z1,
+                const float* gate, const float* dgate, const float* w1, const float* w2,
+                float* dw1, float* db1, float* dw2, float* db2, float* dsq,
+                edet_stream_t stream);
+
+/* ---- heads: out = v(x) * scale[seg][n] + v(res) (drop-connect + residual) ---- */
+int edet_residual_fwd(int dtype, const edet_lazy* x, const edet_lazy* res,
+                      const edet_pyramid* p, int C, const float* scale, void* out,
+                      edet_stream_t stream);
+
+/* ---- resampling & BiFPN weighted fusion ---- */
+int edet_maxpool_fwd(int dtype, const edet_lazy* x, int B, int H, int W, int C, void* y,
+                     edet_stream_t stream);
+int edet_maxpool_bwd(int dtype, const edet_lazy* x, int B, int H, int W, int C,
+                     const void* dy, void* dx, int accumulate, edet_stream_t stream);
+int edet_bifpn_fuse_fwd(int dtype, int n_in, const edet_fuse_input* ins, const float* w,
+                        int B, int H, int W, int C, void* out, edet_stream_t stream);
+int edet_bifpn_fuse_bwd(int dtype, int n_in, const edet_fuse_input* ins, const float* w,
+                        int B, int H, int W, int C, const void* out, const void* dout,
+                        float* dw, edet_stream_t stream);
+
+/* ---- detection loss (focal + Huber), forward and backward in one pass ----
+ * cls: [rows][ldc] logits (A*NC used), box: [rows][ldb] (A*4 used).
+ * cls_t [rows][A] class index, box_t [rows][A][4], npos_sum = sum of positive masks
+ * (the kernel adds the reference's +1).  loss += sum_l (box_weight*box_l + focal_l).
+ * focal_count_scale multiplies the per-level element count of the focal mean (data-parallel
+ * replicas pass the world size so the summed replica gradients equal the global-batch ones).
+ * dcls may alias cls and dbox may alias box (each element is read before it is written).
+ * dcls/dbox (nullable) receive d loss / d logits (pad columns written as 0). */
+int edet_detection_loss(int dtype, const void* cls, int ldc, const void* box, int ldb,
+                        const edet_pyramid* p, int A, int NC, const int32_t* cls_t,
+                        const float* box_t, const float* npos_sum, float alpha, float gamma,
+                        float delta, float box_weight, float focal_count_scale, void* dcls,
+                        void* dbox, float* loss, float* level_parts, edet_stream_t stream);
+int edet_count_positives(const uint8_t* mask, int64_t n, float* out, edet_stream_t stream);
+int edet_onehot_to_index(const float* onehot, int64_t n, int NC, int32_t* out,
+                         edet_stream_t stream);
+
+/* ---- anchors / targets / decode (bit-exact fp32 index work) ---- */
+int edet_anchor_boxes(int fh, int fw, float start_y, float delta_y, float start_x,
+                      float delta_x, int A, const float* half_yx, float* out,
+                      edet_stream_t stream);
+int edet_generate_targets(const float* anchors, const edet_pyramid* p, int A,
+                          const float* gt, const int32_t* gt_cls, const int32_t* n_gt,
+                          int max_gt, float iou_thr, float* box_t, int32_t* cls_t,
+                          uint8_t* mask, edet_stream_t stream);
+int edet_decode_boxes(int dtype, const float* anchors, const edet_pyramid* p, int A,
+                      const void* rel, int ld, float* out, edet_stream_t stream);
+
+/* ---- optimizer: L2 + clip_by_global_norm + SGD momentum + EMA, fused ----
+ * scalars: [0] loss  [1] sum g^2  [2] sum w^2 (L2 params)  [3] gnorm  [4] lr  [5] npos
+ * step: device int32 step counter (incremented by edet_opt_apply). */
+/* norm pass: scalars[1] += sum (g + l2*w)^2, scalars[2] += sum_{i<n_l2} w^2; block 0 also
+ * writes scalars[4] = lr(step) and increments *step. */
+int edet_opt_norm(const float* w, const float* g, int64_t n, int64_t n_l2,
+                  const edet_sched* sched, float* scalars, int32_t* step,
+                  edet_stream_t stream);
+/* apply pass: clip, SGD momentum, EMA; writes the `dtype` compute copy of w (nullable),
+ * scalars[3] = gnorm (pre-clip), scalars[0] += l2 * sum w^2 / 2. */
+int edet_opt_apply(float* w, const float* g, float* v, float* ema, int64_t n, int64_t n_l2,
+                   const edet_sched* sched, float* scalars, int dtype, void* wcompute,
+                   edet_stream_t stream);
+int edet_cast_f32(int dtype, const float* src, void* dst, int64_t n, edet_stream_t stream);
+/* inference-mode BN: express moving mean/var as the sums the lazy loaders expect */
+int edet_bn_inference_stats(int64_t n, const float* mmean, const float* mvar, const float* count,
+                            float* sum, float* sq, edet_stream_t stream);
+int edet_bn_update_moving(int64_t n, const float* sum, const float* sq, const float* count,
+                          float momentum, float* mmean, float* mvar, edet_stream_t stream);
+int edet_dropmask(float* out, int n, float survival, uint64_t seed, const int32_t* step,
+                  edet_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EDET_H_ */

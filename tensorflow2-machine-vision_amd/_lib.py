@@ -1,0 +1,140 @@
+"""ctypes binding of libedet.so (the C-ABI declared in include/edet.h).
+
+This is the only module that touches the shared library.  Every entry point returns an int
+status; non-zero raises ``EdetError`` carrying ``edet_last_error()``.  There is no fallback:
+if the library is missing the import of the package's compute modules fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
+
+MAX_SEG = 5
+F32, BF16 = 0, 1
+ACT_NONE, ACT_SWISH = 0, 1
+MODE_SAME, MODE_UPSAMPLE, MODE_MAXPOOL = 0, 1, 2
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("EDET_LIB", os.path.join(_PKG_DIR, "lib", "libedet.so"))
+
+
+class EdetError(RuntimeError):
+    pass
+
+
+class Pyramid(ctypes.Structure):
+    _fields_ = [("nseg", c_int32), ("batch", c_int32), ("row_off", c_int32 * MAX_SEG),
+                ("H", c_int32 * MAX_SEG), ("W", c_int32 * MAX_SEG)]
+
+
+class BN(ctypes.Structure):
+    _fields_ = [("sum", c_void_p * MAX_SEG), ("sq", c_void_p * MAX_SEG),
+                ("gamma", c_void_p * MAX_SEG), ("beta", c_void_p * MAX_SEG),
+                ("eps", c_float), ("enabled", c_int32)]
+
+
+class Lazy(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("gate", c_void_p), ("bn", BN), ("ld", c_int32), ("act", c_int32)]
+
+
+class SegOut(ctypes.Structure):
+    _fields_ = [("a", c_void_p * MAX_SEG), ("b", c_void_p * MAX_SEG)]
+
+
+class FuseInput(ctypes.Structure):
+    _fields_ = [("v", Lazy), ("dx", c_void_p), ("H", c_int32), ("W", c_int32),
+                ("mode", c_int32), ("accumulate", c_int32)]
+
+
+class Sched(ctypes.Structure):
+    _fields_ = [("adjusted_lr", c_float), ("warmup_init", c_float), ("warmup_steps", c_int32),
+                ("total_steps", c_int32), ("momentum", c_float), ("ema_decay", c_float),
+                ("clip_norm", c_float), ("l2_weight", c_float), ("fixed_lr", c_float),
+                ("pad", c_int32)]
+
+
+P = c_void_p
+PPyr, PLazy, PSeg, PFuse, PSched = (POINTER(Pyramid), POINTER(Lazy), POINTER(SegOut),
+                                    POINTER(FuseInput), POINTER(Sched))
+
+# name -> argtypes (all return int unless listed in _RESTYPE)
+SIGNATURES = {
+    "edet_last_error": [],
+    "edet_abi_version": [],
+    "edet_memset_async": [P, c_int, c_size_t, P],
+    "edet_memcpy_async": [P, P, c_size_t, P],
+    "edet_conv1x1_fwd": [c_int, PLazy, PPyr, c_int, P, c_int, P, P, c_int, c_int, PSeg, P],
+    "edet_conv1x1_dgrad": [c_int, P, c_int, PPyr, c_int, P, c_int, P, c_int, c_int, P],
+    "edet_conv1x1_wgrad": [c_int, PLazy, PPyr, c_int, P, c_int, c_int, P, P, P],
+    "edet_dwconv_fwd": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, P, PPyr, PSeg, P],
+    "edet_dwconv_dgrad": [c_int, P, PPyr, c_int, c_int, c_int, P, P, PPyr, c_int, P],
+    "edet_dwconv_wgrad": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, PPyr, P, P],
+    "edet_stem_fwd": [c_int, P, c_int, c_int, c_int, P, c_int, P, P, P, P],
+    "edet_stem_wgrad": [c_int, P, c_int, c_int, c_int, P, c_int, P, P],
+    "edet_lazy_bwd_reduce": [c_int, PLazy, PPyr, c_int, P, P, P, PSeg, P],
+    "edet_lazy_bwd_apply": [c_int, PLazy, PPyr, c_int, P, P, P, PSeg, P, c_int, P],
+    "edet_se_squeeze": [c_int, PLazy, c_int, c_int, c_int, P, P],
+    "edet_se_fwd": [c_int, c_int, c_int, P, P, P, P, P, P, P, P],
+    "edet_gate_grad": [c_int, PLazy, c_int, c_int, c_int, P, P, P],
+    "edet_se_bwd": [c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P],
+    "edet_residual_fwd": [c_int, PLazy, PLazy, PPyr, c_int, P, P, P],
+    "edet_maxpool_fwd": [c_int, PLazy, c_int, c_int, c_int, c_int, P, P],
+    "edet_maxpool_bwd": [c_int, PLazy, c_int, c_int, c_int, c_int, P, P, c_int, P],
+    "edet_bifpn_fuse_fwd": [c_int, c_int, PFuse, P, c_int, c_int, c_int, c_int, P, P],
+    "edet_bifpn_fuse_bwd": [c_int, c_int, PFuse, P, c_int, c_int, c_int, c_int, P, P, P, P],
+    "edet_detection_loss": [c_int, P, c_int, P, c_int, PPyr, c_int, c_int, P, P, P, c_float,
+                            c_float, c_float, c_float, c_float, P, P, P, P, P],
+    "edet_count_positives": [P, c_int64, P, P],
+    "edet_onehot_to_index": [P, c_int64, c_int, P, P],
+    "edet_anchor_boxes": [c_int, c_int, c_float, c_float, c_float, c_float, c_int, P, P, P],
+    "edet_generate_targets": [P, PPyr, c_int, P, P, P, c_int, c_float, P, P, P, P],
+    "edet_decode_boxes": [c_int, P, PPyr, c_int, P, c_int, P, P],
+    "edet_opt_norm": [P, P, c_int64, c_int64, PSched, P, P, P],
+    "edet_opt_apply": [P, P, P, P, c_int64, c_int64, PSched, P, c_int, P, P],
+    "edet_cast_f32": [c_int, P, P, c_int64, P],
+    "edet_bn_inference_stats": [c_int64, P, P, P, P, P, P],
+    "edet_bn_update_moving": [c_int64, P, P, P, c_float, P, P, P],
+    "edet_dropmask": [P, c_int, c_float, c_uint64, P, P],
+}
+_RESTYPE = {"edet_last_error": c_char_p}
+
+
+class _Lib:
+    def __init__(self, path: str):
+        if not os.path.exists(path):
+            raise ImportError(
+                f"libedet.so not found at {path}: build it with `make -C "
+                f"tensorflow2-machine-vision_amd` (or __graft_entry__.build()). There is no "
+                f"CPU fallback for the EfficientDet hot path.")
+        self.path = path
+        self.dll = ctypes.CDLL(path)
+        self.fns = {}
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(self.dll, name)
+            fn.argtypes = argtypes
+            fn.restype = _RESTYPE.get(name, c_int)
+            self.fns[name] = fn
+
+    def last_error(self) -> str:
+        return self.fns["edet_last_error"]().decode(errors="replace")
+
+    def call(self, name: str, *args):
+        rc = self.fns[name](*args)
+        if rc != 0:
+            raise EdetError(f"{name} failed ({rc}): {self.last_error()}")
+        return rc
+
+
+_LIB: _Lib | None = None
+
+
+def lib() -> _Lib:
+    global _LIB
+    if _LIB is None:
+        _LIB = _Lib(LIB_PATH)
+    return _LIB
+
+
+def call(name: str, *args):
+    return lib().call(name, *args)

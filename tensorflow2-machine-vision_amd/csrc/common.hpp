@@ -1,0 +1,198 @@
+// Shared device helpers for libedet (gfx950 / CDNA4).
+//
+// Storage types: float (EDET_F32) or bf16 held as uint16_t (EDET_BF16). All arithmetic is
+// fp32. Activations are NHWC rows ([rows][ld]); 8-element vectors are the unit of global
+// access (16 B for bf16, 32 B for fp32) so every row stride handed to a vector path must be
+// a multiple of 8 elements.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/edet.h"
+
+namespace edet {
+
+// ------------------------------------------------------------------ error reporting
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+#define EDET_REQUIRE(cond, ...)            \
+  do {                                     \
+    if (!(cond)) {                         \
+      ::edet::set_error(__VA_ARGS__);      \
+      return EDET_EINVAL;                  \
+    }                                      \
+  } while (0)
+
+// ------------------------------------------------------------------ vector types
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef uint16_t bf16_t;
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;  // v_cvt_pk_bf16_f32: RNE, NaN-preserving
+  return __builtin_bit_cast(uint16_t, h);
+}
+
+template <typename T> __device__ __forceinline__ float to_f(T v);
+template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f<uint16_t>(uint16_t v) { return bf2f(v); }
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ uint16_t from_f<uint16_t>(float v) { return f2bf(v); }
+
+// 8 contiguous elements -> fp32 (pointer 16-B aligned)
+__device__ __forceinline__ void ld8(const float* p, float* o) {
+  float4 a = *reinterpret_cast<const float4*>(p);
+  float4 b = *reinterpret_cast<const float4*>(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+__device__ __forceinline__ void ld8(const uint16_t* p, float* o) {
+  uint4 v = *reinterpret_cast<const uint4*>(p);
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(w[i] << 16);
+    o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void st8(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void st8(uint16_t* p, const float* v) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+// masked variants: elements [0, n) valid, others read as 0 / not written
+template <typename T>
+__device__ __forceinline__ void ld8m(const T* p, int n, float* o) {
+  if (n >= 8) { ld8(p, o); return; }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (i < n) ? to_f<T>(p[i]) : 0.f;
+}
+template <typename T>
+__device__ __forceinline__ void st8m(T* p, int n, const float* v) {
+  if (n >= 8) { st8(p, v); return; }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (i < n) p[i] = from_f<T>(v[i]);
+}
+// read-modify-write accumulate of 8 elements
+template <typename T>
+__device__ __forceinline__ void acc8m(T* p, int n, const float* v, int accumulate) {
+  float o[8];
+  if (accumulate) {
+    ld8m(p, n, o);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] += v[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = v[i];
+  }
+  st8m(p, n, o);
+}
+
+// ------------------------------------------------------------------ math
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float swishf_(float x) { return x * sigmoidf_(x); }
+__device__ __forceinline__ float dswishf_(float x) {
+  float s = sigmoidf_(x);
+  return s * (1.f + x * (1.f - s));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
+// floor division for possibly negative numerators (b > 0)
+__device__ __forceinline__ int fdiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
+// TF 'SAME' padding: returns pad_before; out = ceil(in / s)
+__host__ __device__ __forceinline__ int same_pad(int in, int k, int s) {
+  int out = (in + s - 1) / s;
+  int tot = (out - 1) * s + k - in;
+  if (tot < 0) tot = 0;
+  return tot / 2;
+}
+
+// ------------------------------------------------------------------ pyramid helpers
+__host__ __device__ __forceinline__ int seg_rows(const edet_pyramid& p, int s) {
+  return p.batch * p.H[s] * p.W[s];
+}
+__host__ __device__ __forceinline__ int seg_of_row(const edet_pyramid& p, int row) {
+  int s = 0;
+  for (int i = 1; i < p.nseg; ++i)
+    if (row >= p.row_off[i]) s = i;
+  return s;
+}
+__host__ __device__ __forceinline__ int pyr_total_rows(const edet_pyramid& p) {
+  return p.row_off[p.nseg - 1] + seg_rows(p, p.nseg - 1);
+}
+
+// Per-channel affine of the lazy BN for segment `seg`: v = x * sc + sh.
+__device__ __forceinline__ float2 bn_affine(const edet_bn& bn, int seg, int c, float inv_count) {
+  if (!bn.enabled) return make_float2(1.f, 0.f);
+  float mean = bn.sum[seg][c] * inv_count;
+  float var = fmaxf(bn.sq[seg][c] * inv_count - mean * mean, 0.f);
+  float r = rsqrtf(var + bn.eps);
+  float sc = bn.gamma[seg][c] * r;
+  return make_float2(sc, bn.beta[seg][c] - mean * sc);
+}
+// mean / rstd (for x-hat in backward)
+__device__ __forceinline__ float2 bn_mean_rstd(const edet_bn& bn, int seg, int c, float inv_count) {
+  float mean = bn.sum[seg][c] * inv_count;
+  float var = fmaxf(bn.sq[seg][c] * inv_count - mean * mean, 0.f);
+  return make_float2(mean, rsqrtf(var + bn.eps));
+}
+
+__device__ __forceinline__ float lazy_apply(float x, float2 af, int act) {
+  float v = x * af.x + af.y;
+  return act ? swishf_(v) : v;
+}
+
+// Bijective XCD-aware block remap: blocks b and b+8 share an XCD (round-robin dispatch),
+// so give each XCD a contiguous range of logical tile ids.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  if (nwg < 16) return bid;
+  int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+// Segment-chunked row iteration: each segment is split into chunks of CH rows so a chunk
+// never straddles segments.  Returns (seg, chunk-in-seg) for a linear chunk id.
+__host__ __device__ __forceinline__ int total_chunks(const edet_pyramid& p, int CH) {
+  int t = 0;
+  for (int s = 0; s < p.nseg; ++s) t += cdiv(seg_rows(p, s), CH);
+  return t;
+}
+__device__ __forceinline__ void chunk_lookup(const edet_pyramid& p, int CH, int id, int& seg, int& chunk) {
+  for (int s = 0; s < p.nseg; ++s) {
+    int n = cdiv(seg_rows(p, s), CH);
+    if (id < n) { seg = s; chunk = id; return; }
+    id -= n;
+  }
+  seg = p.nseg - 1; chunk = id;  // unreachable with a correct grid
+}
+
+}  // namespace edet
+
+#define EDET_DTYPE_DISPATCH(dtype, T, ...)                 \
+  do {                                                     \
+    if ((dtype) == EDET_F32) {                             \
+      using T = float;                                     \
+      __VA_ARGS__;                                         \
+    } else if ((dtype) == EDET_BF16) {                     \
+      using T = uint16_t;                                  \
+      __VA_ARGS__;                                         \
+    } else {                                               \
+      ::edet::set_error("unsupported dtype %d", (dtype));  \
+      return EDET_EUNSUPPORTED;                            \
+    }                                                      \
+  } while (0)

@@ -1,0 +1,398 @@
+// Depthwise k x k convolution, stride 1/2, TF 'SAME' padding (pad_before = floor(total/2),
+// the extra row/column at the bottom/right), NHWC, over single tensors or the P3..P7 pyramid.
+//
+// Replaces DepthwiseConv2D in layers/mb_conv_block.py:85-91,147 and the depthwise half of
+// SeparableConv2D in layers/bifpn.py:16-21, layers/class_net.py:46-76, layers/box_net.py:49-78.
+//
+// Work unit: one workgroup = one image x one 8x8 output tile x 32 channels.  The input halo
+// tile ((8-1)*s + k)^2 x 32 is staged once into LDS as fp32 with the lazy BN/swish/SE-gate
+// transform of the producer applied on the way in (zero outside the image, i.e. the padding
+// is applied to the *transformed* value exactly as the reference pads the layer input).
+// Thread (c, r) then produces the 8 outputs of row r for channel c.  The epilogue reduces the
+// per-channel BN statistics of the output.
+#include "common.hpp"
+
+namespace edet {
+
+constexpr int DTS = 8;   // spatial tile
+constexpr int DCB = 32;  // channels per block
+
+struct DwArgs {
+  const void* x;
+  const void* w;
+  void* y;
+  const void* dy;
+  void* dx;
+  float* dw;
+  edet_lazy lz;
+  edet_pyramid pin, pout;
+  edet_segout stats;
+  int C, ncb, accumulate, has_stats;
+  int tiles_per_wg, tiles_total;
+};
+
+// tiles over a pyramid's spatial extent (per channel block)
+__device__ __forceinline__ void locate_tile(const edet_pyramid& p, int id, int& seg, int& n, int& ty, int& tx) {
+  seg = 0;
+  for (; seg < p.nseg - 1; ++seg) {
+    const int cnt = p.batch * cdiv(p.H[seg], DTS) * cdiv(p.W[seg], DTS);
+    if (id < cnt) break;
+    id -= cnt;
+  }
+  const int ntx = cdiv(p.W[seg], DTS), nty = cdiv(p.H[seg], DTS);
+  tx = id % ntx; id /= ntx;
+  ty = id % nty;
+  n = id / nty;
+}
+static int host_tiles(const edet_pyramid& p) {
+  int t = 0;
+  for (int s = 0; s < p.nseg; ++s) t += p.batch * cdiv(p.H[s], DTS) * cdiv(p.W[s], DTS);
+  return t;
+}
+
+// Stage the transformed input halo of one tile into LDS (fp32, [IH][IW][DCB]).
+template <typename T, int IH, int IW>
+__device__ __forceinline__ void stage_input(const DwArgs& g, float* tile, const float2* xf, const float* gt,
+                                            int seg, int n, int iy0, int ix0, int c0) {
+  const int H = g.pin.H[seg], W = g.pin.W[seg], C = g.C;
+  const T* X = (const T*)g.x;
+  const size_t base = (size_t)g.pin.row_off[seg] + (size_t)n * H * W;
+  for (int v = threadIdx.x; v < IH * IW * (DCB / 8); v += 256) {
+    const int pix = v >> 2, cv = (v & 3) * 8;
+    const int yy = pix / IW, xx = pix - yy * IW;
+    const int gy = iy0 + yy, gx = ix0 + xx, nc = C - (c0 + cv);
+    float vals[8];
+    if (gy >= 0 && gy < H && gx >= 0 && gx < W && nc > 0) {
+      ld8m(X + (base + (size_t)gy * W + gx) * g.lz.ld + c0 + cv, nc, vals);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vals[j] = (j < nc) ? lazy_apply(vals[j], xf[cv + j], g.lz.act) * gt[cv + j] : 0.f;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vals[j] = 0.f;
+    }
+    float* d = tile + pix * DCB + cv;
+    reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
+    reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+  }
+}
+
+__device__ __forceinline__ void prep_xf(const DwArgs& g, float2* xf, float* gt, int seg, int n, int c0) {
+  const int tid = threadIdx.x;
+  if (tid < DCB) {
+    const int cc = c0 + tid;
+    float2 af = make_float2(1.f, 0.f);
+    float gv = 1.f;
+    if (cc < g.C) {
+      af = bn_affine(g.lz.bn, seg, cc, 1.f / (float)seg_rows(g.pin, seg));
+      if (g.lz.gate) gv = g.lz.gate[(size_t)n * g.C + cc];
+    }
+    xf[tid] = af;
+    gt[tid] = gv;
+  }
+}
+
+template <typename T, int K, int S>
+__global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
+  constexpr int IH = (DTS - 1) * S + K, IW = IH;
+  __shared__ __attribute__((aligned(16))) float tile[IH * IW * DCB];
+  __shared__ float2 xf[DCB];
+  __shared__ float gt[DCB];
+  __shared__ float red[2][8][DCB];
+  const int tid = threadIdx.x, c = tid & 31, r = tid >> 5;
+
+  int id = blockIdx.x;
+  const int cb = id % g.ncb;
+  id /= g.ncb;
+  int seg, n, ty, tx;
+  locate_tile(g.pout, id, seg, n, ty, tx);
+  const int OH = g.pout.H[seg], OW = g.pout.W[seg], H = g.pin.H[seg], W = g.pin.W[seg];
+  const int c0 = cb * DCB;
+  const int pt = same_pad(H, K, S), pl = same_pad(W, K, S);
+  const int oy0 = ty * DTS, ox0 = tx * DTS;
+
+  prep_xf(g, xf, gt, seg, n, c0);
+  __syncthreads();
+  stage_input<T, IH, IW>(g, tile, xf, gt, seg, n, oy0 * S - pt, ox0 * S - pl, c0);
+
+  float wr[K * K];
+  const T* Wp = (const T*)g.w;
+  const bool cvalid = (c0 + c) < g.C;
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(Wp[(size_t)i * g.C + c0 + c]) : 0.f;
+  __syncthreads();
+
+  float acc[DTS];
+#pragma unroll
+  for (int j = 0; j < DTS; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+    for (int kw = 0; kw < K; ++kw) {
+      const float wv = wr[kh * K + kw];
+      const float* trow = tile + ((r * S + kh) * IW + kw) * DCB + c;
+#pragma unroll
+      for (int j = 0; j < DTS; ++j) acc[j] += trow[j * S * DCB] * wv;
+    }
+
+  const int oy = oy0 + r;
+  T* Y = (T*)g.y;
+  const size_t obase = (size_t)g.pout.row_off[seg] + (size_t)n * OH * OW;
+  float s = 0.f, q = 0.f;
+  if (oy < OH && cvalid) {
+#pragma unroll
+    for (int j = 0; j < DTS; ++j) {
+      const int ox = ox0 + j;
+      if (ox < OW) {
+        Y[(obase + (size_t)oy * OW + ox) * g.C + c0 + c] = from_f<T>(acc[j]);
+        s += acc[j];
+        q += acc[j] * acc[j];
+      }
+    }
+  }
+  if (g.has_stats) {
+    red[0][r][c] = s;
+    red[1][r][c] = q;
+    __syncthreads();
+    if (tid < DCB && c0 + tid < g.C) {
+      float ss = 0.f, qq = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
+      atomicAdd(g.stats.a[seg] + c0 + tid, ss);
+      atomicAdd(g.stats.b[seg] + c0 + tid, qq);
+    }
+  }
+}
+
+// dx[n][iy][ix][c] = sum_{kh,kw} dy[n][oy][ox][c] * w[kh][kw][c],  iy = oy*s - pt + kh
+template <typename T, int K, int S>
+__global__ __launch_bounds__(256) void k_dw_dgrad(DwArgs g) {
+  constexpr int HR = (DTS - 1 + K - 1) / S + 2;
+  __shared__ __attribute__((aligned(16))) float tile[HR * HR * DCB];
+  const int tid = threadIdx.x, c = tid & 31, r = tid >> 5;
+
+  int id = blockIdx.x;
+  const int cb = id % g.ncb;
+  id /= g.ncb;
+  int seg, n, ty, tx;
+  locate_tile(g.pin, id, seg, n, ty, tx);
+  const int OH = g.pout.H[seg], OW = g.pout.W[seg], H = g.pin.H[seg], W = g.pin.W[seg];
+  const int c0 = cb * DCB;
+  const int pt = same_pad(H, K, S), pl = same_pad(W, K, S);
+  const int iy0 = ty * DTS, ix0 = tx * DTS;
+  const int oy_lo = fdiv(iy0 + pt - (K - 1) + S - 1, S);
+  const int ox_lo = fdiv(ix0 + pl - (K - 1) + S - 1, S);
+
+  const T* DY = (const T*)g.dy;
+  const size_t obase = (size_t)g.pout.row_off[seg] + (size_t)n * OH * OW;
+  for (int v = tid; v < HR * HR * (DCB / 8); v += 256) {
+    const int pix = v >> 2, cv = (v & 3) * 8;
+    const int yy = pix / HR, xx = pix - yy * HR;
+    const int oy = oy_lo + yy, ox = ox_lo + xx, nc = g.C - (c0 + cv);
+    float vals[8];
+    if (oy >= 0 && oy < OH && ox >= 0 && ox < OW && nc > 0) ld8m(DY + (obase + (size_t)oy * OW + ox) * g.C + c0 + cv, nc, vals);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vals[j] = 0.f;
+    }
+    float* d = tile + pix * DCB + cv;
+    reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
+    reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+  }
+  float wr[K * K];
+  const T* Wp = (const T*)g.w;
+  const bool cvalid = (c0 + c) < g.C;
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(Wp[(size_t)i * g.C + c0 + c]) : 0.f;
+  __syncthreads();
+
+  const int iy = iy0 + r;
+  float acc[DTS];
+#pragma unroll
+  for (int j = 0; j < DTS; ++j) acc[j] = 0.f;
+#pragma unroll
+  for (int kh = 0; kh < K; ++kh) {
+    const int t = iy + pt - kh;
+    if (t < 0 || (S > 1 && (t % S) != 0)) continue;
+    const int ly = t / S - oy_lo;
+#pragma unroll
+    for (int kw = 0; kw < K; ++kw) {
+      const float wv = wr[kh * K + kw];
+#pragma unroll
+      for (int j = 0; j < DTS; ++j) {
+        const int u = ix0 + j + pl - kw;
+        if (u < 0 || (S > 1 && (u % S) != 0)) continue;
+        const int lx = u / S - ox_lo;
+        acc[j] += tile[(ly * HR + lx) * DCB + c] * wv;
+      }
+    }
+  }
+  if (iy < H && cvalid) {
+    T* DX = (T*)g.dx;
+    const size_t ibase = (size_t)g.pin.row_off[seg] + (size_t)n * H * W;
+#pragma unroll
+    for (int j = 0; j < DTS; ++j) {
+      const int ix = ix0 + j;
+      if (ix < W) {
+        T* p = DX + (ibase + (size_t)iy * W + ix) * g.C + c0 + c;
+        *p = from_f<T>(g.accumulate ? to_f<T>(*p) + acc[j] : acc[j]);
+      }
+    }
+  }
+}
+
+// dw[kh][kw][c] += sum_{n,oy,ox} dy[n][oy][ox][c] * v(x)[n][oy*s-pt+kh][ox*s-pl+kw][c]
+template <typename T, int K, int S>
+__global__ __launch_bounds__(256) void k_dw_wgrad(DwArgs g) {
+  constexpr int IH = (DTS - 1) * S + K, IW = IH;
+  constexpr int TILE = IH * IW * DCB, RED = K * K * 8 * DCB;
+  constexpr int LDSF = TILE > RED ? TILE : RED;
+  __shared__ __attribute__((aligned(16))) float lds[LDSF];
+  __shared__ float2 xf[DCB];
+  __shared__ float gt[DCB];
+  const int tid = threadIdx.x, c = tid & 31, r = tid >> 5;
+
+  const int cb = blockIdx.x % g.ncb;
+  const int chunk = blockIdx.x / g.ncb;
+  const int c0 = cb * DCB;
+  const bool cvalid = (c0 + c) < g.C;
+  const int t_begin = chunk * g.tiles_per_wg;
+  const int t_end = min(g.tiles_total, t_begin + g.tiles_per_wg);
+  const T* DY = (const T*)g.dy;
+
+  float acc[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
+
+  for (int t = t_begin; t < t_end; ++t) {
+    int seg, n, ty, tx;
+    locate_tile(g.pout, t, seg, n, ty, tx);
+    const int OH = g.pout.H[seg], OW = g.pout.W[seg], H = g.pin.H[seg], W = g.pin.W[seg];
+    const int pt = same_pad(H, K, S), pl = same_pad(W, K, S);
+    const int oy0 = ty * DTS, ox0 = tx * DTS;
+    __syncthreads();
+    prep_xf(g, xf, gt, seg, n, c0);
+    __syncthreads();
+    stage_input<T, IH, IW>(g, lds, xf, gt, seg, n, oy0 * S - pt, ox0 * S - pl, c0);
+    const int oy = oy0 + r;
+    const size_t obase = (size_t)g.pout.row_off[seg] + (size_t)n * OH * OW;
+    float dyv[DTS];
+#pragma unroll
+    for (int j = 0; j < DTS; ++j) {
+      const int ox = ox0 + j;
+      dyv[j] = (oy < OH && ox < OW && cvalid) ? to_f<T>(DY[(obase + (size_t)oy * OW + ox) * g.C + c0 + c]) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < K; ++kw) {
+        const float* trow = lds + ((r * S + kh) * IW + kw) * DCB + c;
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < DTS; ++j) a += dyv[j] * trow[j * S * DCB];
+        acc[kh * K + kw] += a;
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) lds[(i * 8 + r) * DCB + c] = acc[i];
+  __syncthreads();
+  for (int e = tid; e < K * K * DCB; e += 256) {
+    const int i = e / DCB, cc = e - i * DCB;
+    if (c0 + cc < g.C) {
+      float s = 0.f;
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) s += lds[(i * 8 + rr) * DCB + cc];
+      atomicAdd(g.dw + (size_t)i * g.C + c0 + cc, s);
+    }
+  }
+}
+
+template <typename T, int K, int S>
+static int launch_dw(int which, DwArgs g, hipStream_t s) {
+  g.ncb = cdiv(g.C, DCB);
+  if (which == 0) {
+    const int n = host_tiles(g.pout) * g.ncb;
+    if (n) hipLaunchKernelGGL((k_dw_fwd<T, K, S>), dim3(n), dim3(256), 0, s, g);
+  } else if (which == 1) {
+    const int n = host_tiles(g.pin) * g.ncb;
+    if (n) hipLaunchKernelGGL((k_dw_dgrad<T, K, S>), dim3(n), dim3(256), 0, s, g);
+  } else {
+    g.tiles_total = host_tiles(g.pout);
+    int chunks = cdiv(2048, g.ncb);
+    if (chunks > g.tiles_total) chunks = g.tiles_total;
+    if (chunks < 1) chunks = 1;
+    g.tiles_per_wg = cdiv(g.tiles_total, chunks);
+    chunks = cdiv(g.tiles_total, g.tiles_per_wg);
+    if (g.tiles_total) hipLaunchKernelGGL((k_dw_wgrad<T, K, S>), dim3(chunks * g.ncb), dim3(256), 0, s, g);
+  }
+  return check_launch("edet dwconv");
+}
+
+template <typename T>
+static int dispatch_dw(int which, int k, int stride, const DwArgs& g, hipStream_t s) {
+  if (k == 3 && stride == 1) return launch_dw<T, 3, 1>(which, g, s);
+  if (k == 3 && stride == 2) return launch_dw<T, 3, 2>(which, g, s);
+  if (k == 5 && stride == 1) return launch_dw<T, 5, 1>(which, g, s);
+  if (k == 5 && stride == 2) return launch_dw<T, 5, 2>(which, g, s);
+  set_error("dwconv: unsupported kernel %d stride %d", k, stride);
+  return EDET_EUNSUPPORTED;
+}
+
+static int check_pyrs(const edet_pyramid* pin, const edet_pyramid* pout, int k, int stride) {
+  EDET_REQUIRE(pin && pout && pin->nseg == pout->nseg && pin->batch == pout->batch &&
+                   pin->nseg >= 1 && pin->nseg <= EDET_MAX_SEG,
+               "dwconv: input/output pyramids disagree");
+  for (int i = 0; i < pin->nseg; ++i)
+    EDET_REQUIRE(pout->H[i] == cdiv(pin->H[i], stride) && pout->W[i] == cdiv(pin->W[i], stride),
+                 "dwconv: segment %d output %dx%d != ceil(%dx%d / %d)", i, pout->H[i], pout->W[i],
+                 pin->H[i], pin->W[i], stride);
+  (void)k;
+  return EDET_OK;
+}
+
+}  // namespace edet
+
+using namespace edet;
+
+extern "C" {
+
+int edet_dwconv_fwd(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
+                    int stride, const void* w, void* y, const edet_pyramid* pout,
+                    const edet_segout* stats, edet_stream_t stream) {
+  EDET_REQUIRE(x && w && y, "dwconv_fwd: null argument");
+  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0, "dwconv_fwd: need C%%8==0 and ld%%8==0");
+  int rc = check_pyrs(pin, pout, k, stride);
+  if (rc) return rc;
+  DwArgs g{};
+  g.x = x->x; g.w = w; g.y = y; g.lz = *x; g.pin = *pin; g.pout = *pout; g.C = C;
+  g.has_stats = stats != nullptr;
+  if (stats) g.stats = *stats;
+  EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_dw<T>(0, k, stride, g, (hipStream_t)stream); });
+}
+
+int edet_dwconv_dgrad(int dtype, const void* dy, const edet_pyramid* pout, int C, int k,
+                      int stride, const void* w, void* dx, const edet_pyramid* pin,
+                      int accumulate, edet_stream_t stream) {
+  EDET_REQUIRE(dy && w && dx, "dwconv_dgrad: null argument");
+  EDET_REQUIRE(C % 8 == 0, "dwconv_dgrad: need C%%8==0");
+  int rc = check_pyrs(pin, pout, k, stride);
+  if (rc) return rc;
+  DwArgs g{};
+  g.dy = dy; g.w = w; g.dx = dx; g.pin = *pin; g.pout = *pout; g.C = C; g.accumulate = accumulate;
+  EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_dw<T>(1, k, stride, g, (hipStream_t)stream); });
+}
+
+int edet_dwconv_wgrad(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
+                      int stride, const void* dy, const edet_pyramid* pout, float* dw,
+                      edet_stream_t stream) {
+  EDET_REQUIRE(x && dy && dw, "dwconv_wgrad: null argument");
+  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0, "dwconv_wgrad: need C%%8==0 and ld%%8==0");
+  int rc = check_pyrs(pin, pout, k, stride);
+  if (rc) return rc;
+  DwArgs g{};
+  g.x = x->x; g.dy = dy; g.dw = dw; g.lz = *x; g.pin = *pin; g.pout = *pout; g.C = C;
+  EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_dw<T>(2, k, stride, g, (hipStream_t)stream); });
+}
+
+}  // extern "C"

@@ -1,0 +1,199 @@
+// Detection loss: sigmoid focal loss (losses/focal_loss.py:26-52) + Huber box loss
+// (losses/box_loss.py:21-30) summed as in EfficientDetNetTrain._get_loss
+// (efficientnet/efficientdet_net_train.py:41-52), forward and backward in one pass.
+//
+// Per level l (segment of the pyramid), with N+ = sum(masks) + 1 over the batch:
+//   focal_l = sum FL / (N+ * B*H_l*W_l*A*NC)      (FL / normalizer, then Keras
+//                                                  SUM_OVER_BATCH_SIZE = mean over elements)
+//   box_l   = sum huber(pred - t) * [t != 0] / (4 N+)
+//   loss   += box_weight * box_l + focal_l
+// The one-hot class target of the reference (anchors.py:133) is represented by its index.
+#include "common.hpp"
+
+namespace edet {
+
+constexpr int LCLS_ROWS = 32;
+constexpr int LBOX_ROWS = 256;
+
+struct LossArgs {
+  const void* cls;
+  const void* box;
+  const int32_t* cls_t;
+  const float* box_t;
+  const float* npos;
+  void* dcls;
+  void* dbox;
+  float* loss;
+  float* parts;
+  edet_pyramid p;
+  int ldc, ldb, A, NC;
+  float alpha, gamma, delta, box_weight, count_scale;
+  int nb_cls;
+};
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_loss(LossArgs g) {
+  __shared__ float red[4];
+  const int tid = threadIdx.x;
+  const float npos = *g.npos + 1.f;
+  int b = blockIdx.x;
+  if (b < g.nb_cls) {
+    int seg, chunk;
+    chunk_lookup(g.p, LCLS_ROWS, b, seg, chunk);
+    const int rows = seg_rows(g.p, seg);
+    const int m0 = g.p.row_off[seg] + chunk * LCLS_ROWS;
+    const int nr = min(LCLS_ROWS, g.p.row_off[seg] + rows - m0);
+    const int AN = g.A * g.NC;
+    const float inv = 1.f / (npos * (float)rows * (float)AN * g.count_scale);
+    const float gm1 = g.gamma - 1.f;
+    const T* X = (const T*)g.cls;
+    T* D = (T*)g.dcls;
+    float s = 0.f;
+    for (int e = tid; e < nr * AN; e += 256) {
+      const int r = e / AN, col = e - r * AN;
+      const int m = m0 + r;
+      const int a = col / g.NC, c = col - a * g.NC;
+      const float x = to_f<T>(X[(size_t)m * g.ldc + col]);
+      const float y = (g.cls_t[(size_t)m * g.A + a] == c) ? 1.f : 0.f;
+      const float p = 1.f / (1.f + expf(-x));
+      const float pt = y * p + (1.f - y) * (1.f - p);
+      const float at = y * g.alpha + (1.f - y) * (1.f - g.alpha);
+      const float om = 1.f - pt;
+      const float mod = powf(om, g.gamma);
+      const float ce = fmaxf(x, 0.f) - x * y + log1pf(expf(-fabsf(x)));
+      s += at * mod * ce;
+      if (D) {
+        const float dpt = (2.f * y - 1.f) * p * (1.f - p);
+        const float dmod = (om > 0.f) ? -g.gamma * powf(om, gm1) * dpt : 0.f;
+        D[(size_t)m * g.ldc + col] = from_f<T>(at * (dmod * ce + mod * (p - y)) * inv);
+      }
+    }
+    if (D && g.ldc > AN) {
+      const int pad = g.ldc - AN;
+      for (int e = tid; e < nr * pad; e += 256) {
+        const int r = e / pad;
+        D[(size_t)(m0 + r) * g.ldc + AN + (e - r * pad)] = from_f<T>(0.f);
+      }
+    }
+    s = block_sum(s, red);
+    if (tid == 0) {
+      atomicAdd(g.loss, s * inv);
+      if (g.parts) atomicAdd(g.parts + seg, s * inv);
+    }
+    return;
+  }
+  b -= g.nb_cls;
+  int seg, chunk;
+  chunk_lookup(g.p, LBOX_ROWS, b, seg, chunk);
+  const int rows = seg_rows(g.p, seg);
+  const int m0 = g.p.row_off[seg] + chunk * LBOX_ROWS;
+  const int nr = min(LBOX_ROWS, g.p.row_off[seg] + rows - m0);
+  const int A4 = g.A * 4;
+  const float inv = 1.f / (4.f * npos);
+  const T* P = (const T*)g.box;
+  T* D = (T*)g.dbox;
+  const float dl = g.delta;
+  float s = 0.f;
+  for (int e = tid; e < nr * A4; e += 256) {
+    const int r = e / A4, col = e - r * A4;
+    const int m = m0 + r;
+    const float t = g.box_t[(size_t)m * A4 + col];
+    const float pr = to_f<T>(P[(size_t)m * g.ldb + col]);
+    const float mask = (t != 0.f) ? 1.f : 0.f;
+    const float err = pr - t, ae = fabsf(err);
+    const float h = (ae <= dl) ? 0.5f * err * err : 0.5f * dl * dl + dl * (ae - dl);
+    s += h * mask;
+    if (D) {
+      const float dh = (ae <= dl) ? err : (err > 0.f ? dl : -dl);
+      D[(size_t)m * g.ldb + col] = from_f<T>(dh * mask * inv * g.box_weight);
+    }
+  }
+  if (D && g.ldb > A4) {
+    const int pad = g.ldb - A4;
+    for (int e = tid; e < nr * pad; e += 256) {
+      const int r = e / pad;
+      D[(size_t)(m0 + r) * g.ldb + A4 + (e - r * pad)] = from_f<T>(0.f);
+    }
+  }
+  s = block_sum(s, red);
+  if (tid == 0) {
+    atomicAdd(g.loss, s * inv * g.box_weight);
+    if (g.parts) atomicAdd(g.parts + EDET_MAX_SEG + seg, s * inv);
+  }
+}
+
+__global__ void k_count_pos(const uint8_t* mask, int64_t n, float* out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    s += mask[i] ? 1.f : 0.f;
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+__global__ void k_onehot_index(const float* onehot, int64_t n, int NC, int32_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float* p = onehot + i * NC;
+  int best = 0;
+  float bv = p[0];
+  for (int c = 1; c < NC; ++c)
+    if (p[c] > bv) { bv = p[c]; best = c; }
+  out[i] = best;
+}
+
+}  // namespace edet
+
+using namespace edet;
+
+extern "C" {
+
+int edet_detection_loss(int dtype, const void* cls, int ldc, const void* box, int ldb,
+                        const edet_pyramid* p, int A, int NC, const int32_t* cls_t,
+                        const float* box_t, const float* npos_sum, float alpha, float gamma,
+                        float delta, float box_weight, float focal_count_scale, void* dcls,
+                        void* dbox, float* loss, float* level_parts, edet_stream_t stream) {
+  EDET_REQUIRE(cls && box && p && cls_t && box_t && npos_sum && loss, "detection_loss: null argument");
+  EDET_REQUIRE(ldc >= A * NC && ldb >= A * 4 && p->nseg >= 1 && p->nseg <= EDET_MAX_SEG,
+               "detection_loss: bad strides");
+  LossArgs g{};
+  g.cls = cls; g.box = box; g.cls_t = cls_t; g.box_t = box_t; g.npos = npos_sum; g.dcls = dcls;
+  g.dbox = dbox; g.loss = loss; g.parts = level_parts; g.p = *p; g.ldc = ldc; g.ldb = ldb;
+  g.A = A; g.NC = NC; g.alpha = alpha; g.gamma = gamma; g.delta = delta; g.box_weight = box_weight;
+  g.count_scale = focal_count_scale > 0.f ? focal_count_scale : 1.f;
+  g.nb_cls = total_chunks(*p, LCLS_ROWS);
+  const int nb = g.nb_cls + total_chunks(*p, LBOX_ROWS);
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    if (nb) hipLaunchKernelGGL(k_loss<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, g);
+    return check_launch("edet detection_loss");
+  });
+}
+
+int edet_count_positives(const uint8_t* mask, int64_t n, float* out, edet_stream_t stream) {
+  EDET_REQUIRE(mask && out, "count_positives: null argument");
+  if (n <= 0) return EDET_OK;
+  int nb = (int)((n + 255) / 256);
+  if (nb > 1024) nb = 1024;
+  hipLaunchKernelGGL(k_count_pos, dim3(nb), dim3(256), 0, (hipStream_t)stream, mask, n, out);
+  return check_launch("edet count_positives");
+}
+
+int edet_onehot_to_index(const float* onehot, int64_t n, int NC, int32_t* out,
+                         edet_stream_t stream) {
+  EDET_REQUIRE(onehot && out && NC > 0, "onehot_to_index: bad argument");
+  if (n <= 0) return EDET_OK;
+  hipLaunchKernelGGL(k_onehot_index, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     onehot, n, NC, out);
+  return check_launch("edet onehot_to_index");
+}
+
+}  // extern "C"

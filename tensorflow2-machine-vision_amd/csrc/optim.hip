@@ -1,0 +1,147 @@
+// Fused optimizer step over the flat fp32 parameter buffer:
+//   g' = g + l2 * w            (efficientdet_net_train.py:21-28, 4e-5 * sum l2_loss(kernels))
+//   gnorm = ||g'||_2; g' *= clip / max(gnorm, clip)   (tf.clip_by_global_norm, :129-130)
+//   v = m v - lr g'; w += v                           (Keras SGD momentum, train.py:114-115)
+//   ema -= (1 - d)(ema - w)                           (tfa MovingAverage, train.py:117-119)
+//   lr  = CosineLrSchedule(step)                      (train.py:35-63)
+// plus the fp32 -> compute-dtype weight cast, drop-connect masks and device step counter.
+#include "common.hpp"
+
+namespace edet {
+
+__device__ float sched_lr(const edet_sched& s, int step) {
+  if (s.fixed_lr > 0.f) return s.fixed_lr;
+  const float fs = (float)step;
+  if (step < s.warmup_steps)
+    return s.warmup_init + (fs / (float)s.warmup_steps) * (s.adjusted_lr - s.warmup_init);
+  const float decay = (float)(s.total_steps - s.warmup_steps);
+  return 0.5f * s.adjusted_lr * (1.f + cosf(3.14159265358979323846f * fs / decay));
+}
+
+__global__ __launch_bounds__(256) void k_opt_norm(const float* w, const float* g, int64_t n, int64_t n_l2,
+                                                  edet_sched sc, float* scalars, int32_t* step) {
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float gs = 0.f, ws = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float gv = g[i];
+    if (i < n_l2) {
+      const float wv = w[i];
+      gv += sc.l2_weight * wv;
+      ws += wv * wv;
+    }
+    gs += gv * gv;
+  }
+  gs = wave_sum(gs);
+  ws = wave_sum(ws);
+  if (lane == 0) { red[0][wave] = gs; red[1][wave] = ws; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(scalars + 1, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    atomicAdd(scalars + 2, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+    if (blockIdx.x == 0) {
+      const int s = *step;
+      scalars[4] = sched_lr(sc, s);
+      *step = s + 1;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_opt_apply(float* w, const float* g, float* v, float* ema, int64_t n,
+                                                   int64_t n_l2, edet_sched sc, float* scalars, T* wc) {
+  const float gnorm = sqrtf(scalars[1]);
+  const float clip = sc.clip_norm / fmaxf(gnorm, sc.clip_norm);
+  const float lr = scalars[4];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float wv = w[i];
+    float gv = g[i];
+    if (i < n_l2) gv += sc.l2_weight * wv;
+    gv *= clip;
+    const float vv = sc.momentum * v[i] - lr * gv;
+    v[i] = vv;
+    wv += vv;
+    w[i] = wv;
+    if (ema) ema[i] -= (1.f - sc.ema_decay) * (ema[i] - wv);
+    if (wc) wc[i] = from_f<T>(wv);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    scalars[3] = gnorm;
+    scalars[0] += sc.l2_weight * 0.5f * scalars[2];
+  }
+}
+
+template <typename T>
+__global__ void k_cast(const float* src, T* dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    dst[i] = from_f<T>(src[i]);
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// drop_connect.py:13-18: binary = floor(p + U[0,1)); output scale = binary / p
+__global__ void k_dropmask(float* out, int n, float p, uint64_t seed, const int32_t* step) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h = splitmix64(seed ^ splitmix64(((uint64_t)(uint32_t)*step << 32) | (uint32_t)i));
+  const float u = (float)(h >> 40) * (1.f / 16777216.f);
+  out[i] = floorf(p + u) / p;
+}
+
+static int grid_for(int64_t n) {
+  int64_t nb = (n + 255) / 256;
+  if (nb > 2048) nb = 2048;
+  if (nb < 1) nb = 1;
+  return (int)nb;
+}
+
+}  // namespace edet
+
+using namespace edet;
+
+extern "C" {
+
+int edet_opt_norm(const float* w, const float* g, int64_t n, int64_t n_l2,
+                  const edet_sched* sched, float* scalars, int32_t* step,
+                  edet_stream_t stream) {
+  EDET_REQUIRE(w && g && sched && scalars && step && n_l2 <= n, "opt_norm: bad argument");
+  hipLaunchKernelGGL(k_opt_norm, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, w, g, n, n_l2, *sched,
+                     scalars, step);
+  return check_launch("edet opt_norm");
+}
+
+int edet_opt_apply(float* w, const float* g, float* v, float* ema, int64_t n, int64_t n_l2,
+                   const edet_sched* sched, float* scalars, int dtype, void* wcompute,
+                   edet_stream_t stream) {
+  EDET_REQUIRE(w && g && v && sched && scalars && n_l2 <= n, "opt_apply: bad argument");
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(k_opt_apply<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, w, g, v, ema, n,
+                       n_l2, *sched, scalars, (T*)wcompute);
+    return check_launch("edet opt_apply");
+  });
+}
+
+int edet_cast_f32(int dtype, const float* src, void* dst, int64_t n, edet_stream_t stream) {
+  EDET_REQUIRE(src && dst, "cast_f32: null argument");
+  if (n <= 0) return EDET_OK;
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(k_cast<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, src, (T*)dst, n);
+    return check_launch("edet cast");
+  });
+}
+
+int edet_dropmask(float* out, int n, float survival, uint64_t seed, const int32_t* step,
+                  edet_stream_t stream) {
+  EDET_REQUIRE(out && step && survival > 0.f, "dropmask: bad argument");
+  if (n <= 0) return EDET_OK;
+  hipLaunchKernelGGL(k_dropmask, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, n, survival, seed,
+                     step);
+  return check_launch("edet dropmask");
+}
+
+}  // extern "C"

@@ -1,0 +1,501 @@
+// Stem convolution, max-pool resampling and BiFPN weighted fusion.
+//
+//   stem   : Conv2D 3x3 s2 SAME, no bias (layers/stem.py:15-22,38) + BN statistics
+//   maxpool: MaxPooling2D 3x3 s2 SAME (layers/resample_feature_map.py:35-38); padded cells
+//            are ignored; backward routes each window's gradient to its first maximum in
+//            row-major window order (TF MaxPoolGrad semantics)
+//   fuse   : BiFPNNode.call (layers/bifpn.py:59-65): out = sum_i R_i(v_i) * w_i / (sum w + 1e-4)
+//            with R_i in {identity, nearest resize (tf.image.resize, half-pixel centres),
+//            max-pool}; weights unconstrained (no ReLU)
+#include <float.h>
+#include "common.hpp"
+
+namespace edet {
+
+// ------------------------------------------------------------------ stem
+template <typename T>
+__global__ __launch_bounds__(256) void k_stem_fwd(const T* x, int B, int H, int W, const T* w, int Cout,
+                                                  T* y, float* sum, float* sq) {
+  __shared__ float ws[27 * 64];
+  __shared__ float red[2][64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < 27 * Cout; i += 256) ws[i] = to_f<T>(w[i]);
+  if (tid < 128) (&red[0][0])[tid] = 0.f;
+  __syncthreads();
+  const int OH = cdiv(H, 2), OW = cdiv(W, 2);
+  const int pt = same_pad(H, 3, 2), pl = same_pad(W, 3, 2);
+  const long p = (long)blockIdx.x * 256 + tid;
+  const bool valid = p < (long)B * OH * OW;
+  float xin[27];
+  if (valid) {
+    const int n = (int)(p / ((long)OH * OW));
+    const int rem = (int)(p - (long)n * OH * OW);
+    const int oy = rem / OW, ox = rem - oy * OW;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iy = oy * 2 - pt + kh, ix = ox * 2 - pl + kw;
+        const bool in = iy >= 0 && iy < H && ix >= 0 && ix < W;
+        const T* px = x + (((size_t)n * H + iy) * W + ix) * 3;
+#pragma unroll
+        for (int ci = 0; ci < 3; ++ci) xin[(kh * 3 + kw) * 3 + ci] = in ? to_f<T>(px[ci]) : 0.f;
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 27; ++i) xin[i] = 0.f;
+  }
+  for (int co0 = 0; co0 < Cout; co0 += 8) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 27; ++k) {
+      const float xv = xin[k];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += xv * ws[k * Cout + co0 + j];
+    }
+    if (valid) st8(y + (size_t)p * Cout + co0, acc);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = valid ? acc[j] : 0.f;
+      const float s = wave_sum(a), q = wave_sum(a * a);
+      if (lane == 0) { atomicAdd(&red[0][co0 + j], s); atomicAdd(&red[1][co0 + j], q); }
+    }
+  }
+  __syncthreads();
+  if (tid < Cout) {
+    atomicAdd(sum + tid, red[0][tid]);
+    atomicAdd(sq + tid, red[1][tid]);
+  }
+}
+
+// dw[kh][kw][ci][co] += sum_pixels x_patch * dy
+template <typename T>
+__global__ __launch_bounds__(256) void k_stem_wgrad(const T* x, int B, int H, int W, const T* dy, int Cout,
+                                                    float* dw, long px_per_wg) {
+  __shared__ float patch[64][28];
+  __shared__ float dys[64][65];
+  const int tid = threadIdx.x;
+  const int OH = cdiv(H, 2), OW = cdiv(W, 2);
+  const int pt = same_pad(H, 3, 2), pl = same_pad(W, 3, 2);
+  const long total = (long)B * OH * OW;
+  const long p_begin = (long)blockIdx.x * px_per_wg;
+  const long p_end = min(total, p_begin + px_per_wg);
+  const int NOUT = 27 * Cout;
+  float acc[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) acc[i] = 0.f;
+  for (long p0 = p_begin; p0 < p_end; p0 += 64) {
+    __syncthreads();
+    for (int e = tid; e < 64 * 27; e += 256) {
+      const int px = e / 27, k = e - px * 27;
+      const long p = p0 + px;
+      float v = 0.f;
+      if (p < p_end) {
+        const int n = (int)(p / ((long)OH * OW));
+        const int rem = (int)(p - (long)n * OH * OW);
+        const int oy = rem / OW, ox = rem - oy * OW;
+        const int kh = k / 9, kw = (k / 3) % 3, ci = k % 3;
+        const int iy = oy * 2 - pt + kh, ix = ox * 2 - pl + kw;
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = to_f<T>(x[(((size_t)n * H + iy) * W + ix) * 3 + ci]);
+      }
+      patch[px][k] = v;
+    }
+    for (int e = tid; e < 64 * Cout; e += 256) {
+      const int px = e / Cout, co = e - px * Cout;
+      const long p = p0 + px;
+      dys[px][co] = (p < p_end) ? to_f<T>(dy[(size_t)p * Cout + co]) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int j = tid + i * 256;
+      if (j < NOUT) {
+        const int pk = j / Cout, co = j - pk * Cout;
+        float a = 0.f;
+#pragma unroll 8
+        for (int px = 0; px < 64; ++px) a += patch[px][pk] * dys[px][co];
+        acc[i] += a;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const int j = tid + i * 256;
+    if (j < NOUT) atomicAdd(dw + j, acc[i]);
+  }
+}
+
+// ------------------------------------------------------------------ resample helpers
+// tf.image.resize(method='nearest'): ResizeNearestNeighbor(align_corners=False,
+// half_pixel_centers=True): in = min(floor((o + 0.5) * in/out), in - 1)
+__device__ __forceinline__ int nearest_src(int o, int in, int out) {
+  const float scale = (float)in / (float)out;
+  int i = (int)floorf(((float)o + 0.5f) * scale);
+  if (i > in - 1) i = in - 1;
+  if (i < 0) i = 0;
+  return i;
+}
+
+template <typename T>
+__device__ __forceinline__ void lazy_load8(const edet_lazy& lz, const float2* af, size_t row, int c, int nc, float* o) {
+  ld8m((const T*)lz.x + row * lz.ld + c, nc, o);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = lazy_apply(o[j], af[j], lz.act);
+}
+
+// max over the 3x3 s2 SAME window of output (oy, ox); optionally the argmax (row-major first)
+template <typename T>
+__device__ __forceinline__ void pool_window(const edet_lazy& lz, const float2* af, size_t img_row0, int H, int W,
+                                            int pt, int pl, int oy, int ox, int c, int nc, float* best, int* arg) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { best[j] = -FLT_MAX; arg[j] = -1; }
+  for (int kh = 0; kh < 3; ++kh) {
+    const int iy = oy * 2 - pt + kh;
+    if (iy < 0 || iy >= H) continue;
+    for (int kw = 0; kw < 3; ++kw) {
+      const int ix = ox * 2 - pl + kw;
+      if (ix < 0 || ix >= W) continue;
+      float v[8];
+      lazy_load8<T>(lz, af, img_row0 + (size_t)iy * W + ix, c, nc, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (arg[j] < 0 || v[j] > best[j]) { best[j] = v[j]; arg[j] = iy * W + ix; }
+    }
+  }
+}
+
+__device__ __forceinline__ void affine8(const edet_lazy& lz, int c, int C, float inv, float2* af) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) af[j] = (c + j < C) ? bn_affine(lz.bn, 0, c + j, inv) : make_float2(1.f, 0.f);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_maxpool_fwd(edet_lazy lz, int B, int H, int W, int C, T* y) {
+  const int OH = cdiv(H, 2), OW = cdiv(W, 2), nv = C / 8;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)B * OH * OW * nv) return;
+  const int cv = (int)(idx % nv);
+  const long pix = idx / nv;
+  const int n = (int)(pix / ((long)OH * OW));
+  const int rem = (int)(pix - (long)n * OH * OW);
+  const int oy = rem / OW, ox = rem - oy * OW;
+  float2 af[8];
+  affine8(lz, cv * 8, C, 1.f / (float)(B * H * W), af);
+  float best[8];
+  int arg[8];
+  pool_window<T>(lz, af, (size_t)n * H * W, H, W, same_pad(H, 3, 2), same_pad(W, 3, 2), oy, ox, cv * 8, 8, best, arg);
+  st8(y + (size_t)pix * C + cv * 8, best);
+}
+
+// gather form of the max-pool backward: input pixel collects dy of every window whose
+// (recomputed) argmax is this pixel
+template <typename T>
+__device__ __forceinline__ void pool_bwd_gather(const edet_lazy& lz, const float2* af, const T* dy, size_t img_row0,
+                                                size_t out_row0, int H, int W, int OH, int OW, int C, int iy, int ix,
+                                                int c, float scale, float* d) {
+  const int pt = same_pad(H, 3, 2), pl = same_pad(W, 3, 2);
+  const int oy_lo = max(0, fdiv(iy + pt - 2 + 1, 2)), oy_hi = min(OH - 1, fdiv(iy + pt, 2));
+  const int ox_lo = max(0, fdiv(ix + pl - 2 + 1, 2)), ox_hi = min(OW - 1, fdiv(ix + pl, 2));
+  const int me = iy * W + ix;
+  for (int oy = oy_lo; oy <= oy_hi; ++oy)
+    for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+      float best[8];
+      int arg[8];
+      pool_window<T>(lz, af, img_row0, H, W, pt, pl, oy, ox, c, 8, best, arg);
+      float g[8];
+      ld8(dy + (out_row0 + (size_t)oy * OW + ox) * C + c, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (arg[j] == me) d[j] += g[j] * scale;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_maxpool_bwd(edet_lazy lz, int B, int H, int W, int C, const T* dy, T* dx,
+                                                     int accumulate) {
+  const int OH = cdiv(H, 2), OW = cdiv(W, 2), nv = C / 8;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)B * H * W * nv) return;
+  const int cv = (int)(idx % nv);
+  const long pix = idx / nv;
+  const int n = (int)(pix / ((long)H * W));
+  const int rem = (int)(pix - (long)n * H * W);
+  const int iy = rem / W, ix = rem - iy * W;
+  float2 af[8];
+  affine8(lz, cv * 8, C, 1.f / (float)(B * H * W), af);
+  float d[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] = 0.f;
+  pool_bwd_gather<T>(lz, af, dy, (size_t)n * H * W, (size_t)n * OH * OW, H, W, OH, OW, C, iy, ix, cv * 8, 1.f, d);
+  acc8m(dx + (size_t)pix * C + cv * 8, 8, d, accumulate);
+}
+
+// ------------------------------------------------------------------ BiFPN fusion
+struct FuseArgs {
+  edet_fuse_input in[3];
+  const float* w;
+  const void* fused;
+  const void* dout;
+  void* out;
+  float* dw;
+  int n_in, B, H, W, C;
+  int nb_w, nb_in[3];
+};
+
+// resampled value of input i at output pixel (n, h, w), 8 channels from c
+template <typename T>
+__device__ __forceinline__ void fuse_input_value(const edet_fuse_input& fi, const float2* af, int n, int h, int w,
+                                                 int OH, int OW, int c, float* v) {
+  const int Hi = fi.H, Wi = fi.W;
+  const size_t r0 = (size_t)n * Hi * Wi;
+  if (fi.mode == EDET_MODE_SAME) {
+    lazy_load8<T>(fi.v, af, r0 + (size_t)h * Wi + w, c, 8, v);
+  } else if (fi.mode == EDET_MODE_UPSAMPLE) {
+    const int iy = nearest_src(h, Hi, OH), ix = nearest_src(w, Wi, OW);
+    lazy_load8<T>(fi.v, af, r0 + (size_t)iy * Wi + ix, c, 8, v);
+  } else {
+    int arg[8];
+    pool_window<T>(fi.v, af, r0, Hi, Wi, same_pad(Hi, 3, 2), same_pad(Wi, 3, 2), h, w, c, 8, v, arg);
+  }
+}
+
+__device__ __forceinline__ float fuse_denom(const float* w, int n_in) {
+  float s = 0.f;
+  for (int i = 0; i < n_in; ++i) s += w[i];
+  return s + 1e-4f;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_fuse_fwd(FuseArgs g) {
+  const int nv = g.C / 8;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)g.B * g.H * g.W * nv) return;
+  const int cv = (int)(idx % nv);
+  const long pix = idx / nv;
+  const int n = (int)(pix / ((long)g.H * g.W));
+  const int rem = (int)(pix - (long)n * g.H * g.W);
+  const int h = rem / g.W, w = rem - h * g.W;
+  const float den = fuse_denom(g.w, g.n_in);
+  float o[8];
+  for (int i = 0; i < g.n_in; ++i) {
+    const edet_fuse_input& fi = g.in[i];
+    float2 af[8];
+    affine8(fi.v, cv * 8, g.C, 1.f / (float)(g.B * fi.H * fi.W), af);
+    float v[8];
+    fuse_input_value<T>(fi, af, n, h, w, g.H, g.W, cv * 8, v);
+    const float wi = g.w[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float t = v[j] * wi / den;
+      o[j] = (i == 0) ? t : o[j] + t;
+    }
+  }
+  st8((T*)g.out + (size_t)pix * g.C + cv * 8, o);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_fuse_bwd(FuseArgs g) {
+  __shared__ float red[3][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nv = g.C / 8;
+  const float den = fuse_denom(g.w, g.n_in);
+  int b = blockIdx.x;
+  if (b < g.nb_w) {
+    // weight gradient: dw_i = sum dF * (v_i - F) / den
+    const long idx = (long)b * 256 + tid;
+    float part[3] = {0.f, 0.f, 0.f};
+    if (idx < (long)g.B * g.H * g.W * nv) {
+      const int cv = (int)(idx % nv);
+      const long pix = idx / nv;
+      const int n = (int)(pix / ((long)g.H * g.W));
+      const int rem = (int)(pix - (long)n * g.H * g.W);
+      const int h = rem / g.W, w = rem - h * g.W;
+      float F[8], dF[8];
+      ld8((const T*)g.fused + (size_t)pix * g.C + cv * 8, F);
+      ld8((const T*)g.dout + (size_t)pix * g.C + cv * 8, dF);
+      for (int i = 0; i < g.n_in; ++i) {
+        const edet_fuse_input& fi = g.in[i];
+        float2 af[8];
+        affine8(fi.v, cv * 8, g.C, 1.f / (float)(g.B * fi.H * fi.W), af);
+        float v[8];
+        fuse_input_value<T>(fi, af, n, h, w, g.H, g.W, cv * 8, v);
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += dF[j] * (v[j] - F[j]);
+        part[i] = s / den;
+      }
+    }
+    for (int i = 0; i < g.n_in; ++i) {
+      const float s = wave_sum(part[i]);
+      if (lane == 0) red[i][wave] = s;
+    }
+    __syncthreads();
+    if (tid < g.n_in) atomicAdd(g.dw + tid, red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3]);
+    return;
+  }
+  b -= g.nb_w;
+  int i = 0;
+  for (; i < g.n_in - 1; ++i) {
+    if (b < g.nb_in[i]) break;
+    b -= g.nb_in[i];
+  }
+  const edet_fuse_input& fi = g.in[i];
+  const int Hi = fi.H, Wi = fi.W;
+  const long idx = (long)b * 256 + tid;
+  if (idx >= (long)g.B * Hi * Wi * nv) return;
+  const int cv = (int)(idx % nv);
+  const long pix = idx / nv;
+  const int n = (int)(pix / ((long)Hi * Wi));
+  const int rem = (int)(pix - (long)n * Hi * Wi);
+  const int iy = rem / Wi, ix = rem - iy * Wi;
+  const float wn = g.w[i] / den;
+  const T* dF = (const T*)g.dout;
+  const size_t o0 = (size_t)n * g.H * g.W;
+  float d[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] = 0.f;
+  if (fi.mode == EDET_MODE_SAME) {
+    float v[8];
+    ld8(dF + (o0 + (size_t)iy * g.W + ix) * g.C + cv * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = v[j] * wn;
+  } else if (fi.mode == EDET_MODE_UPSAMPLE) {
+    // output rows h with nearest_src(h) == iy lie in [iy*OH/Hi - 1, (iy+1)*OH/Hi + 1]
+    const int h_lo = max(0, (int)((long)iy * g.H / Hi) - 1), h_hi = min(g.H - 1, (int)((long)(iy + 1) * g.H / Hi) + 1);
+    const int w_lo = max(0, (int)((long)ix * g.W / Wi) - 1), w_hi = min(g.W - 1, (int)((long)(ix + 1) * g.W / Wi) + 1);
+    for (int h = h_lo; h <= h_hi; ++h) {
+      if (nearest_src(h, Hi, g.H) != iy) continue;
+      for (int w = w_lo; w <= w_hi; ++w) {
+        if (nearest_src(w, Wi, g.W) != ix) continue;
+        float v[8];
+        ld8(dF + (o0 + (size_t)h * g.W + w) * g.C + cv * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] += v[j] * wn;
+      }
+    }
+  } else {
+    float2 af[8];
+    affine8(fi.v, cv * 8, g.C, 1.f / (float)(g.B * Hi * Wi), af);
+    pool_bwd_gather<T>(fi.v, af, dF, (size_t)n * Hi * Wi, o0, Hi, Wi, g.H, g.W, g.C, iy, ix, cv * 8, wn, d);
+  }
+  acc8m((T*)fi.dx + (size_t)pix * g.C + cv * 8, 8, d, fi.accumulate);
+}
+
+}  // namespace edet
+
+using namespace edet;
+
+extern "C" {
+
+int edet_stem_fwd(int dtype, const void* x, int B, int H, int W, const void* w, int Cout,
+                  void* y, float* sum, float* sq, edet_stream_t stream) {
+  EDET_REQUIRE(x && w && y && sum && sq, "stem_fwd: null argument");
+  EDET_REQUIRE(Cout % 8 == 0 && Cout <= 64, "stem_fwd: Cout must be a multiple of 8, <= 64");
+  const long px = (long)B * cdiv(H, 2) * cdiv(W, 2);
+  const int nb = (int)((px + 255) / 256);
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    if (nb) hipLaunchKernelGGL(k_stem_fwd<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const T*)x, B, H, W,
+                               (const T*)w, Cout, (T*)y, sum, sq);
+    return check_launch("edet stem_fwd");
+  });
+}
+
+int edet_stem_wgrad(int dtype, const void* x, int B, int H, int W, const void* dy, int Cout,
+                    float* dw, edet_stream_t stream) {
+  EDET_REQUIRE(x && dy && dw, "stem_wgrad: null argument");
+  EDET_REQUIRE(Cout % 8 == 0 && Cout <= 64, "stem_wgrad: Cout must be a multiple of 8, <= 64");
+  const long px = (long)B * cdiv(H, 2) * cdiv(W, 2);
+  long per = (px + 2047) / 2048;
+  per = ((per + 63) / 64) * 64;
+  if (per < 64) per = 64;
+  const int nb = (int)((px + per - 1) / per);
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    if (nb) hipLaunchKernelGGL(k_stem_wgrad<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const T*)x, B, H, W,
+                               (const T*)dy, Cout, dw, per);
+    return check_launch("edet stem_wgrad");
+  });
+}
+
+int edet_maxpool_fwd(int dtype, const edet_lazy* x, int B, int H, int W, int C, void* y,
+                     edet_stream_t stream) {
+  EDET_REQUIRE(x && x->x && y, "maxpool_fwd: null argument");
+  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0 && x->gate == nullptr, "maxpool_fwd: need C%%8==0, no gate");
+  const long n = (long)B * cdiv(H, 2) * cdiv(W, 2) * (C / 8);
+  const int nb = (int)((n + 255) / 256);
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    if (nb) hipLaunchKernelGGL(k_maxpool_fwd<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, *x, B, H, W, C, (T*)y);
+    return check_launch("edet maxpool_fwd");
+  });
+}
+
+int edet_maxpool_bwd(int dtype, const edet_lazy* x, int B, int H, int W, int C,
+                     const void* dy, void* dx, int accumulate, edet_stream_t stream) {
+  EDET_REQUIRE(x && x->x && dy && dx, "maxpool_bwd: null argument");
+  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0 && x->gate == nullptr, "maxpool_bwd: need C%%8==0, no gate");
+  const long n = (long)B * H * W * (C / 8);
+  const int nb = (int)((n + 255) / 256);
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    if (nb) hipLaunchKernelGGL(k_maxpool_bwd<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, *x, B, H, W, C,
+                               (const T*)dy, (T*)dx, accumulate);
+    return check_launch("edet maxpool_bwd");
+  });
+}
+
+static int fuse_setup(FuseArgs& g, int n_in, const edet_fuse_input* ins, const float* w, int B, int H, int W,
+                      int C) {
+  EDET_REQUIRE(ins && w && n_in >= 1 && n_in <= 3, "bifpn_fuse: 1..3 inputs required");
+  EDET_REQUIRE(C % 8 == 0, "bifpn_fuse: need C%%8==0");
+  for (int i = 0; i < n_in; ++i) {
+    const edet_fuse_input& f = ins[i];
+    EDET_REQUIRE(f.v.x && f.v.ld == C && f.v.gate == nullptr, "bifpn_fuse: input %d must be [rows][C]", i);
+    if (f.mode == EDET_MODE_SAME)
+      EDET_REQUIRE(f.H == H && f.W == W, "bifpn_fuse: input %d size mismatch", i);
+    else if (f.mode == EDET_MODE_MAXPOOL)
+      EDET_REQUIRE(cdiv(f.H, 2) == H && cdiv(f.W, 2) == W, "bifpn_fuse: input %d pool size mismatch", i);
+    else
+      EDET_REQUIRE(f.mode == EDET_MODE_UPSAMPLE && f.H > 0 && f.W > 0, "bifpn_fuse: input %d bad mode", i);
+    g.in[i] = f;
+  }
+  g.w = w; g.n_in = n_in; g.B = B; g.H = H; g.W = W; g.C = C;
+  return EDET_OK;
+}
+
+int edet_bifpn_fuse_fwd(int dtype, int n_in, const edet_fuse_input* ins, const float* w,
+                        int B, int H, int W, int C, void* out, edet_stream_t stream) {
+  FuseArgs g{};
+  int rc = fuse_setup(g, n_in, ins, w, B, H, W, C);
+  if (rc) return rc;
+  EDET_REQUIRE(out, "bifpn_fuse_fwd: null out");
+  g.out = out;
+  const long n = (long)B * H * W * (C / 8);
+  const int nb = (int)((n + 255) / 256);
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    if (nb) hipLaunchKernelGGL(k_fuse_fwd<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, g);
+    return check_launch("edet bifpn_fuse_fwd");
+  });
+}
+
+int edet_bifpn_fuse_bwd(int dtype, int n_in, const edet_fuse_input* ins, const float* w,
+                        int B, int H, int W, int C, const void* out, const void* dout,
+                        float* dw, edet_stream_t stream) {
+  FuseArgs g{};
+  int rc = fuse_setup(g, n_in, ins, w, B, H, W, C);
+  if (rc) return rc;
+  EDET_REQUIRE(out && dout && dw, "bifpn_fuse_bwd: null argument");
+  for (int i = 0; i < n_in; ++i) EDET_REQUIRE(ins[i].dx, "bifpn_fuse_bwd: input %d has no dx", i);
+  g.fused = out; g.dout = dout; g.dw = dw;
+  g.nb_w = (int)(((long)B * H * W * (C / 8) + 255) / 256);
+  int nb = g.nb_w;
+  for (int i = 0; i < n_in; ++i) {
+    g.nb_in[i] = (int)(((long)B * ins[i].H * ins[i].W * (C / 8) + 255) / 256);
+    nb += g.nb_in[i];
+  }
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    if (nb) hipLaunchKernelGGL(k_fuse_bwd<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, g);
+    return check_launch("edet bifpn_fuse_bwd");
+  });
+}
+
+}  // extern "C"

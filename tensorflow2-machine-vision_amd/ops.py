@@ -1,0 +1,258 @@
+"""Forward ops of the EfficientDet hot path, each with its recorded backward.
+
+Every function launches libedet kernels on the current stream and, in training mode,
+records a closure on the engine's tape that turns d(output value) into d(input values) and
+accumulates weight gradients into the flat fp32 gradient buffer.
+
+Reference call sites replaced (AIServer/ai_api/ai_models/...):
+  stem            layers/stem.py:37-38
+  conv1x1         layers/mb_conv_block.py:143-154, layers/resample_feature_map.py:43-47,
+                  pointwise halves of SeparableConv2D (bifpn.py:27, class_net.py:89,97, box_net.py:90,97)
+  dwconv          layers/mb_conv_block.py:147, depthwise halves of the SeparableConv2Ds
+  squeeze_excite  layers/se.py:35-39
+  maxpool         layers/resample_feature_map.py:48-49
+  bifpn_fuse      layers/bifpn.py:59-66 (+ the swish of OpAfterCombine, bifpn.py:26)
+  residual        layers/class_net.py:93-96, layers/box_net.py:93-95
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib as L
+from .runtime import Act, BNParam, Engine, GradRec, ParamStore, Pyr, SERec, memset0, seg_out, stream, vp
+
+
+def _stats_out(eng: Engine, bns: Optional[List[BNParam]]):
+    if bns is None or not eng.training:
+        return None
+    return seg_out([(bn.tsum, bn.tsq) for bn in bns])
+
+
+def _bn_grads(bns: List[BNParam]):
+    return seg_out([(bn.dgamma, bn.dbeta) for bn in bns])
+
+
+def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor, int]:
+    """d(value) -> d(raw) through the lazy transform act(bn(raw)) * gate (+ SE branch)."""
+    if not out.has_transform and rec.scale is None:
+        return rec.t, rec.ld
+    assert rec.ld == out.C
+    s = stream()
+    lz = out.lazy()
+    dsq = None
+    if out.se is not None:
+        se = out.se
+        B = out.pyr.batch
+        HW = out.pyr.H * out.pyr.W
+        dgate = eng.zeros_f32(B, out.C)
+        L.call("edet_gate_grad", eng.dt, lz, B, HW, out.C, vp(rec.t), vp(dgate), s)
+        dsq = torch.empty((B, out.C), dtype=torch.float32, device=eng.device)
+        L.call("edet_se_bwd", B, out.C, se.R, HW, vp(se.s), vp(se.z1), vp(se.gate), vp(dgate),
+               vp(se.w1), vp(se.w2), vp(se.dw1), vp(se.db1), vp(se.dw2), vp(se.db2), vp(dsq), s)
+    grads = None
+    if out.bns is not None:
+        grads = _bn_grads(out.bns)
+        L.call("edet_lazy_bwd_reduce", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), grads, s)
+    dx = eng.empty(out.pyr.rows, out.C)
+    L.call("edet_lazy_bwd_apply", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), grads,
+           vp(dx), 0, s)
+    return dx, out.C
+
+
+# --------------------------------------------------------------------------- stem
+def stem(eng: Engine, P: ParamStore, x: torch.Tensor, wname: str, bn: BNParam) -> Act:
+    """Conv 3x3 s2 SAME (no bias) -> BN -> swish.  x: [B, H, W, 3] in the compute dtype."""
+    B, H, W, _ = x.shape
+    Cout = bn.C
+    pyr = Pyr(B, [((H + 1) // 2, (W + 1) // 2)])
+    y = eng.empty(pyr.rows, Cout)
+    if eng.training:
+        L.call("edet_stem_fwd", eng.dt, vp(x), B, H, W, vp(P.wcv(wname)), Cout, vp(y), vp(bn.tsum), vp(bn.tsq), stream())
+    else:
+        scratch = eng.zeros_f32(2, Cout)
+        L.call("edet_stem_fwd", eng.dt, vp(x), B, H, W, vp(P.wcv(wname)), Cout, vp(y), vp(scratch[0]),
+               vp(scratch[1]), stream())
+    out = Act(y, pyr, Cout, [bn], L.ACT_SWISH, training=eng.training, name="stem")
+
+    def bwd():
+        rec = eng.tape.take(out)
+        if rec is None:
+            return
+        d, ld = value_grad_to_raw(eng, out, rec)
+        assert ld == Cout
+        L.call("edet_stem_wgrad", eng.dt, vp(x), B, H, W, vp(d), Cout, vp(P.grad(wname)), stream())
+
+    eng.record(bwd)
+    return out
+
+
+# --------------------------------------------------------------------------- 1x1 conv
+def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optional[str] = None,
+            bns: Optional[List[BNParam]] = None, act: int = L.ACT_NONE, ldy: Optional[int] = None,
+            out_buf: Optional[torch.Tensor] = None, name: str = "") -> Act:
+    """y = v(x) @ W^T (+ b); output is lazy BN/act when ``bns`` given.  W stored [N][K]."""
+    K = x.C
+    ldy = N if ldy is None else ldy
+    y = out_buf if out_buf is not None else eng.empty(x.pyr.rows, ldy)
+    bias = P.view(bname) if bname else None
+    L.call("edet_conv1x1_fwd", eng.dt, x.lazy(), x.pyr.c, K, vp(P.wcv(wname)), N, vp(bias), vp(y), ldy, 0,
+           _stats_out(eng, bns), stream())
+    out = Act(y, x.pyr, N, bns, act, ld=ldy, training=eng.training, name=name)
+
+    def bwd():
+        rec = eng.tape.take(out)
+        if rec is None:
+            return
+        d, ld = value_grad_to_raw(eng, out, rec)
+        s = stream()
+        L.call("edet_conv1x1_wgrad", eng.dt, x.lazy(), x.pyr.c, K, vp(d), ld, N, vp(P.grad(wname)),
+               vp(P.grad(bname) if bname else None), s)
+        dx, acc = eng.tape.dst(x)
+        L.call("edet_conv1x1_dgrad", eng.dt, vp(d), ld, x.pyr.c, N, vp(P.wcv(wname)), K, vp(dx), K, acc, s)
+
+    eng.record(bwd)
+    return out
+
+
+# --------------------------------------------------------------------------- depthwise
+def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
+           bns: Optional[List[BNParam]] = None, act: int = L.ACT_NONE, name: str = "") -> Act:
+    C = x.C
+    pout = x.pyr.strided(stride)
+    y = eng.empty(pout.rows, C)
+    L.call("edet_dwconv_fwd", eng.dt, x.lazy(), x.pyr.c, C, k, stride, vp(P.wcv(wname)), vp(y), pout.c,
+           _stats_out(eng, bns), stream())
+    out = Act(y, pout, C, bns, act, training=eng.training, name=name)
+
+    def bwd():
+        rec = eng.tape.take(out)
+        if rec is None:
+            return
+        d, ld = value_grad_to_raw(eng, out, rec)
+        assert ld == C
+        s = stream()
+        L.call("edet_dwconv_wgrad", eng.dt, x.lazy(), x.pyr.c, C, k, stride, vp(d), pout.c, vp(P.grad(wname)), s)
+        dx, acc = eng.tape.dst(x)
+        L.call("edet_dwconv_dgrad", eng.dt, vp(d), pout.c, C, k, stride, vp(P.wcv(wname)), vp(dx), x.pyr.c, acc, s)
+
+    eng.record(bwd)
+    return out
+
+
+# --------------------------------------------------------------------------- SE
+def squeeze_excite(eng: Engine, P: ParamStore, x: Act, prefix: str, R: int):
+    """Attach the SE gate to x (the swish(BN(dw)) value) in place: v -> v * sigmoid(...)."""
+    assert x.pyr.nseg == 1 and x.gate is None
+    B, C = x.pyr.batch, x.C
+    HW = x.pyr.H * x.pyr.W
+    s = stream()
+    svec = eng.zeros_f32(B, C)
+    L.call("edet_se_squeeze", eng.dt, x.lazy(), B, HW, C, vp(svec), s)
+    z1 = torch.empty((B, R), dtype=torch.float32, device=eng.device)
+    gate = torch.empty((B, C), dtype=torch.float32, device=eng.device)
+    w1, b1 = P.view(prefix + "/conv2d/kernel"), P.view(prefix + "/conv2d/bias")
+    w2, b2 = P.view(prefix + "/conv2d_1/kernel"), P.view(prefix + "/conv2d_1/bias")
+    L.call("edet_se_fwd", B, C, R, vp(svec), vp(w1), vp(b1), vp(w2), vp(b2), vp(z1), vp(gate), s)
+    rec = SERec(svec, z1, gate, w1, b1, w2, b2, P.grad(prefix + "/conv2d/kernel"), P.grad(prefix + "/conv2d/bias"),
+                P.grad(prefix + "/conv2d_1/kernel"), P.grad(prefix + "/conv2d_1/bias"), R)
+    x.set_gate(gate, rec)
+    return x
+
+
+# --------------------------------------------------------------------------- resampling
+def maxpool(eng: Engine, x: Act, name: str = "") -> Act:
+    assert x.pyr.nseg == 1
+    B, H, W, C = x.pyr.batch, x.pyr.H, x.pyr.W, x.C
+    pout = x.pyr.strided(2)
+    y = eng.empty(pout.rows, C)
+    L.call("edet_maxpool_fwd", eng.dt, x.lazy(), B, H, W, C, vp(y), stream())
+    out = Act(y, pout, C, training=eng.training, name=name)
+
+    def bwd():
+        rec = eng.tape.take(out)
+        if rec is None:
+            return
+        dx, acc = eng.tape.dst(x)
+        L.call("edet_maxpool_bwd", eng.dt, x.lazy(), B, H, W, C, vp(rec.t), vp(dx), acc, stream())
+
+    eng.record(bwd)
+    return out
+
+
+def bifpn_fuse(eng: Engine, P: ParamStore, inputs: Sequence[Tuple[Act, int]], wnames: Sequence[str],
+               H: int, W: int, name: str = "") -> Act:
+    """sum_i R_i(v_i) * w_i / (sum w + 1e-4); returned lazily as swish(sum) (OpAfterCombine)."""
+    n = len(inputs)
+    C = inputs[0][0].C
+    B = inputs[0][0].pyr.batch
+    wvec = P.view(wnames[0])  # the node's WSM_0..WSM_{n-1} scalars as one [n] parameter
+    assert wvec.numel() == n
+    fi = (L.FuseInput * n)()
+    for i, (a, mode) in enumerate(inputs):
+        assert a.pyr.nseg == 1 and a.C == C
+        fi[i].v = a.lazy()
+        fi[i].H, fi[i].W, fi[i].mode = a.pyr.H, a.pyr.W, mode
+    pyr = Pyr(B, [(H, W)])
+    y = eng.empty(pyr.rows, C)
+    L.call("edet_bifpn_fuse_fwd", eng.dt, n, fi, vp(wvec), B, H, W, C, vp(y), stream())
+    out = Act(y, pyr, C, None, L.ACT_SWISH, training=eng.training, name=name)
+
+    def bwd():
+        rec = eng.tape.take(out)
+        if rec is None:
+            return
+        dF, _ = value_grad_to_raw(eng, out, rec)
+        fb = (L.FuseInput * n)()
+        for i, (a, mode) in enumerate(inputs):
+            dx, acc = eng.tape.dst(a)
+            fb[i].v = a.lazy()
+            fb[i].H, fb[i].W, fb[i].mode = a.pyr.H, a.pyr.W, mode
+            fb[i].dx = dx.data_ptr()
+            fb[i].accumulate = acc
+        L.call("edet_bifpn_fuse_bwd", eng.dt, n, fb, vp(wvec), B, H, W, C, vp(y), vp(dF),
+               vp(P.grad(wnames[0])), stream())
+
+    eng.record(bwd)
+    return out
+
+
+# --------------------------------------------------------------------------- heads
+def residual(eng: Engine, x: Act, res: Act, scale: Optional[torch.Tensor], name: str = "") -> Act:
+    """out = v(x) * scale[level][image] + v(res)  (drop-connect survival scale, 1 at inference)."""
+    C = x.C
+    y = eng.empty(x.pyr.rows, C)
+    L.call("edet_residual_fwd", eng.dt, x.lazy(), res.lazy(), x.pyr.c, C, vp(scale), vp(y), stream())
+    out = Act(y, x.pyr, C, training=eng.training, name=name)
+
+    def bwd():
+        rec = eng.tape.take(out)
+        if rec is None:
+            return
+        # d v(x) = dout * scale ; d v(res) = dout (aliased: x's backward reads it before res's
+        # remaining consumer accumulates into it — x is produced from res)
+        eng.tape.alias(x, rec.t, rec.ld, scale)
+        eng.tape.alias(res, rec.t, rec.ld)
+
+    eng.record(bwd)
+    return out
+
+
+def assemble_pyramid(eng: Engine, buf: torch.Tensor, pyr: Pyr, parts: Sequence[Act], bns: List[BNParam],
+                     name: str = "") -> Act:
+    """The last BiFPN cell writes its five node outputs into one pyramid buffer; this op is
+    the (copy-free) join and, backwards, the split of the pyramid gradient into views."""
+    C = parts[0].C
+    out = Act(buf, pyr, C, bns, L.ACT_NONE, training=eng.training, name=name)
+
+    def bwd():
+        rec = eng.tape.take(out)
+        if rec is None:
+            return
+        assert rec.ld == C and rec.scale is None
+        for s, a in enumerate(parts):
+            eng.tape.alias(a, rec.t[pyr.seg_slice(s)], C)
+
+    eng.record(bwd)
+    return out

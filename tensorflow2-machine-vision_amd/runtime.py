@@ -1,0 +1,424 @@
+"""Host runtime for the EfficientDet hot path: buffers, lazy activations, parameters, tape.
+
+Design:
+  * Every activation is an ``Act``: a raw NHWC buffer ``[rows][ld]`` plus an optional
+    *pending* per-channel transform ``v = act(bn(raw)) * gate`` that consumers apply while
+    loading.  Training-mode BatchNorm therefore never runs as its own forward pass: the
+    producing kernel emits per-channel sums, the consuming kernel normalises.
+  * ``Pyr`` is the row layout of an activation: one segment for a plain tensor, five for the
+    P3..P7 feature pyramid the heads run over in single launches.
+  * ``ParamStore`` keeps every trainable variable in one flat fp32 buffer (master weights),
+    a flat gradient buffer (one all-reduce for data parallelism), momentum / EMA slots and a
+    compute-dtype copy for the kernels; BN moving statistics and per-step batch statistics
+    live in their own flat arenas so each is zeroed / updated by one launch.
+  * ``Tape`` records one backward closure per forward op (explicit reverse-mode AD on the
+    static EfficientDet graph; no torch.autograd).  Gradients of an activation accumulate in
+    place through the kernels' ``accumulate`` flag.
+
+PyTorch is used only for device memory (caching allocator) and streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+ROW_ALIGN = 128  # segment starts of a pyramid buffer (GEMM row tiles never straddle levels)
+PARAM_ALIGN = 64  # elements; keeps every weight view 256-B aligned
+
+
+def _vp(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def round_up(x: int, a: int) -> int:
+    return (x + a - 1) // a * a
+
+
+# --------------------------------------------------------------------------- layout
+class Pyr:
+    """Row layout: segment s holds batch*H*W rows starting at a 128-aligned offset."""
+
+    def __init__(self, batch: int, sizes: Sequence[Tuple[int, int]]):
+        assert 1 <= len(sizes) <= L.MAX_SEG
+        self.batch = int(batch)
+        self.sizes = [(int(h), int(w)) for h, w in sizes]
+        self.nseg = len(self.sizes)
+        self.row_off: List[int] = []
+        off = 0
+        for h, w in self.sizes:
+            self.row_off.append(off)
+            off = round_up(off + self.batch * h * w, ROW_ALIGN)
+        self.rows = self.row_off[-1] + self.seg_rows(self.nseg - 1)
+        c = L.Pyramid()
+        c.nseg, c.batch = self.nseg, self.batch
+        for i, (h, w) in enumerate(self.sizes):
+            c.row_off[i], c.H[i], c.W[i] = self.row_off[i], h, w
+        self.c = c
+
+    def seg_rows(self, s: int) -> int:
+        h, w = self.sizes[s]
+        return self.batch * h * w
+
+    def seg_slice(self, s: int) -> slice:
+        return slice(self.row_off[s], self.row_off[s] + self.seg_rows(s))
+
+    def strided(self, s: int) -> "Pyr":
+        return Pyr(self.batch, [((h + s - 1) // s, (w + s - 1) // s) for h, w in self.sizes])
+
+    @property
+    def H(self):
+        assert self.nseg == 1
+        return self.sizes[0][0]
+
+    @property
+    def W(self):
+        assert self.nseg == 1
+        return self.sizes[0][1]
+
+    def __repr__(self):
+        return f"Pyr(batch={self.batch}, sizes={self.sizes})"
+
+
+# --------------------------------------------------------------------------- BN
+class BNParam:
+    """One Keras BatchNormalization (momentum 0.99, eps 1e-3 by default)."""
+
+    def __init__(self, name: str, C: int, momentum: float, eps: float):
+        self.name, self.C, self.momentum, self.eps = name, C, momentum, eps
+        self.gamma = self.beta = self.dgamma = self.dbeta = None
+        self.mmean = self.mvar = self.count = None
+        self.tsum = self.tsq = None    # batch statistics (training)
+        self.isum = self.isq = None    # moving statistics as sums (inference)
+
+    def stats(self, training: bool):
+        return (self.tsum, self.tsq) if training else (self.isum, self.isq)
+
+
+# --------------------------------------------------------------------------- activations
+class SERec:
+    """Saved state of one squeeze-excitation (layers/se.py) for its backward."""
+
+    def __init__(self, s, z1, gate, w1, b1, w2, b2, dw1, db1, dw2, db2, R):
+        self.s, self.z1, self.gate = s, z1, gate
+        self.w1, self.b1, self.w2, self.b2 = w1, b1, w2, b2
+        self.dw1, self.db1, self.dw2, self.db2 = dw1, db1, dw2, db2
+        self.R = R
+
+
+class Act:
+    """Raw activation buffer + pending transform v = act(bn(raw)) * gate."""
+
+    __slots__ = ("raw", "pyr", "C", "ld", "bns", "act", "gate", "se", "training", "name", "_lz")
+
+    def __init__(self, raw: torch.Tensor, pyr: Pyr, C: int, bns: Optional[List[BNParam]] = None,
+                 act: int = L.ACT_NONE, ld: Optional[int] = None, training: bool = False,
+                 name: str = ""):
+        self.raw, self.pyr, self.C = raw, pyr, C
+        self.ld = C if ld is None else ld
+        assert raw.dim() == 2 and raw.shape[0] >= pyr.rows and raw.shape[1] == self.ld, (raw.shape, pyr.rows, self.ld)
+        self.bns = bns
+        if bns is not None:
+            assert len(bns) == pyr.nseg
+        self.act, self.gate, self.se = act, None, None
+        self.training, self.name = training, name
+        self._lz = None
+
+    @property
+    def has_transform(self) -> bool:
+        return self.bns is not None or self.act != L.ACT_NONE or self.gate is not None
+
+    def set_gate(self, gate: torch.Tensor, se: SERec):
+        self.gate, self.se, self._lz = gate, se, None
+
+    def lazy(self) -> L.Lazy:
+        if self._lz is None:
+            lz = L.Lazy()
+            lz.x = self.raw.data_ptr()
+            lz.gate = self.gate.data_ptr() if self.gate is not None else None
+            lz.ld = self.ld
+            lz.act = self.act
+            if self.bns is not None:
+                lz.bn.enabled = 1
+                lz.bn.eps = self.bns[0].eps
+                for s, bn in enumerate(self.bns):
+                    ssum, ssq = bn.stats(self.training)
+                    lz.bn.sum[s] = ssum.data_ptr()
+                    lz.bn.sq[s] = ssq.data_ptr()
+                    lz.bn.gamma[s] = bn.gamma.data_ptr()
+                    lz.bn.beta[s] = bn.beta.data_ptr()
+            self._lz = lz
+        return self._lz
+
+    def seg_view(self, s: int) -> torch.Tensor:
+        return self.raw[self.pyr.seg_slice(s), : self.C]
+
+    def __repr__(self):
+        return f"Act({self.name}, C={self.C}, {self.pyr})"
+
+
+def seg_out(pairs: Sequence[Tuple[torch.Tensor, torch.Tensor]]) -> L.SegOut:
+    so = L.SegOut()
+    for i, (a, b) in enumerate(pairs):
+        so.a[i] = a.data_ptr()
+        so.b[i] = b.data_ptr()
+    return so
+
+
+# --------------------------------------------------------------------------- parameters
+class ParamSpec:
+    __slots__ = ("name", "shape", "init", "l2", "offset", "size")
+
+    def __init__(self, name, shape, init, l2):
+        self.name, self.shape, self.init, self.l2 = name, tuple(shape), init, l2
+        self.size = int(np.prod(self.shape))
+        self.offset = -1
+
+
+class ParamStore:
+    """Flat fp32 master weights / grads / momentum / EMA + compute-dtype copy + BN arenas.
+
+    Variables matching the reference's L2 regex (``.*(kernel|weight):0$``,
+    efficientdet_net_train.py:21) are laid out first so the fused optimizer applies the
+    4e-5 * w gradient term to one prefix.
+    """
+
+    def __init__(self):
+        self.specs: Dict[str, ParamSpec] = {}
+        self.order: List[str] = []
+        self.bns: List[BNParam] = []
+        self.finalized = False
+
+    # ---- registration
+    def add(self, name: str, shape, init, l2: bool) -> str:
+        assert not self.finalized and name not in self.specs, name
+        self.specs[name] = ParamSpec(name, shape, init, l2)
+        self.order.append(name)
+        return name
+
+    def add_bn(self, name: str, C: int, momentum: float, eps: float) -> BNParam:
+        bn = BNParam(name, C, momentum, eps)
+        self.add(name + "/gamma", (C,), ("const", 1.0), False)
+        self.add(name + "/beta", (C,), ("const", 0.0), False)
+        self.bns.append(bn)
+        return bn
+
+    # ---- allocation
+    def finalize(self, device, compute_dtype: torch.dtype, seed: int = 0):
+        assert not self.finalized
+        names = [n for n in self.order if self.specs[n].l2] + [n for n in self.order if not self.specs[n].l2]
+        off = 0
+        self.n_l2 = 0
+        for n in names:
+            sp = self.specs[n]
+            sp.offset = off
+            off = round_up(off + sp.size, PARAM_ALIGN)
+            if sp.l2:
+                self.n_l2 = off
+        self.numel = off
+        self.n_trainable = sum(sp.size for sp in self.specs.values())
+        host = np.zeros(self.numel, np.float32)
+        rng = np.random.default_rng(seed)
+        for n in self.order:  # init in registration order (deterministic per model)
+            sp = self.specs[n]
+            host[sp.offset: sp.offset + sp.size] = _init_values(sp, rng).reshape(-1)
+        self.device = device
+        self.w = torch.from_numpy(host).to(device)
+        self.g = torch.zeros_like(self.w)
+        self.v = torch.zeros_like(self.w)
+        self.ema = self.w.clone()
+        self.compute_dtype = compute_dtype
+        if compute_dtype == torch.float32:
+            self.wc = self.w
+        else:
+            self.wc = torch.empty(self.numel, dtype=compute_dtype, device=device)
+        # BN arenas
+        nch = sum(bn.C for bn in self.bns)
+        self.n_bn = nch
+        self.bn_mm = torch.zeros(max(nch, 1), device=device)
+        self.bn_mv = torch.ones(max(nch, 1), device=device)
+        self.bn_count = torch.ones(max(nch, 1), device=device)
+        self.bn_tstats = torch.zeros(2, max(nch, 1), device=device)
+        self.bn_istats = torch.zeros(2, max(nch, 1), device=device)
+        o = 0
+        for bn in self.bns:
+            sl = slice(o, o + bn.C)
+            bn.gamma, bn.beta = self.view(bn.name + "/gamma"), self.view(bn.name + "/beta")
+            bn.dgamma, bn.dbeta = self.grad(bn.name + "/gamma"), self.grad(bn.name + "/beta")
+            bn.mmean, bn.mvar, bn.count = self.bn_mm[sl], self.bn_mv[sl], self.bn_count[sl]
+            bn.tsum, bn.tsq = self.bn_tstats[0, sl], self.bn_tstats[1, sl]
+            bn.isum, bn.isq = self.bn_istats[0, sl], self.bn_istats[1, sl]
+            o += bn.C
+        self.finalized = True
+        self.refresh_compute_copy()
+
+    def refresh_compute_copy(self):
+        if self.wc is not self.w:
+            L.call("edet_cast_f32", L.BF16, _vp(self.w), _vp(self.wc), self.numel, stream())
+
+    # ---- views
+    def _sl(self, name):
+        sp = self.specs[name]
+        return slice(sp.offset, sp.offset + sp.size), sp.shape
+
+    def view(self, name) -> torch.Tensor:
+        sl, shape = self._sl(name)
+        return self.w[sl].view(shape)
+
+    def grad(self, name) -> torch.Tensor:
+        sl, shape = self._sl(name)
+        return self.g[sl].view(shape)
+
+    def wcv(self, name) -> torch.Tensor:
+        sl, shape = self._sl(name)
+        return self.wc[sl].view(shape)
+
+    # ---- host round trip (checkpoints, oracle parity)
+    def state_dict(self) -> Dict[str, np.ndarray]:
+        host = self.w.detach().float().cpu().numpy()
+        out = {n: host[self.specs[n].offset: self.specs[n].offset + self.specs[n].size].reshape(self.specs[n].shape).copy()
+               for n in self.order}
+        mm, mv = self.bn_mm.cpu().numpy(), self.bn_mv.cpu().numpy()
+        o = 0
+        for bn in self.bns:
+            out[bn.name + "/moving_mean"] = mm[o:o + bn.C].copy()
+            out[bn.name + "/moving_variance"] = mv[o:o + bn.C].copy()
+            o += bn.C
+        return out
+
+    def load_state_dict(self, sd: Dict[str, np.ndarray]):
+        host = self.w.detach().cpu().numpy().copy()
+        for n in self.order:
+            sp = self.specs[n]
+            a = np.asarray(sd[n], np.float32).reshape(-1)
+            assert a.size == sp.size, (n, a.size, sp.size)
+            host[sp.offset: sp.offset + sp.size] = a
+        self.w.copy_(torch.from_numpy(host))
+        self.ema.copy_(self.w)
+        mm, mv = self.bn_mm.cpu().numpy(), self.bn_mv.cpu().numpy()
+        o = 0
+        for bn in self.bns:
+            if bn.name + "/moving_mean" in sd:
+                mm[o:o + bn.C] = sd[bn.name + "/moving_mean"]
+                mv[o:o + bn.C] = sd[bn.name + "/moving_variance"]
+            o += bn.C
+        self.bn_mm.copy_(torch.from_numpy(mm))
+        self.bn_mv.copy_(torch.from_numpy(mv))
+        self.refresh_compute_copy()
+
+    def grads_dict(self) -> Dict[str, np.ndarray]:
+        host = self.g.detach().cpu().numpy()
+        return {n: host[self.specs[n].offset: self.specs[n].offset + self.specs[n].size].reshape(self.specs[n].shape).copy()
+                for n in self.order}
+
+
+def _init_values(sp: ParamSpec, rng: np.random.Generator) -> np.ndarray:
+    """Reference initialisers."""
+    kind = sp.init[0]
+    shape = sp.shape
+    if kind == "const":
+        return np.full(shape, sp.init[1], np.float32)
+    if kind == "normal":  # utils/conv_kernel_initializer.py: N(0, sqrt(2 / fan_out))
+        return rng.normal(0.0, sp.init[1], size=shape).astype(np.float32)
+    if kind == "glorot":  # keras glorot_uniform: U(-l, l), l = sqrt(6 / (fan_in + fan_out))
+        lim = math.sqrt(6.0 / (sp.init[1] + sp.init[2]))
+        return rng.uniform(-lim, lim, size=shape).astype(np.float32)
+    if kind == "vs_fan_in":  # keras VarianceScaling(): truncated normal, std sqrt(1/fan_in)/0.8796
+        std = math.sqrt(1.0 / sp.init[1]) / 0.87962566103423978
+        v = rng.normal(0.0, std, size=shape)
+        bad = np.abs(v) > 2 * std
+        while bad.any():
+            v[bad] = rng.normal(0.0, std, size=int(bad.sum()))
+            bad = np.abs(v) > 2 * std
+        return v.astype(np.float32)
+    raise ValueError(sp.init)
+
+
+# --------------------------------------------------------------------------- tape
+class GradRec:
+    __slots__ = ("t", "ld", "scale")
+
+    def __init__(self, t: torch.Tensor, ld: int, scale: Optional[torch.Tensor] = None):
+        self.t, self.ld, self.scale = t, ld, scale
+
+
+class Tape:
+    """Explicit reverse-mode AD: one closure per forward op, run in reverse order."""
+
+    def __init__(self, engine: "Engine"):
+        self.eng = engine
+        self.entries: List = []
+        self.g: Dict[Act, GradRec] = {}
+
+    def record(self, fn):
+        self.entries.append(fn)
+
+    def dst(self, act: Act) -> Tuple[torch.Tensor, int]:
+        """Destination for d(value of act): (buffer [rows][C], accumulate flag)."""
+        rec = self.g.get(act)
+        if rec is not None:
+            assert rec.scale is None and rec.ld == act.C, "cannot accumulate into a scaled/strided grad"
+            return rec.t, 1
+        t = self.eng.empty(act.pyr.rows, act.C)
+        self.g[act] = GradRec(t, act.C)
+        return t, 0
+
+    def alias(self, act: Act, t: torch.Tensor, ld: int, scale=None):
+        assert act not in self.g, f"grad of {act} already exists"
+        self.g[act] = GradRec(t, ld, scale)
+
+    def take(self, act: Act) -> Optional[GradRec]:
+        return self.g.pop(act, None)
+
+    def backward(self):
+        entries, self.entries = self.entries, []
+        for fn in reversed(entries):
+            fn()
+        self.g.clear()
+
+
+# --------------------------------------------------------------------------- engine
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Engine:
+    """Per-model execution context: compute dtype, device, training flag, tape."""
+
+    def __init__(self, dtype: str, device):
+        assert dtype in ("bf16", "f32")
+        self.dt = L.BF16 if dtype == "bf16" else L.F32
+        self.tdtype = torch.bfloat16 if dtype == "bf16" else torch.float32
+        self.device = torch.device(device)
+        self.training = False
+        self.tape: Optional[Tape] = None
+
+    def empty(self, rows: int, C: int, dtype=None) -> torch.Tensor:
+        return torch.empty((rows, C), dtype=dtype or self.tdtype, device=self.device)
+
+    def zeros_f32(self, *shape) -> torch.Tensor:
+        t = torch.empty(shape, dtype=torch.float32, device=self.device)
+        memset0(t)
+        return t
+
+    def record(self, fn):
+        if self.training and self.tape is not None:
+            self.tape.record(fn)
+
+
+def memset0(t: torch.Tensor):
+    L.call("edet_memset_async", _vp(t), 0, t.numel() * t.element_size(), stream())
+
+
+def memcpy(dst: torch.Tensor, src: torch.Tensor):
+    n = src.numel() * src.element_size()
+    assert dst.numel() * dst.element_size() >= n
+    L.call("edet_memcpy_async", _vp(dst), _vp(src), n, stream())
+
+
+vp = _vp

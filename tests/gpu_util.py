@@ -1,0 +1,92 @@
+"""Helpers for the GPU parity tests: descriptors for raw tensors and CPU fp64 references."""
+import ctypes
+
+import numpy as np
+import torch
+
+from tf2mv_amd import _lib as L
+from tf2mv_amd.runtime import Pyr, stream, vp
+
+DEV = "cuda"
+TDT = {"f32": torch.float32, "bf16": torch.bfloat16}
+DT = {"f32": L.F32, "bf16": L.BF16}
+TOL = {"f32": dict(rtol=2e-5, atol=2e-5), "bf16": dict(rtol=3e-2, atol=3e-2)}
+
+
+def g(t, dt="f32"):
+    return t.to(DEV, TDT[dt]).contiguous()
+
+
+class LazyDesc:
+    """Lazy value spec + its CPU fp64 evaluation."""
+
+    def __init__(self, x, pyr: Pyr, C, bn=None, act=0, gate=None, eps=1e-3, ld=None):
+        # x: device tensor [rows, ld];  bn: list per seg of (sum, sq, gamma, beta) device fp32
+        self.x, self.pyr, self.C, self.bn, self.act, self.gate, self.eps = x, pyr, C, bn, act, gate, eps
+        self.ld = ld or C
+        lz = L.Lazy()
+        lz.x = x.data_ptr()
+        lz.gate = gate.data_ptr() if gate is not None else None
+        lz.ld, lz.act = self.ld, act
+        if bn:
+            lz.bn.enabled = 1
+            lz.bn.eps = eps
+            for s, (a, b, c, d) in enumerate(bn):
+                lz.bn.sum[s], lz.bn.sq[s], lz.bn.gamma[s], lz.bn.beta[s] = a.data_ptr(), b.data_ptr(), c.data_ptr(), d.data_ptr()
+        self.c = lz
+
+    def cpu_value(self):
+        x = self.x[:, : self.C].double().cpu()
+        out = x.clone()
+        for s in range(self.pyr.nseg):
+            sl = self.pyr.seg_slice(s)
+            v = x[sl]
+            if self.bn:
+                su, sq, ga, be = (t.double().cpu() for t in self.bn[s])
+                n = self.pyr.seg_rows(s)
+                mean = su / n
+                var = torch.clamp(sq / n - mean * mean, min=0)
+                v = (v - mean) / torch.sqrt(var + self.eps) * ga + be
+            if self.act:
+                v = v * torch.sigmoid(v)
+            if self.gate is not None:
+                hw = self.pyr.sizes[s][0] * self.pyr.sizes[s][1]
+                gt = self.gate.double().cpu()
+                v = v * gt.repeat_interleave(hw, 0)
+            out[sl] = v
+        return out
+
+
+def make_bn(x, pyr: Pyr, C, rng, shift=0.0):
+    """Random BN params and *exact* batch stats of x per segment (fp32 device)."""
+    segs = []
+    xc = x[:, :C].double().cpu()
+    for s in range(pyr.nseg):
+        v = xc[pyr.seg_slice(s)]
+        su = v.sum(0).float().to(DEV)
+        sq = (v * v).sum(0).float().to(DEV)
+        ga = torch.tensor(rng.uniform(0.5, 1.5, C), dtype=torch.float32, device=DEV)
+        be = torch.tensor(rng.uniform(-0.5, 0.5, C) + shift, dtype=torch.float32, device=DEV)
+        segs.append((su, sq, ga, be))
+    return segs
+
+
+def seg_out(pairs):
+    so = L.SegOut()
+    for i, (a, b) in enumerate(pairs):
+        so.a[i], so.b[i] = a.data_ptr(), b.data_ptr()
+    return so
+
+
+def zeros(*shape):
+    return torch.zeros(shape, dtype=torch.float32, device=DEV)
+
+
+def close(a, b, dt, scale=None, **kw):
+    a = a.double().cpu() if isinstance(a, torch.Tensor) else torch.as_tensor(a, dtype=torch.float64)
+    b = b.double().cpu() if isinstance(b, torch.Tensor) else torch.as_tensor(b, dtype=torch.float64)
+    tol = dict(TOL[dt])
+    tol.update(kw)
+    if scale is not None:
+        tol["atol"] = tol["atol"] * scale
+    torch.testing.assert_close(a, b, **tol)

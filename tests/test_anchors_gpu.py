@@ -1,0 +1,76 @@
+"""Rows a18-a20 on the GPU: anchors bit-exact, targets' masks/indices bit-exact, encoded and
+decoded boxes within 2 ulp-level tolerance (transcendentals) of the numpy oracle."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_anchors as RA
+from tf2mv_amd.anchors import Anchors
+
+pytestmark = pytest.mark.gpu
+ASPECTS = [(1.0, 1.0), (1.4, 0.7), (0.7, 1.4)]
+
+
+@pytest.mark.parametrize("args", [(0, 0, (10, 10), 3, [(1.0, 1.0)], 3.0), (3, 7, (512, 512), 3, ASPECTS, 4.0),
+                                  (3, 7, (640, 640), 3, ASPECTS, 4.0), (3, 7, (128, 128), 3, ASPECTS, 4.0)])
+def test_anchor_boxes_bit_exact(args):
+    a = Anchors(*args)
+    ref = RA.generate_boxes(*args)
+    for got, want in zip(a.boxes, ref):
+        np.testing.assert_array_equal(got.cpu().numpy(), want)
+
+
+def synthetic_gt(rng, B, G, size):
+    boxes = np.zeros((B, G, 4), np.float32)
+    cls = np.zeros((B, G), np.int32)
+    n = rng.integers(1, G + 1, B).astype(np.int32)
+    for b in range(B):
+        for k in range(n[b]):
+            s = np.exp(rng.uniform(np.log(16), np.log(size * 0.8)))
+            ar = rng.uniform(0.5, 2.0)
+            h, w = s * np.sqrt(ar), s / np.sqrt(ar)
+            cy, cx = rng.uniform(0, size, 2)
+            boxes[b, k] = [cy - h / 2, cx - w / 2, cy + h / 2, cx + w / 2]
+            cls[b, k] = rng.integers(1, 81)
+    return boxes.astype(np.float32), cls, n
+
+
+@pytest.mark.parametrize("size,B", [(128, 3), (512, 2)])
+def test_generate_targets_and_decode(size, B):
+    rng = np.random.default_rng(size)
+    a = Anchors(3, 7, (size, size), 3, ASPECTS, 4.0)
+    ref_levels = RA.generate_boxes(3, 7, (size, size), 3, ASPECTS, 4.0)
+    G = 9
+    boxes, cls, n = synthetic_gt(rng, B, G, size)
+    # add the test_anchors style exact hit: a GT equal to an anchor
+    boxes[0, 0] = ref_levels[0][3, 5, 4]
+    t = a.generate_targets_batched(torch.tensor(boxes), torch.tensor(cls), torch.tensor(n))
+    pyr = t.pyr
+    tb, tc, tm = t.box.cpu().numpy(), t.cls.cpu().numpy(), t.mask.cpu().numpy()
+    npos = 0
+    for b in range(B):
+        ob, oc, om, oi = RA.generate_targets(ref_levels, boxes[b, : n[b]], cls[b, : n[b]], 81)
+        for s, (H, W) in enumerate(a.level_sizes):
+            sl = pyr.seg_slice(s)
+            rows = slice(sl.start + b * H * W, sl.start + (b + 1) * H * W)
+            np.testing.assert_array_equal(tm[rows].reshape(H, W, 9), om[s][..., 0].astype(np.uint8))
+            np.testing.assert_array_equal(tc[rows].reshape(H, W, 9), oi[s])
+            np.testing.assert_allclose(tb[rows].reshape(H, W, 9, 4), ob[s], rtol=2e-6, atol=1e-6)
+            npos += int(om[s].sum())
+    assert npos > 0
+    # decode of the encoded targets returns the GT box of every positive anchor (a20)
+    dec = a.convert_outputs_boxes(t.box.view(pyr.rows, 36), pyr=pyr, ld=36)
+    for s, (H, W) in enumerate(a.level_sizes):
+        d = dec[s].cpu().numpy()
+        enc = tb[pyr.seg_slice(s)].reshape(B, H, W, 9, 4)
+        want = RA.decode(ref_levels[s][None], enc)
+        np.testing.assert_allclose(d, want, rtol=1e-5, atol=1e-3)
+
+
+def test_reference_format_roundtrip():
+    rng = np.random.default_rng(1)
+    a = Anchors(0, 0, (10, 10), 3, [(1.0, 1.0)], 3.0)
+    ob, oc, om = a.generate_targets(torch.tensor([[3, 3, 6, 6], [5, 5, 9, 9]], dtype=torch.float32),
+                                    torch.tensor([1, 2]), 3)
+    assert bool(om[0][4, 4, 0, 0]) and oc[0][4, 4, 0].tolist() == [0, 1, 0]
+    assert ob[0][4, 4, 0].abs().max().item() == 0.0

@@ -1,0 +1,46 @@
+"""The C-ABI library loads and exports every symbol include/edet.h declares (no GPU calls)."""
+import ctypes
+import os
+import re
+
+from tf2mv_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "edet.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(edet_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_every_header_symbol_is_exported_and_bound():
+    fns = header_functions()
+    assert len(fns) >= 30
+    dll = ctypes.CDLL(_lib.LIB_PATH)
+    for f in fns:
+        assert hasattr(dll, f), f"libedet.so does not export {f}"
+    assert set(fns) == set(_lib.SIGNATURES), set(fns) ^ set(_lib.SIGNATURES)
+
+
+def test_struct_layouts_match_header():
+    # sizes follow from the C layout rules for the declared field order
+    assert ctypes.sizeof(_lib.Pyramid) == 4 * (2 + 3 * 5)
+    assert ctypes.sizeof(_lib.BN) == 8 * 20 + 8
+    assert ctypes.sizeof(_lib.Lazy) == 8 + 8 + ctypes.sizeof(_lib.BN) + 8
+    assert ctypes.sizeof(_lib.FuseInput) == ctypes.sizeof(_lib.Lazy) + 8 + 16
+    assert ctypes.sizeof(_lib.Sched) == 40
+
+
+def test_error_path_without_gpu():
+    lib = _lib.lib()
+    assert lib.fns["edet_abi_version"]() == 1
+    # argument validation happens before any HIP call
+    rc = lib.fns["edet_conv1x1_fwd"](0, None, None, 8, None, 8, None, None, 8, 0, None, None)
+    assert rc == -1 and "null" in lib.last_error()
+    try:
+        lib.call("edet_dwconv_fwd", 0, None, None, 8, 3, 1, None, None, None, None, None)
+    except _lib.EdetError as e:
+        assert "dwconv_fwd" in str(e)
+    else:
+        raise AssertionError("expected EdetError")

@@ -1,0 +1,481 @@
+"""Per-kernel parity: libedet (HIP, through the C-ABI) vs fp64 torch-CPU references.
+
+fp32 storage must match to ~1e-5; bf16 storage to bf16 rounding (3e-2 relative on O(1)
+values).  Shapes include ragged sizes, odd spatial extents (TF SAME asymmetric padding),
+channel counts that are not tile multiples and 2-segment pyramids with padding rows.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as Fn
+
+from tf2mv_amd import _lib as L
+from tf2mv_amd.runtime import Pyr, stream, vp
+from gpu_util import DEV, DT, TDT, LazyDesc, close, g, make_bn, seg_out, zeros
+
+pytestmark = pytest.mark.gpu
+DTS = ["f32", "bf16"]
+
+
+def rnd(rng, *shape, scale=1.0):
+    return torch.tensor(rng.standard_normal(shape) * scale, dtype=torch.float32)
+
+
+def pyr_data(rng, pyr, C, dt, scale=1.0):
+    x = rnd(rng, pyr.rows, C, scale=scale)
+    return g(x, dt)
+
+
+# ----------------------------------------------------------------- conv1x1
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("M,K,N,lazy,nseg", [(300, 24, 40, 0, 1), (1000, 96, 144, 1, 1), (777, 64, 729, 2, 1),
+                                            (513, 40, 64, 3, 2), (4096, 192, 1152, 1, 1)])
+def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
+    rng = np.random.default_rng(M + K + N)
+    pyr = Pyr(2, [(13, 11), (7, 5)]) if nseg == 2 else Pyr(1, [(M, 1)])
+    x = pyr_data(rng, pyr, K, dt)
+    bn = make_bn(x, pyr, K, rng) if lazy else None
+    gate = g(torch.rand(pyr.batch, K), "f32") if lazy == 1 else None
+    lz = LazyDesc(x, pyr, K, bn=bn, act=1 if lazy in (1, 3) else 0, gate=gate)
+    w = g(rnd(rng, N, K, scale=1 / math.sqrt(K)), dt)
+    b = g(rnd(rng, N), "f32")
+    y = torch.empty(pyr.rows, N, dtype=TDT[dt], device=DEV)
+    st = [(zeros(N), zeros(N)) for _ in range(nseg)]
+    L.call("edet_conv1x1_fwd", DT[dt], lz.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, seg_out(st), stream())
+    ref = lz.cpu_value() @ w.double().cpu().t() + b.double().cpu()
+    for s in range(nseg):
+        sl = pyr.seg_slice(s)
+        close(y[sl], ref[sl], dt)
+        close(st[s][0], ref[sl].sum(0), dt, scale=pyr.seg_rows(s) ** 0.5 * 4)
+        close(st[s][1], (ref[sl] ** 2).sum(0), dt, scale=pyr.seg_rows(s) ** 0.5 * 8, rtol=5e-2 if dt == "bf16" else 1e-4)
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("M,N,K,ldy", [(300, 40, 24, 40), (777, 729, 64, 736), (2048, 1152, 192, 1152)])
+def test_conv1x1_dgrad(dt, M, N, K, ldy):
+    rng = np.random.default_rng(M * 7 + N)
+    pyr = Pyr(1, [(M, 1)])
+    dy = torch.zeros(M, ldy)
+    dy[:, :N] = rnd(rng, M, N)
+    dy = g(dy, dt)
+    w = g(rnd(rng, N, K, scale=1 / math.sqrt(N)), dt)
+    dx = g(torch.full((M, K), 0.5), dt)
+    L.call("edet_conv1x1_dgrad", DT[dt], vp(dy), ldy, pyr.c, N, vp(w), K, vp(dx), K, 1, stream())
+    ref = dy[:, :N].double().cpu() @ w.double().cpu() + 0.5
+    close(dx, ref, dt)
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("K,N,lazy,nseg", [(24, 40, 0, 1), (96, 144, 1, 1), (64, 729, 0, 2), (40, 64, 2, 2)])
+def test_conv1x1_wgrad(dt, K, N, lazy, nseg):
+    rng = np.random.default_rng(K * 13 + N)
+    pyr = Pyr(3, [(17, 9), (5, 3)]) if nseg == 2 else Pyr(2, [(37, 29)])
+    x = pyr_data(rng, pyr, K, dt)
+    # poison padding rows: they must be ignored
+    x[pyr.seg_rows(0):pyr.row_off[-1]] = float("nan")
+    bn = make_bn(x.nan_to_num(0.0), pyr, K, rng) if lazy else None
+    gate = g(torch.rand(pyr.batch, K), "f32") if (lazy == 1 and nseg == 1) else None
+    lz = LazyDesc(x, pyr, K, bn=bn, act=1 if lazy else 0, gate=gate)
+    ld = N if N % 8 == 0 else N + (8 - N % 8)
+    dy = torch.zeros(pyr.rows, ld)
+    dy[:, :N] = rnd(rng, pyr.rows, N)
+    dy = g(dy, dt)
+    dy[pyr.seg_rows(0):pyr.row_off[-1]] = float("nan")
+    dw = zeros(N, K)
+    db = zeros(N)
+    L.call("edet_conv1x1_wgrad", DT[dt], lz.c, pyr.c, K, vp(dy), ld, N, vp(dw), vp(db), stream())
+    v = lz.cpu_value()
+    d = dy[:, :N].double().cpu()
+    refw = torch.zeros(N, K, dtype=torch.float64)
+    refb = torch.zeros(N, dtype=torch.float64)
+    for s in range(nseg):
+        sl = pyr.seg_slice(s)
+        refw += d[sl].t() @ v[sl]
+        refb += d[sl].sum(0)
+    close(dw, refw, dt, scale=pyr.rows ** 0.5 * 2)
+    close(db, refb, dt, scale=pyr.rows ** 0.5 * 2)
+
+
+# ----------------------------------------------------------------- depthwise
+def dw_ref(v, pyr_in, k, s, w):  # v: fp64 [rows, C] values; returns [rows_out, C]
+    outs = []
+    C = v.shape[1]
+    pout = pyr_in.strided(s)
+    res = torch.zeros(pout.rows, C, dtype=torch.float64)
+    for sg in range(pyr_in.nseg):
+        H, W = pyr_in.sizes[sg]
+        xi = v[pyr_in.seg_slice(sg)].view(pyr_in.batch, H, W, C).permute(0, 3, 1, 2)
+        OH, OW = (H + s - 1) // s, (W + s - 1) // s
+        ph = max((OH - 1) * s + k - H, 0)
+        pw = max((OW - 1) * s + k - W, 0)
+        xi = Fn.pad(xi, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2))
+        wt = w.t().reshape(C, 1, k, k)
+        y = Fn.conv2d(xi, wt, stride=s, groups=C)
+        res[pout.seg_slice(sg)] = y.permute(0, 2, 3, 1).reshape(-1, C)
+    return res
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("k,s,H,W,C,lazy,nseg", [(3, 1, 16, 16, 32, 0, 1), (3, 2, 17, 13, 96, 1, 1),
+                                                 (5, 2, 20, 9, 144, 1, 1), (5, 1, 11, 12, 40, 2, 1),
+                                                 (3, 1, 9, 9, 64, 3, 2)])
+def test_dwconv_fwd_bwd(dt, k, s, H, W, C, lazy, nseg):
+    rng = np.random.default_rng(k * 100 + s * 10 + H)
+    B = 2
+    pin = Pyr(B, [(H, W), ((H + 1) // 2, (W + 1) // 2)]) if nseg == 2 else Pyr(B, [(H, W)])
+    pout = pin.strided(s)
+    x = pyr_data(rng, pin, C, dt)
+    bn = make_bn(x, pin, C, rng) if lazy else None
+    gate = g(torch.rand(B, C), "f32") if lazy == 1 else None
+    lz = LazyDesc(x, pin, C, bn=bn, act=1 if lazy in (1, 3) else 0, gate=gate)
+    w = g(rnd(rng, k * k, C, scale=0.3), dt)
+    y = torch.empty(pout.rows, C, dtype=TDT[dt], device=DEV)
+    st = [(zeros(C), zeros(C)) for _ in range(nseg)]
+    L.call("edet_dwconv_fwd", DT[dt], lz.c, pin.c, C, k, s, vp(w), vp(y), pout.c, seg_out(st), stream())
+    v = lz.cpu_value().requires_grad_(True)
+    wr = w.double().cpu().requires_grad_(True)
+    ref = dw_ref(v, pin, k, s, wr)
+    for sg in range(nseg):
+        sl = pout.seg_slice(sg)
+        close(y[sl], ref[sl].detach(), dt)
+        close(st[sg][0], ref[sl].detach().sum(0), dt, scale=pout.seg_rows(sg) ** 0.5 * 4)
+    # backward
+    dy = pyr_data(rng, pout, C, dt)
+    dyc = dy.double().cpu()
+    mask = torch.zeros(pout.rows, 1, dtype=torch.float64)
+    for sg in range(nseg):
+        mask[pout.seg_slice(sg)] = 1
+    (ref * dyc * mask).sum().backward()
+    dx = g(torch.full((pin.rows, C), 0.25), dt)
+    L.call("edet_dwconv_dgrad", DT[dt], vp(dy), pout.c, C, k, s, vp(w), vp(dx), pin.c, 1, stream())
+    for sg in range(nseg):
+        sl = pin.seg_slice(sg)
+        close(dx[sl], v.grad[sl] + 0.25, dt)
+    dw = zeros(k * k, C)
+    L.call("edet_dwconv_wgrad", DT[dt], lz.c, pin.c, C, k, s, vp(dy), pout.c, vp(dw), stream())
+    close(dw, wr.grad, dt, scale=pout.rows ** 0.5 * 3)
+
+
+# ----------------------------------------------------------------- lazy backward (BN train bwd)
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("C,act,gate,dsq,scale,nseg", [(40, 0, 0, 0, 0, 1), (96, 1, 1, 1, 0, 1), (64, 1, 0, 0, 1, 2),
+                                                        (144, 1, 0, 0, 0, 1)])
+def test_lazy_backward(dt, C, act, gate, dsq, scale, nseg):
+    rng = np.random.default_rng(C + act * 7 + nseg)
+    B = 3
+    pyr = Pyr(B, [(11, 7), (6, 4)]) if nseg == 2 else Pyr(B, [(9, 10)])
+    x = pyr_data(rng, pyr, C, dt, scale=2.0)
+    bn = make_bn(x, pyr, C, rng)
+    gt = g(torch.rand(B, C) + 0.5, "f32") if gate else None
+    lz = LazyDesc(x, pyr, C, bn=bn, act=act, gate=gt)
+    dv = pyr_data(rng, pyr, C, dt)
+    dsqt = g(rnd(rng, B, C) * 0.1, "f32") if dsq else None
+    sc = g(torch.tensor(rng.choice([0.0, 1.25], size=(nseg, B)), dtype=torch.float32), "f32") if scale else None
+    grads = [(zeros(C), zeros(C)) for _ in range(nseg)]
+    so = seg_out(grads)
+    L.call("edet_lazy_bwd_reduce", DT[dt], lz.c, pyr.c, C, vp(dv), vp(sc), vp(dsqt), so, stream())
+    dx = torch.empty(pyr.rows, C, dtype=TDT[dt], device=DEV)
+    L.call("edet_lazy_bwd_apply", DT[dt], lz.c, pyr.c, C, vp(dv), vp(sc), vp(dsqt), so, vp(dx), 0, stream())
+    # reference: autograd through BN(train, batch stats recomputed) -> act -> gate, with dsq term
+    xc = x.double().cpu()
+    for sg in range(nseg):
+        sl = pyr.seg_slice(sg)
+        xs = xc[sl].clone().requires_grad_(True)
+        su, sq, ga, be = (t.double().cpu() for t in bn[sg])
+        ga = ga.clone().requires_grad_(True)
+        be = be.clone().requires_grad_(True)
+        n = xs.shape[0]
+        mean = xs.mean(0)
+        var = ((xs - mean) ** 2).mean(0)
+        u = (xs - mean) / torch.sqrt(var + 1e-3) * ga + be
+        a = u * torch.sigmoid(u) if act else u
+        hw = pyr.sizes[sg][0] * pyr.sizes[sg][1]
+        d = dv[sl].double().cpu()
+        if sc is not None:
+            d = d * sc[sg].double().cpu().repeat_interleave(hw)[:, None]
+        if gt is not None:
+            d = d * gt.double().cpu().repeat_interleave(hw, 0)
+        if dsqt is not None:
+            d = d + dsqt.double().cpu().repeat_interleave(hw, 0)
+        (a * d).sum().backward()
+        close(dx[sl], xs.grad, dt, scale=4)
+        close(grads[sg][1], be.grad, dt, scale=n ** 0.5 * 2)
+        close(grads[sg][0], ga.grad, dt, scale=n ** 0.5 * 2)
+
+
+# ----------------------------------------------------------------- SE
+@pytest.mark.parametrize("dt", DTS)
+def test_squeeze_excite(dt):
+    rng = np.random.default_rng(5)
+    B, H, W, C, R = 3, 9, 7, 96, 4
+    pyr = Pyr(B, [(H, W)])
+    x = pyr_data(rng, pyr, C, dt)
+    bn = make_bn(x, pyr, C, rng)
+    lz = LazyDesc(x, pyr, C, bn=bn, act=1)
+    w1, b1 = g(rnd(rng, R, C, scale=0.2)), g(rnd(rng, R, scale=0.1))
+    w2, b2 = g(rnd(rng, C, R, scale=0.3)), g(rnd(rng, C, scale=0.1))
+    s = zeros(B, C)
+    L.call("edet_se_squeeze", DT[dt], lz.c, B, H * W, C, vp(s), stream())
+    z1, gate = zeros(B, R), zeros(B, C)
+    L.call("edet_se_fwd", B, C, R, vp(s), vp(w1), vp(b1), vp(w2), vp(b2), vp(z1), vp(gate), stream())
+    v = lz.cpu_value()
+    sref = v.view(B, H * W, C).mean(1)
+    close(s, sref, dt)
+    W1, B1, W2, B2 = (t.double().cpu().requires_grad_(True) for t in (w1, b1, w2, b2))
+    sr = sref.clone().requires_grad_(True)
+    zr = sr @ W1.t() + B1
+    gr = torch.sigmoid((zr * torch.sigmoid(zr)) @ W2.t() + B2)
+    close(gate, gr.detach(), dt)
+    # backward given dgate
+    dgate = g(rnd(rng, B, C))
+    dws = [zeros(R, C), zeros(R), zeros(C, R), zeros(C)]
+    dsq = zeros(B, C)
+    L.call("edet_se_bwd", B, C, R, H * W, vp(s), vp(z1), vp(gate), vp(dgate), vp(w1), vp(w2), vp(dws[0]), vp(dws[1]),
+           vp(dws[2]), vp(dws[3]), vp(dsq), stream())
+    (gr * dgate.double().cpu()).sum().backward()
+    for a, b in zip(dws, (W1.grad, B1.grad, W2.grad, B2.grad)):
+        close(a, b, "f32", rtol=1e-4, atol=1e-4)
+    close(dsq, sr.grad / (H * W), "f32", rtol=1e-4, atol=1e-5)
+    # gate grad: sum_hw dv * v
+    dv = pyr_data(rng, pyr, C, dt)
+    dg = zeros(B, C)
+    L.call("edet_gate_grad", DT[dt], lz.c, B, H * W, C, vp(dv), vp(dg), stream())
+    close(dg, (dv.double().cpu() * v).view(B, H * W, C).sum(1), dt, scale=8)
+
+
+# ----------------------------------------------------------------- maxpool / fuse / residual / stem
+def maxpool_ref(v, B, H, W, C):
+    xi = v.view(B, H, W, C).permute(0, 3, 1, 2)
+    OH, OW = (H + 1) // 2, (W + 1) // 2
+    ph, pw = max((OH - 1) * 2 + 3 - H, 0), max((OW - 1) * 2 + 3 - W, 0)
+    xi = Fn.pad(xi, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2), value=-math.inf)
+    return Fn.max_pool2d(xi, 3, 2).permute(0, 2, 3, 1).reshape(-1, C)
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("H,W", [(16, 16), (9, 7)])
+def test_maxpool(dt, H, W):
+    rng = np.random.default_rng(H * W)
+    B, C = 2, 64
+    pyr = Pyr(B, [(H, W)])
+    x = pyr_data(rng, pyr, C, dt)
+    bn = make_bn(x, pyr, C, rng)
+    lz = LazyDesc(x, pyr, C, bn=bn)
+    OH, OW = (H + 1) // 2, (W + 1) // 2
+    y = torch.empty(B * OH * OW, C, dtype=TDT[dt], device=DEV)
+    L.call("edet_maxpool_fwd", DT[dt], lz.c, B, H, W, C, vp(y), stream())
+    v = lz.cpu_value().requires_grad_(True)
+    ref = maxpool_ref(v, B, H, W, C)
+    close(y, ref.detach(), dt)
+    dy = g(rnd(rng, B * OH * OW, C), dt)
+    (ref * dy.double().cpu()).sum().backward()
+    dx = torch.empty(B * H * W, C, dtype=TDT[dt], device=DEV)
+    L.call("edet_maxpool_bwd", DT[dt], lz.c, B, H, W, C, vp(dy), vp(dx), 0, stream())
+    if dt == "f32":
+        close(dx, v.grad, dt)
+    else:  # bf16 ties may route differently; totals must agree
+        close(dx.double().cpu().sum(0), v.grad.sum(0), dt, scale=8)
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_bifpn_fuse(dt):
+    rng = np.random.default_rng(11)
+    B, C, H, W = 2, 64, 8, 8
+    ins = []
+    specs = [((H, W), L.MODE_SAME), ((H // 2, W // 2), L.MODE_UPSAMPLE), ((H * 2, W * 2), L.MODE_MAXPOOL)]
+    descs = []
+    fi = (L.FuseInput * 3)()
+    dxs = []
+    for i, ((h, w), mode) in enumerate(specs):
+        pyr = Pyr(B, [(h, w)])
+        x = pyr_data(rng, pyr, C, dt)
+        bn = make_bn(x, pyr, C, rng) if i != 1 else None
+        d = LazyDesc(x, pyr, C, bn=bn)
+        descs.append((d, h, w, mode))
+        fi[i].v, fi[i].H, fi[i].W, fi[i].mode = d.c, h, w, mode
+        dx = g(torch.full((pyr.rows, C), 0.5 if i == 0 else 0.0), dt)
+        dxs.append(dx)
+        fi[i].dx, fi[i].accumulate = dx.data_ptr(), 1 if i == 0 else 0
+    wv = g(torch.tensor([1.0, 0.7, 1.3]))
+    out = torch.empty(B * H * W, C, dtype=TDT[dt], device=DEV)
+    L.call("edet_bifpn_fuse_fwd", DT[dt], 3, fi, vp(wv), B, H, W, C, vp(out), stream())
+    vs = [d.cpu_value().requires_grad_(True) for d, *_ in descs]
+    wr = wv.double().cpu().requires_grad_(True)
+    den = wr.sum() + 1e-4
+    r0 = vs[0]
+    up = vs[1].view(B, H // 2, W // 2, C)[:, torch.arange(H) // 2][:, :, torch.arange(W) // 2].reshape(-1, C)
+    r2 = maxpool_ref(vs[2], B, H * 2, W * 2, C)
+    ref = r0 * wr[0] / den + up * wr[1] / den + r2 * wr[2] / den
+    close(out, ref.detach(), dt)
+    dout = g(rnd(rng, B * H * W, C), dt)
+    (ref * dout.double().cpu()).sum().backward()
+    dw = zeros(3)
+    L.call("edet_bifpn_fuse_bwd", DT[dt], 3, fi, vp(wv), B, H, W, C, vp(out), vp(dout), vp(dw), stream())
+    close(dxs[0], vs[0].grad + 0.5, dt)
+    close(dxs[1], vs[1].grad, dt)
+    if dt == "f32":
+        close(dxs[2], vs[2].grad, dt)
+    close(dw, wr.grad, dt, scale=30)
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_residual(dt):
+    rng = np.random.default_rng(3)
+    pyr = Pyr(2, [(8, 8), (4, 4)])
+    C = 64
+    x = pyr_data(rng, pyr, C, dt)
+    r = pyr_data(rng, pyr, C, dt)
+    lx = LazyDesc(x, pyr, C, bn=make_bn(x, pyr, C, rng), act=1)
+    lr = LazyDesc(r, pyr, C, bn=make_bn(r, pyr, C, rng))
+    sc = g(torch.tensor([[1.25, 0.0], [0.0, 1.25]]))
+    out = torch.empty(pyr.rows, C, dtype=TDT[dt], device=DEV)
+    L.call("edet_residual_fwd", DT[dt], lx.c, lr.c, pyr.c, C, vp(sc), vp(out), stream())
+    vx, vr = lx.cpu_value(), lr.cpu_value()
+    for s in range(2):
+        sl = pyr.seg_slice(s)
+        m = sc[s].double().cpu().repeat_interleave(pyr.sizes[s][0] * pyr.sizes[s][1])[:, None]
+        close(out[sl], vx[sl] * m + vr[sl], dt)
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_stem(dt):
+    rng = np.random.default_rng(9)
+    B, H, W, Co = 2, 21, 18, 32
+    x = g(torch.rand(B, H, W, 3), dt)
+    w = g(rnd(rng, 3, 3, 3, Co, scale=0.3), dt)
+    OH, OW = (H + 1) // 2, (W + 1) // 2
+    y = torch.empty(B * OH * OW, Co, dtype=TDT[dt], device=DEV)
+    su, sq = zeros(Co), zeros(Co)
+    L.call("edet_stem_fwd", DT[dt], vp(x), B, H, W, vp(w), Co, vp(y), vp(su), vp(sq), stream())
+    xc = x.double().cpu().permute(0, 3, 1, 2)
+    ph, pw = max((OH - 1) * 2 + 3 - H, 0), max((OW - 1) * 2 + 3 - W, 0)
+    xp = Fn.pad(xc, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2))
+    wr = w.double().cpu().permute(3, 2, 0, 1).clone().requires_grad_(True)
+    ref = Fn.conv2d(xp, wr, stride=2).permute(0, 2, 3, 1).reshape(-1, Co)
+    close(y, ref.detach(), dt)
+    close(su, ref.detach().sum(0), dt, scale=20)
+    dy = g(rnd(rng, B * OH * OW, Co), dt)
+    (ref * dy.double().cpu()).sum().backward()
+    dw = zeros(3, 3, 3, Co)
+    L.call("edet_stem_wgrad", DT[dt], vp(x), B, H, W, vp(dy), Co, vp(dw), stream())
+    close(dw, wr.grad.permute(2, 3, 1, 0), dt, scale=20)
+
+
+# ----------------------------------------------------------------- loss
+@pytest.mark.parametrize("dt", DTS)
+def test_detection_loss(dt):
+    rng = np.random.default_rng(21)
+    A, NC = 9, 5
+    pyr = Pyr(2, [(4, 4), (2, 2)])
+    ldc, ldb = 48, 40
+    cls = torch.zeros(pyr.rows, ldc)
+    cls[:, : A * NC] = rnd(rng, pyr.rows, A * NC, scale=3.0)
+    box = torch.zeros(pyr.rows, ldb)
+    box[:, : A * 4] = rnd(rng, pyr.rows, A * 4, scale=0.2)
+    cls_g, box_g = g(cls, dt), g(box, dt)
+    ct = torch.tensor(rng.integers(0, NC, (pyr.rows, A)), dtype=torch.int32)
+    bt = rnd(rng, pyr.rows, A, 4, scale=0.2)
+    bt[rng.random((pyr.rows, A, 4)) < 0.5] = 0.0
+    mask = (ct > 0).to(torch.uint8)
+    npos = zeros(1)
+    mask_g = mask.to(DEV)
+    for s in range(pyr.nseg):
+        sl = pyr.seg_slice(s)
+        L.call("edet_count_positives", vp(mask_g[sl]), pyr.seg_rows(s) * A, vp(npos), stream())
+    loss = zeros(1)
+    parts = zeros(10)
+    ctg, btg = ct.to(DEV), bt.to(DEV)
+    L.call("edet_detection_loss", DT[dt], vp(cls_g), ldc, vp(box_g), ldb, pyr.c, A, NC, vp(ctg), vp(btg), vp(npos),
+           0.25, 1.5, 0.1, 50.0, 1.0, vp(cls_g), vp(box_g), vp(loss), vp(parts), stream())
+    # reference (oracle formulas, fp64)
+    from oracle.ref_model import RefEfficientDet
+    npr = float(mask.sum()) + 1.0
+    tot = 0.0
+    xs = cls[:, : A * NC].double().requires_grad_(True)
+    bs = box[:, : A * 4].double().requires_grad_(True)
+    for s in range(pyr.nseg):
+        sl = pyr.seg_slice(s)
+        x = xs[sl].view(-1, A, NC)
+        y = Fn.one_hot(ct[sl].long(), NC).double()
+        p = torch.sigmoid(x)
+        pt = y * p + (1 - y) * (1 - p)
+        at = y * 0.25 + (1 - y) * 0.75
+        ce = torch.clamp(x, min=0) - x * y + torch.log1p(torch.exp(-x.abs()))
+        tot = tot + (at * (1 - pt) ** 1.5 * ce / npr).sum() / x.numel()
+        t = bt[sl].double().view(-1, A * 4)
+        e = bs[sl] - t
+        hub = torch.where(e.abs() <= 0.1, 0.5 * e ** 2, 0.005 + 0.1 * (e.abs() - 0.1))
+        tot = tot + 50.0 * (hub * (t != 0)).sum() / (4 * npr)
+    tot.backward()
+    close(npos, torch.tensor([npr - 1]), "f32")
+    close(loss, tot.detach().reshape(1), "f32", rtol=1e-4 if dt == "f32" else 2e-2)
+    close(cls_g[:, : A * NC], xs.grad, dt, scale=1e-3)
+    close(box_g[:, : A * 4], bs.grad, dt, scale=1e-1)
+    assert float(cls_g[:, A * NC:].abs().max()) == 0.0
+
+
+# ----------------------------------------------------------------- optimizer
+def test_optimizer_step():
+    rng = np.random.default_rng(2)
+    n, n_l2 = 10000, 6000
+    w = g(rnd(rng, n))
+    gr = g(rnd(rng, n) * 3)
+    v = g(rnd(rng, n) * 0.1)
+    ema = g(rnd(rng, n))
+    sc = L.Sched()
+    sc.adjusted_lr, sc.warmup_init, sc.warmup_steps, sc.total_steps = 0.08, 0.008, 10, 100
+    sc.momentum, sc.ema_decay, sc.clip_norm, sc.l2_weight = 0.9, 0.9998, 10.0, 4e-5
+    scal = zeros(8)
+    step = torch.tensor([3], dtype=torch.int32, device=DEV)
+    W0, G0, V0, E0 = (t.double().cpu() for t in (w, gr, v, ema))
+    wc = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    L.call("edet_opt_norm", vp(w), vp(gr), n, n_l2, sc, vp(scal), vp(step), stream())
+    L.call("edet_opt_apply", vp(w), vp(gr), vp(v), vp(ema), n, n_l2, sc, vp(scal), L.BF16, vp(wc), stream())
+    gg = G0.clone()
+    gg[:n_l2] += 4e-5 * W0[:n_l2]
+    gn = gg.norm()
+    lr = 0.008 + 3 / 10 * (0.08 - 0.008)
+    gg *= 10.0 / max(float(gn), 10.0)
+    V1 = 0.9 * V0 - lr * gg
+    W1 = W0 + V1
+    E1 = E0 - (1 - 0.9998) * (E0 - W1)
+    close(scal[3], gn, "f32", rtol=1e-5)
+    close(scal[4], torch.tensor(lr), "f32", rtol=1e-6)
+    close(scal[0], 4e-5 * (W0[:n_l2] ** 2).sum() / 2, "f32", rtol=1e-5)
+    close(w, W1, "f32", rtol=1e-5, atol=1e-6)
+    close(v, V1, "f32", rtol=1e-5, atol=1e-6)
+    close(ema, E1, "f32", rtol=1e-5, atol=1e-6)
+    close(wc, W1, "bf16")
+    assert int(step.item()) == 4
+
+
+def test_bn_moving_update_and_inference_stats():
+    rng = np.random.default_rng(4)
+    n = 300
+    su, sq = g(rnd(rng, n) * 50), g(torch.rand(n) * 500 + 2500)
+    cnt = g(torch.full((n,), 100.0))
+    mm, mv = g(rnd(rng, n)), g(torch.rand(n) + 0.5)
+    MM, MV = mm.double().cpu(), mv.double().cpu()
+    L.call("edet_bn_update_moving", n, vp(su), vp(sq), vp(cnt), 0.99, vp(mm), vp(mv), stream())
+    mean = su.double().cpu() / 100
+    var = sq.double().cpu() / 100 - mean ** 2
+    close(mm, MM - (MM - mean) * 0.01, "f32", rtol=1e-5)
+    close(mv, MV - (MV - var * 100 / 99) * 0.01, "f32", rtol=1e-5)
+    s2, q2 = zeros(n), zeros(n)
+    L.call("edet_bn_inference_stats", n, vp(mm), vp(mv), vp(cnt), vp(s2), vp(q2), stream())
+    m2 = s2.double().cpu() / 100
+    close(m2, mm, "f32", rtol=1e-6)
+    close(q2.double().cpu() / 100 - m2 ** 2, mv, "f32", rtol=1e-3, atol=1e-4)
+
+
+def test_dropmask():
+    out = torch.empty(4000, device=DEV)
+    step = torch.zeros(1, dtype=torch.int32, device=DEV)
+    L.call("edet_dropmask", vp(out), 4000, 0.8, 7, vp(step), stream())
+    o = out.cpu()
+    vals = set(np.round(o.numpy(), 5).tolist())
+    assert vals <= {0.0, 1.25}
+    frac = float((o > 0).float().mean())
+    assert 0.76 < frac < 0.84

@@ -1,0 +1,185 @@
+"""Model-level parity: the full EfficientDet-D0 topology through
+libedet vs the fp64 CPU oracle (oracle/ref_model.py) on identical parameters and inputs.
+
+Reduced size for oracle speed: D0 topology at 128x128, batch 2, 5 classes; drop-connect
+masks injected (the reference draws them randomly).  fp32 storage: outputs within 1e-3
+relative (north_star tolerance); bf16 storage: loss within 3 %, gradient cosine > 0.99.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle.ref_model import RefEfficientDet, ref_train_step
+from tf2mv_amd.anchors import Anchors
+from tf2mv_amd.config import efficientnet_b0_blocks, get_efficientdet_config
+from tf2mv_amd.model import EfficientDetNet, EfficientDetNetTrain
+
+pytestmark = pytest.mark.gpu
+SIZE, B, NC = 128, 2, 5
+
+
+def cfg(survival=0.8):
+    return get_efficientdet_config("efficientdet-d0", {"image_size": SIZE, "num_classes": NC, "survival_prob": survival})
+
+
+def synth(seed=0):
+    rng = np.random.default_rng(seed)
+    x = rng.random((B, SIZE, SIZE, 3), dtype=np.float32)
+    G = 6
+    boxes = np.zeros((B, G, 4), np.float32)
+    cls = np.zeros((B, G), np.int32)
+    n = np.full(B, G, np.int32)
+    for b in range(B):
+        for k in range(G):
+            s = np.exp(rng.uniform(np.log(12), np.log(90)))
+            ar = rng.uniform(0.5, 2)
+            h, w = s * np.sqrt(ar), s / np.sqrt(ar)
+            cy, cx = rng.uniform(0, SIZE, 2)
+            boxes[b, k] = [cy - h / 2, cx - w / 2, cy + h / 2, cx + w / 2]
+            cls[b, k] = rng.integers(1, NC)
+    return x, boxes, cls, n
+
+
+def make_targets(model, anchors, boxes, cls, n):
+    t = anchors.generate_targets_batched(torch.tensor(boxes), torch.tensor(cls), torch.tensor(n))
+    pyr = t.pyr
+    yb, yc, ym = [], [], []
+    tb, tc, tm = t.box.cpu().numpy(), t.cls.cpu().numpy(), t.mask.cpu().numpy()
+    for s, l in enumerate(model.levels):
+        H, W = model.level_hw[l]
+        sl = pyr.seg_slice(s)
+        yb.append(tb[sl].reshape(B, H, W, 9, 4))
+        yc.append(np.eye(NC, dtype=np.float32)[tc[sl]].reshape(B, H, W, 9, NC))
+        ym.append(tm[sl].reshape(B, H, W, 9, 1).astype(bool))
+    return t, yb, yc, ym
+
+
+def fixed_masks(model, seed=3):
+    rng = np.random.default_rng(seed)
+    reps = model.cfg.box_class_repeats - 1
+    m = rng.choice([0.0, 1.25], size=(2, reps, len(model.levels), B), p=[0.3, 0.7]).astype(np.float32)
+    return m
+
+
+def rel_err(a, b):
+    a = torch.as_tensor(a, dtype=torch.float64)
+    b = torch.as_tensor(b, dtype=torch.float64)
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def test_bifpn_topology_matches_reference():
+    """bifpn.py:108-117: P6'=(P6,P7) P5'=(P5,P6') P4'=(P4,P5') P3''=(P3,P4') P4''=(P4,P4',P3'')
+    P5''=(P5,P5',P4'') P6''=(P6,P6',P5'') P7''=(P7,P6'') with ids 0..4 inputs, 5.. nodes."""
+    m = EfficientDetNet(efficientnet_b0_blocks(), cfg(), dtype="f32")
+    assert [n["inputs"] for n in m.cells[0]] == [[3, 4], [2, 5], [1, 6], [0, 7], [1, 7, 8], [2, 6, 9], [3, 5, 10], [4, 11]]
+    assert [n["level"] for n in m.cells[0]] == [6, 5, 4, 3, 4, 5, 6, 7]
+    # trainable parameter count of full D0 (3,874,802)
+    d0 = EfficientDetNet(efficientnet_b0_blocks(), get_efficientdet_config("efficientdet-d0"), dtype="f32")
+    assert d0.P.n_trainable == 3874802
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_forward_parity_fp32(training):
+    m = EfficientDetNet(efficientnet_b0_blocks(), cfg(), dtype="f32", seed=1)
+    x, *_ = synth(1)
+    if not training:  # non-trivial moving statistics
+        sd = m.state_dict()
+        rng = np.random.default_rng(7)
+        for k in sd:
+            if k.endswith("moving_mean"):
+                sd[k] = rng.normal(0, 0.3, sd[k].shape).astype(np.float32)
+            elif k.endswith("moving_variance"):
+                sd[k] = rng.uniform(0.5, 2.0, sd[k].shape).astype(np.float32)
+        m.load_state_dict(sd)
+    fm = fixed_masks(m)
+    masks = {"class_net": torch.tensor(fm[0]).cuda(), "box_net": torch.tensor(fm[1]).cuda()}
+    boxes, classes = m.call(torch.tensor(x).cuda(), training=training, masks=masks if training else None)
+    ref = RefEfficientDet(m, m.state_dict())
+    rmasks = {"class_net": fm[0], "box_net": fm[1]}
+    rb, rc = ref.forward(x, training, rmasks if training else None)
+    for l in range(5):
+        assert boxes[l].shape == tuple(rb[l].shape) and classes[l].shape == tuple(rc[l].shape)
+        assert rel_err(boxes[l].cpu(), rb[l].detach()) < 1e-3, l
+        assert rel_err(classes[l].cpu(), rc[l].detach()) < 1e-3, l
+
+
+def _train_model(dtype, seed=1):
+    c = cfg()
+    anchors = Anchors(c.min_level, c.max_level, (SIZE, SIZE), c.num_scales, c.aspect_ratios, c.anchor_scale)
+    m = EfficientDetNetTrain(efficientnet_b0_blocks(), c, anchors, dtype=dtype, seed=seed,
+                             lr_schedule={"fixed_lr": 0.01})
+    return m, anchors
+
+
+def test_train_step_parity_fp32():
+    m, anchors = _train_model("f32")
+    x, boxes, cls, n = synth(2)
+    t, yb, yc, ym = make_targets(m, anchors, boxes, cls, n)
+    fm = fixed_masks(m)
+    m.fixed_masks = {"class_net": torch.tensor(fm[0]).cuda(), "box_net": torch.tensor(fm[1]).cuda()}
+    sd0 = m.state_dict()
+    ref = RefEfficientDet(m, sd0)
+    loss_r, gn_r, new_r, grads_r, st, parts = ref_train_step(ref, x, yb, yc, ym, {"class_net": fm[0], "box_net": fm[1]},
+                                                             lr=0.01)
+    out = m.train_step((torch.tensor(x).cuda(), t))
+    loss, gn = float(out["loss"]), float(out["gnorm"])
+    assert abs(loss - float(loss_r)) / float(loss_r) < 1e-4, (loss, float(loss_r))
+    assert abs(gn - float(gn_r)) / float(gn_r) < 1e-3, (gn, float(gn_r))
+    g = m.P.grads_dict()
+    gnorm_r = float(gn_r)
+    bad = []
+    for k, gr in grads_r.items():
+        gg = torch.tensor(g[k], dtype=torch.float64)
+        if m.P.specs[k].l2:
+            gg = gg + 4e-5 * torch.tensor(sd0[k], dtype=torch.float64)
+        err = float((gg - gr).norm())
+        if err > 1e-3 * float(gr.norm()) + 1e-6 * gnorm_r:
+            bad.append((k, err, float(gr.norm())))
+    assert not bad, bad[:10]
+    sd1 = m.state_dict()
+    for k, v in new_r.items():
+        np.testing.assert_allclose(sd1[k], v.numpy(), rtol=1e-3, atol=1e-5, err_msg=k)
+
+
+def test_train_step_reference_format_equals_compact():
+    m, anchors = _train_model("f32")
+    x, boxes, cls, n = synth(4)
+    t, yb, yc, ym = make_targets(m, anchors, boxes, cls, n)
+    m.fixed_masks = {k: torch.ones(2, 5, B).cuda() for k in ("class_net", "box_net")}
+    sd0 = m.state_dict()
+    l1 = float(m.train_step((torch.tensor(x).cuda(), t))["loss"])
+    g1 = m.P.g.clone()
+    m.load_state_dict(sd0)
+    data = (torch.tensor(x).cuda(), tuple(torch.tensor(a).cuda() for a in yb), tuple(torch.tensor(a).cuda() for a in yc),
+            tuple(torch.tensor(a).cuda() for a in ym))
+    l2 = float(m.train_step(data)["loss"])
+    assert l1 == l2
+    assert torch.equal(g1, m.P.g) or float((g1 - m.P.g).abs().max()) < 1e-6 * float(g1.abs().max())
+
+
+def test_train_step_bf16_close_to_fp32_oracle():
+    m, anchors = _train_model("bf16")
+    x, boxes, cls, n = synth(5)
+    t, yb, yc, ym = make_targets(m, anchors, boxes, cls, n)
+    fm = fixed_masks(m)
+    m.fixed_masks = {"class_net": torch.tensor(fm[0]).cuda(), "box_net": torch.tensor(fm[1]).cuda()}
+    sd0 = m.state_dict()
+    ref = RefEfficientDet(m, sd0)
+    loss_r, gn_r, _, grads_r, _, _ = ref_train_step(ref, x, yb, yc, ym, {"class_net": fm[0], "box_net": fm[1]}, lr=0.01)
+    out = m.train_step((torch.tensor(x).cuda(), t))
+    loss = float(out["loss"])
+    assert np.isfinite(loss) and abs(loss - float(loss_r)) / float(loss_r) < 3e-2, (loss, float(loss_r))
+    g = m.P.grads_dict()
+    a = np.concatenate([g[k].ravel() + (4e-5 * sd0[k].ravel() if m.P.specs[k].l2 else 0) for k in grads_r])
+    b = np.concatenate([grads_r[k].numpy().ravel() for k in grads_r])
+    cos = float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
+    assert cos > 0.99, cos
+
+
+def test_training_reduces_loss_bf16():
+    m, anchors = _train_model("bf16", seed=3)
+    x, boxes, cls, n = synth(6)
+    t, *_ = make_targets(m, anchors, boxes, cls, n)
+    xs = torch.tensor(x).cuda()
+    losses = [float(m.train_step((xs, t))["loss"]) for _ in range(8)]
+    assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
