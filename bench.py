@@ -71,8 +71,11 @@ def algorithmic_bytes(name, args, es):
     if name == "edet_conv1x1_wgrad":
         p, K, N = args[2], args[3], args[6]
         return rows(p) * (K + N) * es
-    if name in ("edet_dwconv_fwd", "edet_dwconv_wgrad"):
+    if name == "edet_dwconv_fwd":
         pin, C, pout = args[2], args[3], args[8]
+        return (rows(pin) + rows(pout)) * C * es
+    if name == "edet_dwconv_wgrad":
+        pin, C, pout = args[2], args[3], args[7]
         return (rows(pin) + rows(pout)) * C * es
     if name == "edet_dwconv_dgrad":
         pout, C, pin, acc = args[2], args[3], args[8], args[9]
@@ -142,7 +145,7 @@ class KernelTimer:
 def cpu_baseline(model, seconds=12.0):
     """Oracle fp32 train step (forward + loss + backward) on the host cores, 1 image/iteration."""
     from oracle.ref_model import RefEfficientDet
-    threads = len(os.sched_getaffinity(0))
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     torch.set_num_threads(threads)
     ref = RefEfficientDet(model, model.state_dict(), dtype=torch.float32)
     train_keys = [k for k in ref.p if not k.endswith(("moving_mean", "moving_variance"))]

@@ -8,6 +8,10 @@ from __future__ import annotations
 
 import ctypes
 import os
+
+# libedet.so links libamdhip64.so.7; load torch first so the process has ONE HIP runtime
+# (torch's) and libedet binds to it instead of bringing up a second one.
+import torch  # noqa: F401
 from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
 
 MAX_SEG = 5

@@ -477,7 +477,7 @@ class EfficientDetNetTrain(EfficientDetNet):
         if self.npos_allreduce is not None:
             self.npos_allreduce(self.scalars[5:6])
         masks = self._make_masks(B)
-        eng.tape = Tape(eng)
+        eng.tape = Tape(eng, getattr(self, "grad_trace", None))
         cls, box, pyr2 = self._forward(x, True, masks)
         # fused focal + Huber loss: gradients are written in place over the logits
         L.call("edet_detection_loss", eng.dt, vp(cls.raw), cls.ld, vp(box.raw), box.ld, pyr.c, self.A, self.NC,

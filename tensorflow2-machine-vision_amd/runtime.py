@@ -350,10 +350,11 @@ class GradRec:
 class Tape:
     """Explicit reverse-mode AD: one closure per forward op, run in reverse order."""
 
-    def __init__(self, engine: "Engine"):
+    def __init__(self, engine: "Engine", trace: Optional[list] = None):
         self.eng = engine
         self.entries: List = []
         self.g: Dict[Act, GradRec] = {}
+        self.trace = trace  # debug: list receiving (act name, fp32 copy of d(value)) per take()
 
     def record(self, fn):
         self.entries.append(fn)
@@ -373,7 +374,11 @@ class Tape:
         self.g[act] = GradRec(t, ld, scale)
 
     def take(self, act: Act) -> Optional[GradRec]:
-        return self.g.pop(act, None)
+        rec = self.g.pop(act, None)
+        if self.trace is not None and rec is not None:
+            rows = [rec.t[act.pyr.seg_slice(s), : act.C].float() for s in range(act.pyr.nseg)]
+            self.trace.append((act.name, torch.cat(rows, 0).clone(), None if rec.scale is None else rec.scale.clone()))
+        return rec
 
     def backward(self):
         entries, self.entries = self.entries, []
