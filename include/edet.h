@@ -121,9 +121,10 @@ int edet_memcpy_async(void* dst, const void* src, size_t bytes, edet_stream_t st
 int edet_conv1x1_fwd(int dtype, const edet_lazy* a, const edet_pyramid* rows, int K,
                      const void* wt, int N, const float* bias, void* y, int ldy,
                      int accumulate, const edet_segout* stats, edet_stream_t stream);
-/* dx[m][k] = sum_n dy[m][n] * wt[n][k] */
+/* dx[m][k] = sum_n dy[m][n] * w[n][k]; wkn is the transposed compute copy [K][roundup(N,8)]
+ * written by edet_transpose_cast */
 int edet_conv1x1_dgrad(int dtype, const void* dy, int lddy, const edet_pyramid* rows, int N,
-                       const void* wt, int K, void* dx, int lddx, int accumulate,
+                       const void* wkn, int K, void* dx, int lddx, int accumulate,
                        edet_stream_t stream);
 /* dwt[n][k] += sum_m dy[m][n] * v(a)[m][k];  dbias[n] += sum_m dy[m][n]  (valid rows only) */
 int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, int K,
@@ -230,6 +231,10 @@ int edet_opt_apply(float* w, const float* g, float* v, float* ema, int64_t n, in
                    const edet_sched* sched, float* scalars, int dtype, void* wcompute,
                    edet_stream_t stream);
 int edet_cast_f32(int dtype, const float* src, void* dst, int64_t n, edet_stream_t stream);
+/* fp32 [N][K] 1x1 kernels -> `dtype` [K][roundup(N,8)] copies; table[e] = {src_off, dst_off, N, K}
+ * (int64, device memory); grid = max_tiles (32x32 tiles of the largest entry) x n_entries */
+int edet_transpose_cast(int dtype, const float* src, void* dst, const int64_t* table, int n_entries,
+                        int max_tiles, edet_stream_t stream);
 /* inference-mode BN: express moving mean/var as the sums the lazy loaders expect */
 int edet_bn_inference_stats(int64_t n, const float* mmean, const float* mvar, const float* count,
                             float* sum, float* sq, edet_stream_t stream);

@@ -97,6 +97,7 @@ SIGNATURES = {
     "edet_opt_norm": [P, P, c_int64, c_int64, PSched, P, P, P],
     "edet_opt_apply": [P, P, P, P, c_int64, c_int64, PSched, P, c_int, P, P],
     "edet_cast_f32": [c_int, P, P, c_int64, P],
+    "edet_transpose_cast": [c_int, P, P, P, c_int, c_int, P],
     "edet_bn_inference_stats": [c_int64, P, P, P, P, P, P],
     "edet_bn_update_moving": [c_int64, P, P, P, c_float, P, P, P],
     "edet_dropmask": [P, c_int, c_float, c_uint64, P, P],

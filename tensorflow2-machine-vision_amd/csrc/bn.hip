@@ -13,8 +13,28 @@
 
 namespace edet {
 
-constexpr int RCH = 256;  // rows per chunk
-constexpr int RCB = 64;   // channels per block
+// Row kernels: a block covers R full rows per pass with TPR threads per row (TPR = C/8
+// 8-channel vectors, or 256 for C > 2048 with up to 2 vectors per thread), so every pass is
+// R contiguous rows of the NHWC tensor (fully coalesced, no idle lanes for C = 96/144/240...)
+// and each thread keeps a fixed channel vector -> per-thread partial sums need no atomics.
+constexpr int RVPT = 2;  // vectors per thread (C <= 4096)
+
+struct RowGeom {
+  int TPR, R, VPT, CH;  // threads per row, rows per pass, vectors per thread, rows per chunk
+};
+
+static RowGeom row_geom(int C) {
+  RowGeom r;
+  const int NV = C / 8;
+  r.TPR = NV <= 256 ? NV : 256;
+  r.VPT = cdiv(NV, r.TPR);
+  r.R = 256 / r.TPR;
+  int passes = 16384 / (r.R * C);
+  if (passes < 1) passes = 1;
+  if (passes > 16) passes = 16;
+  r.CH = r.R * passes;
+  return r;
+}
 
 struct LArgs {
   edet_lazy lz;
@@ -26,169 +46,222 @@ struct LArgs {
   const float* dv_scale;
   const float* dsq;
   float* out;  // se_squeeze / gate_grad output [batch][C]
-  int C, ncb, accumulate, hw, chunks_per_img;
+  int C, accumulate, hw, chunks_per_img;
+  RowGeom geo;
 };
 
-// per-block channel table: affine (sc, sh) and (mean, rstd)
-__device__ __forceinline__ void load_chan_table(const edet_lazy& lz, int seg, float inv, int c0, int C,
-                                                float2* af, float2* mr) {
-  const int tid = threadIdx.x;
-  if (tid < RCB) {
-    const int c = c0 + tid;
+// per-channel tables in dynamic LDS: af (sc, sh), mr (mean, rstd), gb (dgamma/M, dbeta/M)
+__device__ __forceinline__ void load_tables(const edet_lazy& lz, int seg, float inv, int C, float2* af, float2* mr,
+                                            float2* gb, const edet_segout* grads) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float2 a = make_float2(1.f, 0.f), b = make_float2(0.f, 1.f);
-    if (c < C && lz.bn.enabled) {
+    if (lz.bn.enabled) {
       a = bn_affine(lz.bn, seg, c, inv);
       b = bn_mean_rstd(lz.bn, seg, c, inv);
     }
-    af[tid] = a;
-    mr[tid] = b;
+    af[c] = a;
+    if (mr) mr[c] = b;
+    if (gb) gb[c] = lz.bn.enabled ? make_float2(grads->a[seg][c] * inv, grads->b[seg][c] * inv) : make_float2(0.f, 0.f);
   }
 }
 
-// du for 8 channels of one row; also returns xhat
+// du (gradient at the BN output) and xhat for the 8 channels at c of row m (image n)
 template <typename T>
-__device__ __forceinline__ void lazy_du(const LArgs& g, int seg, int m, int n, int cv8, int cc, int nc,
-                                        const float2* af, const float2* mr, float* du, float* xh) {
+__device__ __forceinline__ void lazy_du(const LArgs& g, int seg, int m, int n, int c, const float2* af,
+                                        const float2* mr, float* du, float* xh) {
   float x[8], d[8];
-  ld8m((const T*)g.lz.x + (size_t)m * g.lz.ld + cc, nc, x);
-  ld8m((const T*)g.dv + (size_t)m * g.C + cc, nc, d);
+  ld8((const T*)g.lz.x + (size_t)m * g.lz.ld + c, x);
+  ld8((const T*)g.dv + (size_t)m * g.C + c, d);
   const float dvs = g.dv_scale ? g.dv_scale[seg * g.p.batch + n] : 1.f;
+  float gt[8], ds[8];
+  if (g.lz.gate) ld8(g.lz.gate + (size_t)n * g.C + c, gt);
+  if (g.dsq) ld8(g.dsq + (size_t)n * g.C + c, ds);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float2 a = af[cv8 + j];
+    const float2 a = af[c + j];
     const float u = x[j] * a.x + a.y;
     float gg = d[j] * dvs;
-    if (j < nc) {
-      if (g.lz.gate) gg *= g.lz.gate[(size_t)n * g.C + cc + j];
-      if (g.dsq) gg += g.dsq[(size_t)n * g.C + cc + j];
-    }
+    if (g.lz.gate) gg *= gt[j];
+    if (g.dsq) gg += ds[j];
     du[j] = g.lz.act ? gg * dswishf_(u) : gg;
-    const float2 b = mr[cv8 + j];
+    const float2 b = mr[c + j];
     xh[j] = (x[j] - b.x) * b.y;
   }
 }
 
+// Persistent over chunks (block b takes chunks b, b+grid, ...): per-thread partials live in
+// registers until the segment changes, so each block issues 2C atomics per segment.
 template <typename T>
-__global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g) {
-  __shared__ float2 af[RCB], mr[RCB];
-  __shared__ float red[2][32][RCB + 1];
-  const int tid = threadIdx.x, cv = tid & 7, rs = tid >> 3;
-  const int cb = blockIdx.x % g.ncb;
-  int seg, chunk;
-  chunk_lookup(g.p, RCH, blockIdx.x / g.ncb, seg, chunk);
-  const int c0 = cb * RCB;
-  const int rows = seg_rows(g.p, seg);
-  load_chan_table(g.lz, seg, 1.f / (float)rows, c0, g.C, af, mr);
-  __syncthreads();
-  const int off = g.p.row_off[seg];
-  const int m_begin = off + chunk * RCH, m_end = min(off + rows, m_begin + RCH);
-  const int hw = g.p.H[seg] * g.p.W[seg];
-  const int cc = c0 + cv * 8, nc = g.C - cc;
-  float s[8], q[8];
+__device__ __forceinline__ void flush_reduce(const LArgs& g, const RowGeom& geo, int seg, int rr, int tv, float* red,
+                                             float (&s)[RVPT][8], float (&q)[RVPT][8]) {
+  const int C = g.C, NV = C / 8, tid = threadIdx.x;
+  if (rr < geo.R) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { s[j] = 0.f; q[j] = 0.f; }
-  if (nc > 0) {
-    for (int m = m_begin + rs; m < m_end; m += 32) {
-      const int n = (m - off) / hw;
-      float du[8], xh[8];
-      lazy_du<T>(g, seg, m, n, cv * 8, cc, nc, af, mr, du, xh);
+    for (int v = 0; v < RVPT; ++v) {
+      const int cv = tv + v * geo.TPR;
+      if (v < geo.VPT && cv < NV) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { s[j] += du[j]; q[j] += du[j] * xh[j]; }
+        for (int j = 0; j < 8; ++j) {
+          red[(0 * geo.R + rr) * C + cv * 8 + j] = s[v][j];
+          red[(1 * geo.R + rr) * C + cv * 8 + j] = q[v][j];
+        }
+      }
     }
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { red[0][rs][cv * 8 + j] = s[j]; red[1][rs][cv * 8 + j] = q[j]; }
+  for (int v = 0; v < RVPT; ++v)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s[v][j] = 0.f; q[v][j] = 0.f; }
   __syncthreads();
-  if (tid < RCB && c0 + tid < g.C) {
+  for (int c = tid; c < C; c += blockDim.x) {
     float ss = 0.f, qq = 0.f;
-#pragma unroll 8
-    for (int i = 0; i < 32; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
-    atomicAdd(g.grads.b[seg] + c0 + tid, ss);  // dbeta
-    atomicAdd(g.grads.a[seg] + c0 + tid, qq);  // dgamma
+    for (int i = 0; i < geo.R; ++i) { ss += red[i * C + c]; qq += red[(geo.R + i) * C + c]; }
+    atomicAdd(g.grads.b[seg] + c, ss);  // dbeta
+    atomicAdd(g.grads.a[seg] + c, qq);  // dgamma
   }
+  __syncthreads();
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int C = g.C;
+  float2* af = reinterpret_cast<float2*>(smem);
+  float2* mr = af + C;
+  float* red = reinterpret_cast<float*>(mr + C);  // [2][R][C]
+  const RowGeom geo = g.geo;
+  const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
+  const int NV = C / 8;
+  float s[RVPT][8], q[RVPT][8];
+#pragma unroll
+  for (int v = 0; v < RVPT; ++v)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s[v][j] = 0.f; q[v][j] = 0.f; }
+  int cur_seg = -1;
+  for (int b = blockIdx.x; b < nchunks; b += gridDim.x) {
+    int seg, chunk;
+    chunk_lookup(g.p, geo.CH, b, seg, chunk);
+    const int rows = seg_rows(g.p, seg);
+    if (seg != cur_seg) {
+      if (cur_seg >= 0) flush_reduce<T>(g, geo, cur_seg, rr, tv, red, s, q);
+      load_tables(g.lz, seg, 1.f / (float)rows, C, af, mr, nullptr, nullptr);
+      cur_seg = seg;
+      __syncthreads();
+    }
+    const int off = g.p.row_off[seg];
+    const int m_begin = off + chunk * geo.CH, m_end = min(off + rows, m_begin + geo.CH);
+    const int hw = g.p.H[seg] * g.p.W[seg];
+    if (rr < geo.R) {
+      for (int m = m_begin + rr; m < m_end; m += geo.R) {
+        const int n = (m - off) / hw;
+#pragma unroll
+        for (int v = 0; v < RVPT; ++v) {
+          const int cv = tv + v * geo.TPR;
+          if (v < geo.VPT && cv < NV) {
+            float du[8], xh[8];
+            lazy_du<T>(g, seg, m, n, cv * 8, af, mr, du, xh);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { s[v][j] += du[j]; q[v][j] += du[j] * xh[j]; }
+          }
+        }
+      }
+    }
+  }
+  if (cur_seg >= 0) flush_reduce<T>(g, geo, cur_seg, rr, tv, red, s, q);
 }
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g) {
-  __shared__ float2 af[RCB], mr[RCB], gb[RCB];
-  const int tid = threadIdx.x, cv = tid & 7, rs = tid >> 3;
-  const int cb = blockIdx.x % g.ncb;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int C = g.C;
+  float2* af = reinterpret_cast<float2*>(smem);
+  float2* mr = af + C;
+  float2* gb = mr + C;
+  const RowGeom geo = g.geo;
+  const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
   int seg, chunk;
-  chunk_lookup(g.p, RCH, blockIdx.x / g.ncb, seg, chunk);
-  const int c0 = cb * RCB;
+  chunk_lookup(g.p, geo.CH, blockIdx.x, seg, chunk);
   const int rows = seg_rows(g.p, seg);
-  const float inv = 1.f / (float)rows;
-  load_chan_table(g.lz, seg, inv, c0, g.C, af, mr);
-  if (tid < RCB) {
-    const int c = c0 + tid;
-    gb[tid] = (g.lz.bn.enabled && c < g.C) ? make_float2(g.grads.a[seg][c] * inv, g.grads.b[seg][c] * inv)
-                                          : make_float2(0.f, 0.f);
-  }
+  load_tables(g.lz, seg, 1.f / (float)rows, C, af, mr, gb, &g.grads);
   __syncthreads();
+  if (rr >= geo.R) return;
   const int off = g.p.row_off[seg];
-  const int m_begin = off + chunk * RCH, m_end = min(off + rows, m_begin + RCH);
+  const int m_begin = off + chunk * geo.CH, m_end = min(off + rows, m_begin + geo.CH);
   const int hw = g.p.H[seg] * g.p.W[seg];
-  const int cc = c0 + cv * 8, nc = g.C - cc;
-  if (nc <= 0) return;
+  const int NV = C / 8;
   T* DX = (T*)g.dx;
-  for (int m = m_begin + rs; m < m_end; m += 32) {
+  const bool bn = g.lz.bn.enabled;
+  for (int m = m_begin + rr; m < m_end; m += geo.R) {
     const int n = (m - off) / hw;
-    float du[8], xh[8], o[8];
-    lazy_du<T>(g, seg, m, n, cv * 8, cc, nc, af, mr, du, xh);
-    if (g.lz.bn.enabled) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float2 d = gb[cv * 8 + j];  // (dgamma/M, dbeta/M)
-        o[j] = af[cv * 8 + j].x * (du[j] - d.y - xh[j] * d.x);
+    for (int v = 0; v < RVPT; ++v) {
+      const int cv = tv + v * geo.TPR;
+      if (v < geo.VPT && cv < NV) {
+        const int c = cv * 8;
+        float du[8], xh[8], o[8];
+        lazy_du<T>(g, seg, m, n, c, af, mr, du, xh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float2 d = gb[c + j];
+          o[j] = bn ? af[c + j].x * (du[j] - d.y - xh[j] * d.x) : du[j];
+        }
+        acc8m(DX + (size_t)m * C + c, 8, o, g.accumulate);
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = du[j];
     }
-    acc8m(DX + (size_t)m * g.C + cc, nc, o, g.accumulate);
   }
 }
 
 // out[n][c] += (scale) * sum_hw f(row)   -- SE squeeze (mean of v(x)) or gate grad (dv * v(x))
 template <typename T, bool GATEGRAD>
 __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
-  __shared__ float2 af[RCB], mr[RCB];
-  __shared__ float red[32][RCB + 1];
-  const int tid = threadIdx.x, cv = tid & 7, rs = tid >> 3;
-  const int cb = blockIdx.x % g.ncb;
-  const int id = blockIdx.x / g.ncb;
-  const int n = id / g.chunks_per_img, chunk = id - n * g.chunks_per_img;
-  const int c0 = cb * RCB;
-  const int rows = seg_rows(g.p, 0);
-  load_chan_table(g.lz, 0, 1.f / (float)rows, c0, g.C, af, mr);
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int C = g.C;
+  float2* af = reinterpret_cast<float2*>(smem);
+  float* red = reinterpret_cast<float*>(af + C);  // [R][C]
+  const RowGeom geo = g.geo;
+  const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
+  const int n = blockIdx.x / g.chunks_per_img, chunk = blockIdx.x - n * g.chunks_per_img;
+  load_tables(g.lz, 0, 1.f / (float)seg_rows(g.p, 0), C, af, nullptr, nullptr, nullptr);
   __syncthreads();
-  const int m_begin = n * g.hw + chunk * RCH, m_end = min((n + 1) * g.hw, m_begin + RCH);
-  const int cc = c0 + cv * 8, nc = g.C - cc;
-  float s[8];
+  const int m_begin = n * g.hw + chunk * geo.CH, m_end = min((n + 1) * g.hw, m_begin + geo.CH);
+  const int NV = C / 8;
+  float s[RVPT][8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s[j] = 0.f;
-  if (nc > 0) {
-    for (int m = m_begin + rs; m < m_end; m += 32) {
-      float x[8];
-      ld8m((const T*)g.lz.x + (size_t)m * g.lz.ld + cc, nc, x);
-      float d[8];
-      if (GATEGRAD) ld8m((const T*)g.dv + (size_t)m * g.C + cc, nc, d);
+  for (int v = 0; v < RVPT; ++v)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float v = lazy_apply(x[j], af[cv * 8 + j], g.lz.act);
-        s[j] += GATEGRAD ? d[j] * v : v;
+    for (int j = 0; j < 8; ++j) s[v][j] = 0.f;
+  if (rr < geo.R) {
+    for (int m = m_begin + rr; m < m_end; m += geo.R) {
+#pragma unroll
+      for (int v = 0; v < RVPT; ++v) {
+        const int cv = tv + v * geo.TPR;
+        if (v < geo.VPT && cv < NV) {
+          const int c = cv * 8;
+          float x[8], d[8];
+          ld8((const T*)g.lz.x + (size_t)m * g.lz.ld + c, x);
+          if (GATEGRAD) ld8((const T*)g.dv + (size_t)m * C + c, d);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float val = lazy_apply(x[j], af[c + j], g.lz.act);
+            s[v][j] += GATEGRAD ? d[j] * val : val;
+          }
+        }
       }
     }
-  }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[rs][cv * 8 + j] = s[j];
+    for (int v = 0; v < RVPT; ++v) {
+      const int cv = tv + v * geo.TPR;
+      if (v < geo.VPT && cv < NV)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[rr * C + cv * 8 + j] = s[v][j];
+    }
+  }
   __syncthreads();
-  if (tid < RCB && c0 + tid < g.C) {
+  const float scale = GATEGRAD ? 1.f : 1.f / (float)g.hw;
+  for (int c = tid; c < C; c += blockDim.x) {
     float ss = 0.f;
-#pragma unroll 8
-    for (int i = 0; i < 32; ++i) ss += red[i][tid];
-    if (!GATEGRAD) ss *= 1.f / (float)g.hw;
-    atomicAdd(g.out + (size_t)n * g.C + c0 + tid, ss);
+    for (int i = 0; i < geo.R; ++i) ss += red[i * C + c];
+    atomicAdd(g.out + (size_t)n * C + c, ss * scale);
   }
 }
 
@@ -274,34 +347,42 @@ __global__ __launch_bounds__(256) void k_se_bwd(int C, int R, int HW, const floa
 // heads: out = v(x) * scale[seg][n] + v(res)   (class_net.py:93-96 with drop_connect.py:4-18)
 template <typename T>
 __global__ __launch_bounds__(256) void k_residual(LArgs g) {
-  __shared__ float2 ax[RCB], ar[RCB], dummy[RCB];
-  const int tid = threadIdx.x, cv = tid & 7, rs = tid >> 3;
-  const int cb = blockIdx.x % g.ncb;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int C = g.C;
+  float2* ax = reinterpret_cast<float2*>(smem);
+  float2* ar = ax + C;
+  const RowGeom geo = g.geo;
+  const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
   int seg, chunk;
-  chunk_lookup(g.p, RCH, blockIdx.x / g.ncb, seg, chunk);
-  const int c0 = cb * RCB;
+  chunk_lookup(g.p, geo.CH, blockIdx.x, seg, chunk);
   const int rows = seg_rows(g.p, seg);
   const float inv = 1.f / (float)rows;
-  load_chan_table(g.lz, seg, inv, c0, g.C, ax, dummy);
+  load_tables(g.lz, seg, inv, C, ax, nullptr, nullptr, nullptr);
+  load_tables(g.res, seg, inv, C, ar, nullptr, nullptr, nullptr);
   __syncthreads();
-  load_chan_table(g.res, seg, inv, c0, g.C, ar, dummy);
-  __syncthreads();
+  if (rr >= geo.R) return;
   const int off = g.p.row_off[seg];
-  const int m_begin = off + chunk * RCH, m_end = min(off + rows, m_begin + RCH);
+  const int m_begin = off + chunk * geo.CH, m_end = min(off + rows, m_begin + geo.CH);
   const int hw = g.p.H[seg] * g.p.W[seg];
-  const int cc = c0 + cv * 8, nc = g.C - cc;
-  if (nc <= 0) return;
+  const int NV = C / 8;
   T* OUT = (T*)g.dx;
-  for (int m = m_begin + rs; m < m_end; m += 32) {
+  for (int m = m_begin + rr; m < m_end; m += geo.R) {
     const int n = (m - off) / hw;
     const float sc = g.dv_scale ? g.dv_scale[seg * g.p.batch + n] : 1.f;
-    float x[8], r[8], o[8];
-    ld8m((const T*)g.lz.x + (size_t)m * g.lz.ld + cc, nc, x);
-    ld8m((const T*)g.res.x + (size_t)m * g.res.ld + cc, nc, r);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      o[j] = lazy_apply(x[j], ax[cv * 8 + j], g.lz.act) * sc + lazy_apply(r[j], ar[cv * 8 + j], g.res.act);
-    st8m(OUT + (size_t)m * g.C + cc, nc, o);
+    for (int v = 0; v < RVPT; ++v) {
+      const int cv = tv + v * geo.TPR;
+      if (v < geo.VPT && cv < NV) {
+        const int c = cv * 8;
+        float x[8], r[8], o[8];
+        ld8((const T*)g.lz.x + (size_t)m * g.lz.ld + c, x);
+        ld8((const T*)g.res.x + (size_t)m * g.res.ld + c, r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          o[j] = lazy_apply(x[j], ax[c + j], g.lz.act) * sc + lazy_apply(r[j], ar[c + j], g.res.act);
+        st8(OUT + (size_t)m * C + c, o);
+      }
+    }
   }
 }
 
@@ -330,7 +411,7 @@ __global__ void k_bn_infer_stats(int64_t n, const float* mm, const float* mv, co
 
 static int lazy_checks(const edet_lazy* x, const edet_pyramid* p, int C) {
   EDET_REQUIRE(x && p && x->x, "lazy: null argument");
-  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0, "lazy: need C%%8==0, ld%%8==0 (C=%d ld=%d)", C, x->ld);
+  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0 && C <= 8 * 256 * RVPT, "lazy: need C%%8==0, ld%%8==0, C<=4096 (C=%d ld=%d)", C, x->ld);
   EDET_REQUIRE(p->nseg >= 1 && p->nseg <= EDET_MAX_SEG, "lazy: bad pyramid");
   EDET_REQUIRE(x->gate == nullptr || p->nseg == 1, "lazy: gate needs one segment");
   return EDET_OK;
@@ -342,6 +423,8 @@ using namespace edet;
 
 extern "C" {
 
+static dim3 row_block(const RowGeom& geo) { return dim3(geo.TPR * geo.R); }
+
 int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, int C,
                          const void* dv, const float* dv_scale, const float* dsq,
                          const edet_segout* grads, edet_stream_t stream) {
@@ -351,10 +434,12 @@ int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, i
   EDET_REQUIRE(dsq == nullptr || p->nseg == 1, "lazy_bwd_reduce: dsq needs one segment");
   LArgs g{};
   g.lz = *x; g.p = *p; g.grads = *grads; g.dv = dv; g.dv_scale = dv_scale; g.dsq = dsq; g.C = C;
-  g.ncb = cdiv(C, RCB);
-  const int nb = total_chunks(*p, RCH) * g.ncb;
+  g.geo = row_geom(C);
+  const int nb = total_chunks(*p, g.geo.CH);
+  const size_t lds = 2 * C * sizeof(float2) + 2 * (size_t)g.geo.R * C * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_lazy_bwd_reduce<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, g);
+    const int grid = nb < 2048 ? nb : 2048;
+    if (nb) hipLaunchKernelGGL(k_lazy_bwd_reduce<T>, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
     return check_launch("edet lazy_bwd_reduce");
   });
 }
@@ -371,10 +456,11 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
   LArgs g{};
   g.lz = *x; g.p = *p; if (grads) g.grads = *grads; g.dv = dv; g.dx = dx; g.dv_scale = dv_scale;
   g.dsq = dsq; g.C = C; g.accumulate = accumulate;
-  g.ncb = cdiv(C, RCB);
-  const int nb = total_chunks(*p, RCH) * g.ncb;
+  g.geo = row_geom(C);
+  const int nb = total_chunks(*p, g.geo.CH);
+  const size_t lds = 3 * C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_lazy_bwd_apply<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, g);
+    if (nb) hipLaunchKernelGGL(k_lazy_bwd_apply<T>, dim3(nb), row_block(g.geo), lds, (hipStream_t)stream, g);
     return check_launch("edet lazy_bwd_apply");
   });
 }
@@ -382,17 +468,18 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
 static int img_reduce(int dtype, bool gategrad, const edet_lazy* x, int B, int HW, int C,
                       const void* dv, float* out, hipStream_t s) {
   EDET_REQUIRE(x && out && x->x && (!gategrad || dv), "se reduce: null argument");
-  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0, "se reduce: need C%%8==0");
+  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0 && C <= 8 * 256 * RVPT, "se reduce: need C%%8==0");
   LArgs g{};
   g.lz = *x; g.lz.gate = nullptr;  // the pre-gate value
   g.p.nseg = 1; g.p.batch = B; g.p.row_off[0] = 0; g.p.H[0] = HW; g.p.W[0] = 1;
   g.dv = dv; g.out = out; g.C = C; g.hw = HW;
-  g.ncb = cdiv(C, RCB);
-  g.chunks_per_img = cdiv(HW, RCH);
-  const int nb = B * g.chunks_per_img * g.ncb;
+  g.geo = row_geom(C);
+  g.chunks_per_img = cdiv(HW, g.geo.CH);
+  const int nb = B * g.chunks_per_img;
+  const size_t lds = C * sizeof(float2) + (size_t)g.geo.R * C * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (gategrad) hipLaunchKernelGGL((k_img_reduce<T, true>), dim3(nb), dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((k_img_reduce<T, false>), dim3(nb), dim3(256), 0, s, g);
+    if (gategrad) hipLaunchKernelGGL((k_img_reduce<T, true>), dim3(nb), row_block(g.geo), lds, s, g);
+    else hipLaunchKernelGGL((k_img_reduce<T, false>), dim3(nb), row_block(g.geo), lds, s, g);
     return check_launch("edet se reduce");
   });
 }
@@ -437,10 +524,11 @@ int edet_residual_fwd(int dtype, const edet_lazy* x, const edet_lazy* res,
   EDET_REQUIRE(out, "residual_fwd: null out");
   LArgs g{};
   g.lz = *x; g.res = *res; g.p = *p; g.dv_scale = scale; g.dx = out; g.C = C;
-  g.ncb = cdiv(C, RCB);
-  const int nb = total_chunks(*p, RCH) * g.ncb;
+  g.geo = row_geom(C);
+  const int nb = total_chunks(*p, g.geo.CH);
+  const size_t lds = 2 * C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_residual<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, g);
+    if (nb) hipLaunchKernelGGL(k_residual<T>, dim3(nb), row_block(g.geo), lds, (hipStream_t)stream, g);
     return check_launch("edet residual");
   });
 }

@@ -91,65 +91,100 @@ __device__ __forceinline__ void prep_xf(const DwArgs& g, float2* xf, float* gt, 
   }
 }
 
+// Persistent: block w owns channel block (w % ncb) and every G-th spatial tile; BN statistics
+// stay in registers until the segment changes (one flush per block and segment).
 template <typename T, int K, int S>
 __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
   constexpr int IH = (DTS - 1) * S + K, IW = IH;
   __shared__ __attribute__((aligned(16))) float tile[IH * IW * DCB];
+  __shared__ __attribute__((aligned(16))) T otile[DTS * DTS * DCB];
   __shared__ float2 xf[DCB];
   __shared__ float gt[DCB];
   __shared__ float red[2][8][DCB];
   const int tid = threadIdx.x, c = tid & 31, r = tid >> 5;
-
-  int id = blockIdx.x;
-  const int cb = id % g.ncb;
-  id /= g.ncb;
-  int seg, n, ty, tx;
-  locate_tile(g.pout, id, seg, n, ty, tx);
-  const int OH = g.pout.H[seg], OW = g.pout.W[seg], H = g.pin.H[seg], W = g.pin.W[seg];
+  const int w = blockIdx.x;
+  const int cb = w % g.ncb, G = gridDim.x / g.ncb;
   const int c0 = cb * DCB;
-  const int pt = same_pad(H, K, S), pl = same_pad(W, K, S);
-  const int oy0 = ty * DTS, ox0 = tx * DTS;
-
-  prep_xf(g, xf, gt, seg, n, c0);
-  __syncthreads();
-  stage_input<T, IH, IW>(g, tile, xf, gt, seg, n, oy0 * S - pt, ox0 * S - pl, c0);
-
+  const bool cvalid = (c0 + c) < g.C;
   float wr[K * K];
   const T* Wp = (const T*)g.w;
-  const bool cvalid = (c0 + c) < g.C;
 #pragma unroll
   for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(Wp[(size_t)i * g.C + c0 + c]) : 0.f;
-  __syncthreads();
-
-  float acc[DTS];
-#pragma unroll
-  for (int j = 0; j < DTS; ++j) acc[j] = 0.f;
-#pragma unroll
-  for (int kh = 0; kh < K; ++kh)
-#pragma unroll
-    for (int kw = 0; kw < K; ++kw) {
-      const float wv = wr[kh * K + kw];
-      const float* trow = tile + ((r * S + kh) * IW + kw) * DCB + c;
-#pragma unroll
-      for (int j = 0; j < DTS; ++j) acc[j] += trow[j * S * DCB] * wv;
-    }
-
-  const int oy = oy0 + r;
   T* Y = (T*)g.y;
-  const size_t obase = (size_t)g.pout.row_off[seg] + (size_t)n * OH * OW;
   float s = 0.f, q = 0.f;
-  if (oy < OH && cvalid) {
+  int cur_seg = -1;
+
+  for (int t = w / g.ncb; t < g.tiles_total; t += G) {
+    int seg, n, ty, tx;
+    locate_tile(g.pout, t, seg, n, ty, tx);
+    const int OH = g.pout.H[seg], OW = g.pout.W[seg], H = g.pin.H[seg], W = g.pin.W[seg];
+    const int pt = same_pad(H, K, S), pl = same_pad(W, K, S);
+    const int oy0 = ty * DTS, ox0 = tx * DTS;
+    __syncthreads();  // previous tile's LDS readers are done
+    if (seg != cur_seg) {
+      if (cur_seg >= 0 && g.has_stats) {
+        red[0][r][c] = s;
+        red[1][r][c] = q;
+        __syncthreads();
+        if (tid < DCB && c0 + tid < g.C) {
+          float ss = 0.f, qq = 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
+          atomicAdd(g.stats.a[cur_seg] + c0 + tid, ss);
+          atomicAdd(g.stats.b[cur_seg] + c0 + tid, qq);
+        }
+      }
+      s = 0.f;
+      q = 0.f;
+      cur_seg = seg;
+    }
+    prep_xf(g, xf, gt, seg, n, c0);
+    __syncthreads();
+    stage_input<T, IH, IW>(g, tile, xf, gt, seg, n, oy0 * S - pt, ox0 * S - pl, c0);
+    __syncthreads();
+
+    float acc[DTS];
+#pragma unroll
+    for (int j = 0; j < DTS; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < K; ++kw) {
+        const float wv = wr[kh * K + kw];
+        const float* trow = tile + ((r * S + kh) * IW + kw) * DCB + c;
+#pragma unroll
+        for (int j = 0; j < DTS; ++j) acc[j] += trow[j * S * DCB] * wv;
+      }
+    const int oy = oy0 + r;
 #pragma unroll
     for (int j = 0; j < DTS; ++j) {
-      const int ox = ox0 + j;
-      if (ox < OW) {
-        Y[(obase + (size_t)oy * OW + ox) * g.C + c0 + c] = from_f<T>(acc[j]);
+      otile[(r * DTS + j) * DCB + c] = from_f<T>(acc[j]);
+      if (oy < OH && ox0 + j < OW && cvalid) {
         s += acc[j];
         q += acc[j] * acc[j];
       }
     }
+    __syncthreads();
+    // one 16-byte vector per thread: pixel tid/4, channels (tid%4)*8 .. +8
+    {
+      const int px = tid >> 2, cv = (tid & 3) * 8;
+      const int py = oy0 + (px >> 3), pxx = ox0 + (px & 7), nc = g.C - (c0 + cv);
+      if (py < OH && pxx < OW && nc > 0) {
+        const size_t o = ((size_t)g.pout.row_off[seg] + (size_t)n * OH * OW + (size_t)py * OW + pxx) * g.C + c0 + cv;
+        if constexpr (sizeof(T) == 2) {
+          if (nc >= 8) {
+            *reinterpret_cast<uint4*>(Y + o) = *reinterpret_cast<const uint4*>(otile + px * DCB + cv);
+          } else {
+            for (int j = 0; j < nc; ++j) Y[o + j] = otile[px * DCB + cv + j];
+          }
+        } else {
+          for (int j = 0; j < 8 && j < nc; ++j) Y[o + j] = otile[px * DCB + cv + j];
+        }
+      }
+    }
   }
-  if (g.has_stats) {
+  if (cur_seg >= 0 && g.has_stats) {
+    __syncthreads();
     red[0][r][c] = s;
     red[1][r][c] = q;
     __syncthreads();
@@ -157,8 +192,8 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
       float ss = 0.f, qq = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
-      atomicAdd(g.stats.a[seg] + c0 + tid, ss);
-      atomicAdd(g.stats.b[seg] + c0 + tid, qq);
+      atomicAdd(g.stats.a[cur_seg] + c0 + tid, ss);
+      atomicAdd(g.stats.b[cur_seg] + c0 + tid, qq);
     }
   }
 }
@@ -312,8 +347,10 @@ template <typename T, int K, int S>
 static int launch_dw(int which, DwArgs g, hipStream_t s) {
   g.ncb = cdiv(g.C, DCB);
   if (which == 0) {
-    const int n = host_tiles(g.pout) * g.ncb;
-    if (n) hipLaunchKernelGGL((k_dw_fwd<T, K, S>), dim3(n), dim3(256), 0, s, g);
+    g.tiles_total = host_tiles(g.pout);
+    // about 2048 resident blocks (8 per CU), each walking tiles of one channel block
+    const int G = std::max(1, std::min(g.tiles_total, cdiv(2048, g.ncb)));
+    if (g.tiles_total) hipLaunchKernelGGL((k_dw_fwd<T, K, S>), dim3(G * g.ncb), dim3(256), 0, s, g);
   } else if (which == 1) {
     const int n = host_tiles(g.pin) * g.ncb;
     if (n) hipLaunchKernelGGL((k_dw_dgrad<T, K, S>), dim3(n), dim3(256), 0, s, g);

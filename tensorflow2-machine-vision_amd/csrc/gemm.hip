@@ -228,6 +228,213 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   }
 }
 
+// ------------------------------------------------------------------ A-resident GEMM
+// One workgroup owns BM rows and keeps its whole (lazily transformed) A tile [BM][K] in LDS,
+// then walks its columns in 64-wide chunks (A is read from HBM exactly once whatever N is —
+// the expand convs have N = 6K).  The whole C tile [BM][cols] is staged in LDS and written
+// back as one linear stream of 16-byte stores (rows are contiguous when ldc == N), so HBM
+// sees full cache lines.  For small M the columns are split over `nsplit` workgroups per row
+// tile (A re-read from L2) so the grid still fills the 256 CUs.
+constexpr int RNB = 64;
+
+template <typename T, int BM, bool LAZY>
+__global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, int cps, int LDC) {
+  constexpr int WM = BM / 2, FM = WM / 16, FN = 2;
+  const int LDA = KP + 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* As = reinterpret_cast<T*>(smem);
+  T* Bs = As + BM * LDA;
+  T* Cs = Bs + RNB * LDA;                                 // [BM][LDC] (this split's columns)
+  float* red = reinterpret_cast<float*>(Cs + BM * LDC);   // [2][LDC] per-block BN partials
+  float2* xf = reinterpret_cast<float2*>(red + 2 * LDC);  // [K] (LAZY)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  // persistent: block w owns column split (w % nsplit) and every G-th row tile, so the BN
+  // statistics leave the block once per segment instead of once per tile (same-address
+  // atomics from thousands of tiles serialise in L2).
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int G = gridDim.x / nsplit;
+  const int split = w % nsplit, wt = w / nsplit;
+  const int K = g.K, N = g.N;
+  const int ntm = cdiv(g.M, BM);
+  const int ch_begin = split * cps;
+  const int ch_end = min(cdiv(N, RNB), ch_begin + cps);
+  if (ch_begin >= ch_end) return;
+  const int cbase = ch_begin * RNB;                      // first column of this split
+  const int ncols = min(N, ch_end * RNB) - cbase;         // valid columns of this split
+  for (int c = tid; c < 2 * LDC; c += 256) red[c] = 0.f;
+  int cur_seg = -1;
+
+  for (int tm = wt; tm < ntm; tm += G) {
+  const int row0 = tm * BM;
+  const int seg = seg_of_row(g.pyr, row0);
+  const int seg_off = g.pyr.row_off[seg];
+  const int seg_end = seg_off + seg_rows(g.pyr, seg);
+  const int hw = g.pyr.H[seg] * g.pyr.W[seg];
+  if (seg != cur_seg) {
+    __syncthreads();
+    if (cur_seg >= 0 && g.has_stats)
+      for (int c = tid; c < ncols; c += 256) {
+        atomicAdd(g.stats.a[cur_seg] + cbase + c, red[c]);
+        atomicAdd(g.stats.b[cur_seg] + cbase + c, red[LDC + c]);
+        red[c] = 0.f;
+        red[LDC + c] = 0.f;
+      }
+    if constexpr (LAZY) {
+      const float inv = 1.f / (float)seg_rows(g.pyr, seg);
+      for (int k = tid; k < K; k += 256) xf[k] = bn_affine(g.lz.bn, seg, k, inv);
+    }
+    cur_seg = seg;
+    __syncthreads();
+  }
+  // ---- A tile (once per row tile)
+  const T* A = (const T*)g.a;
+  const int kv8 = KP / 8;
+  for (int v = tid; v < BM * kv8; v += 256) {
+    const int r = v / kv8, kv = (v - r * kv8) * 8;
+    const int grow = row0 + r, nk = K - kv;
+    T* dst = &As[r * LDA + kv];
+    if (grow < g.M && nk > 0) {
+      if constexpr (LAZY) {
+        float vals[8];
+        ld8m(A + (size_t)grow * g.lda + kv, nk, vals);
+        const float* gp = g.lz.gate ? g.lz.gate + (size_t)((grow - seg_off) / hw) * K : nullptr;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (j < nk) {
+            float u = lazy_apply(vals[j], xf[kv + j], g.lz.act);
+            if (gp) u *= gp[kv + j];
+            vals[j] = u;
+          } else {
+            vals[j] = 0.f;
+          }
+        }
+        st8(dst, vals);
+      } else {
+        cp8(dst, A + (size_t)grow * g.lda + kv, nk);
+      }
+    } else {
+      zero8(dst);
+    }
+  }
+  const T* B = (const T*)g.b;
+  for (int ch = ch_begin; ch < ch_end; ++ch) {
+    const int col0 = ch * RNB;
+    for (int v = tid; v < RNB * kv8; v += 256) {
+      const int n = v / kv8, kv = (v - n * kv8) * 8;
+      const int gn = col0 + n, nk = K - kv;
+      T* dst = &Bs[n * LDA + kv];
+      if (gn < N && nk > 0) cp8(dst, B + (size_t)gn * g.ldb + kv, nk);
+      else zero8(dst);
+    }
+    __syncthreads();
+
+    floatx4 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < KP; k0 += 32) {
+      if constexpr (sizeof(T) == 2) {
+        bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          af[i] = lds_frag_bf16(&As[(wm * WM + i * 16 + (lane & 15)) * LDA + k0 + 8 * (lane >> 4)]);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          bfr[j] = lds_frag_bf16(&Bs[(wn * 32 + j * 16 + (lane & 15)) * LDA + k0 + 8 * (lane >> 4)]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          float af[FM], bfr[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i) af[i] = As[(wm * WM + i * 16 + (lane & 15)) * LDA + k0 + 4 * s + (lane >> 4)];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bfr[j] = Bs[(wn * 32 + j * 16 + (lane & 15)) * LDA + k0 + 4 * s + (lane >> 4)];
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    // bias, BN statistics (fp32, accumulated in LDS across tiles), stage into the C tile
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int cl = wn * 32 + j * 16 + (lane & 15);
+      const int col = col0 + cl;
+      const float bv = (g.bias && col < N) ? g.bias[col] : 0.f;
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rl = wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          const float v = acc[i][j][r] + bv;
+          if (col - cbase < LDC) Cs[rl * LDC + col - cbase] = from_f<T>(v);
+          if (row0 + rl < seg_end && col < N) { s += v; q += v * v; }
+        }
+      if (g.has_stats) {
+        s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+        q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+        if (lane < 16 && col < N) {
+          atomicAdd(&red[col - cbase], s);
+          atomicAdd(&red[LDC + col - cbase], q);
+        }
+      }
+    }
+    __syncthreads();
+  }
+// ---- write the staged tile: one linear stream when the rows are contiguous
+  T* C = (T*)g.c;
+  const int rows = min(BM, g.M - row0);
+  if (ncols == N && g.ldc == N && (N & 7) == 0 && LDC == N) {
+    const int nvec = rows * N / 8;
+    T* dst = C + (size_t)row0 * N;
+    for (int v = tid; v < nvec; v += 256) {
+      float vals[8];
+      const T* src = Cs + v * 8;
+      if constexpr (sizeof(T) == 2) {
+        uint4 raw = *reinterpret_cast<const uint4*>(src);
+        if (!g.accumulate) { *reinterpret_cast<uint4*>(dst + v * 8) = raw; continue; }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vals[j] = to_f<T>(src[j]);
+      acc8m(dst + v * 8, 8, vals, g.accumulate);
+    }
+  } else {
+    const int cv8 = cdiv(ncols, 8);
+    const bool vec_ok = (g.ldc % 8) == 0;
+    for (int v = tid; v < rows * cv8; v += 256) {
+      const int r = v / cv8, cv = (v - r * cv8) * 8;
+      const int nn = ncols - cv;
+      float vals[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vals[j] = to_f<T>(Cs[r * LDC + cv + j]);
+      T* dst = C + (size_t)(row0 + r) * g.ldc + cbase + cv;
+      if (vec_ok) {
+        acc8m(dst, nn, vals, g.accumulate);
+      } else {
+        for (int j = 0; j < 8 && j < nn; ++j) dst[j] = from_f<T>(g.accumulate ? to_f<T>(dst[j]) + vals[j] : vals[j]);
+      }
+    }
+  }
+  }  // row tiles
+  __syncthreads();
+  if (cur_seg >= 0 && g.has_stats)
+    for (int c = tid; c < ncols; c += 256) {
+      atomicAdd(g.stats.a[cur_seg] + cbase + c, red[c]);
+      atomicAdd(g.stats.b[cur_seg] + cbase + c, red[LDC + c]);
+    }
+}
+
 // ------------------------------------------------------------------ weight gradient
 struct WgradArgs {
   const void* a;
@@ -369,6 +576,168 @@ __global__ __launch_bounds__(256) void k_wgrad(WgradArgs g) {
   if (do_db && tid < TN && n0 + tid < g.N) atomicAdd(g.db + n0 + tid, dbacc);
 }
 
+// bf16 weight gradient with natural-layout LDS images and gfx950 transposed LDS reads.
+// dW[n][k] = sum_m dY[m][n] * v(A)[m][k]: both operands are m-major in HBM, and the MFMA
+// wants 8 consecutive m per lane, so the [m][n] / [m][k] tiles are written to LDS exactly as
+// they arrive (16-byte stores) and read with ds_read_b64_tr_b16, which hands lane i of each
+// 16-lane group column i of 4 rows.  64-row stages, double-buffered in LDS with the next
+// stage prefetched into registers: one barrier per stage.
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef short v8s_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) v4s_t lds_v4s;
+
+__device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* img, int ldm, int r0, int c0) {
+  const int lane = threadIdx.x & 63, q = (lane & 15) >> 2, p = lane & 3;
+  const uint16_t* a = img + (r0 + 8 * (lane >> 4) + q) * ldm + c0 + 4 * p;
+  const v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a);
+  const v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(a + 4 * ldm));
+  const v8s_t c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, c);
+}
+
+constexpr int WT_BM = 64, WT_LDM = 64 + 8;
+
+template <bool LAZY>
+__global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
+  __shared__ __attribute__((aligned(16))) uint16_t Ds[2][WT_BM * WT_LDM];
+  __shared__ __attribute__((aligned(16))) uint16_t Xs[2][WT_BM * WT_LDM];
+  __shared__ float2 xf[EDET_MAX_SEG][64];
+  __shared__ float dbred[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int ntiles = g.ntn * g.ntk;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = lid / ntiles, tile = lid - split * ntiles;
+  const int tn = tile / g.ntk, tk = tile - tn * g.ntk;
+  const int n0 = tn * 64, kk0 = tk * 64;
+  const int m_begin = split * g.rows_per;
+  const int m_end = min(g.M, m_begin + g.rows_per);
+  const bool do_db = (g.db != nullptr) && tk == 0;
+  const uint16_t* DY = (const uint16_t*)g.dy;
+  const uint16_t* A = (const uint16_t*)g.a;
+  if constexpr (LAZY) {
+    for (int e = tid; e < g.pyr.nseg * 64; e += 256) {
+      const int sg = e >> 6, k = kk0 + (e & 63);
+      xf[sg][e & 63] = (k < g.K) ? bn_affine(g.lz.bn, sg, k, 1.f / (float)seg_rows(g.pyr, sg)) : make_float2(1.f, 0.f);
+    }
+  }
+  // each thread moves rows (tid>>3) and (tid>>3)+32, 8-column vector (tid&7)*8 of both tiles
+  const int lr = tid >> 3, lc = (tid & 7) * 8;
+  uint4 rd[2], rx[2];
+  int rseg[2];
+  auto fetch = [&](int m0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = m0 + lr + 32 * h;
+      const int sg = seg_of_row(g.pyr, row);
+      const bool live = row < m_end && row < g.pyr.row_off[sg] + seg_rows(g.pyr, sg);
+      rseg[h] = live ? sg : -1;
+      const int nn = g.N - (n0 + lc), nk = g.K - (kk0 + lc);
+      rd[h] = make_uint4(0, 0, 0, 0);
+      rx[h] = make_uint4(0, 0, 0, 0);
+      if (live && nn >= 8) rd[h] = *reinterpret_cast<const uint4*>(DY + (size_t)row * g.lddy + n0 + lc);
+      else if (live && nn > 0) {
+        float v[8];
+        ld8m(DY + (size_t)row * g.lddy + n0 + lc, nn, v);
+        uint16_t t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = from_f<uint16_t>(v[j]);
+        rd[h] = *reinterpret_cast<uint4*>(t);
+      }
+      if (live && nk >= 8) rx[h] = *reinterpret_cast<const uint4*>(A + (size_t)row * g.lda + kk0 + lc);
+      else if (live && nk > 0) {
+        float v[8];
+        ld8m(A + (size_t)row * g.lda + kk0 + lc, nk, v);
+        uint16_t t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = from_f<uint16_t>(v[j]);
+        rx[h] = *reinterpret_cast<uint4*>(t);
+      }
+    }
+  };
+  auto commit = [&](int buf, int m0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = lr + 32 * h;
+      *reinterpret_cast<uint4*>(&Ds[buf][r * WT_LDM + lc]) = rd[h];
+      uint4 x = rx[h];
+      if constexpr (LAZY) {
+        if (rseg[h] >= 0) {
+          const int row = m0 + r, sg = rseg[h];
+          const uint16_t* t = reinterpret_cast<const uint16_t*>(&x);
+          const float* gp = g.lz.gate ? g.lz.gate + (size_t)((row - g.pyr.row_off[sg]) / (g.pyr.H[sg] * g.pyr.W[sg])) * g.K + kk0 + lc : nullptr;
+          uint16_t o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float u = 0.f;
+            if (kk0 + lc + j < g.K) {
+              u = lazy_apply(to_f<uint16_t>(t[j]), xf[sg][lc + j], g.lz.act);
+              if (gp) u *= gp[j];
+            }
+            o[j] = from_f<uint16_t>(u);
+          }
+          x = *reinterpret_cast<uint4*>(o);
+        }
+      }
+      *reinterpret_cast<uint4*>(&Xs[buf][r * WT_LDM + lc]) = x;
+    }
+  };
+
+  floatx4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float dbacc = 0.f;
+  if constexpr (LAZY) __syncthreads();  // xf tables
+  if (m_begin < m_end) {
+    fetch(m_begin);
+    commit(0, m_begin);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int m0 = m_begin; m0 < m_end; m0 += WT_BM) {
+    const bool more = m0 + WT_BM < m_end;
+    if (more) fetch(m0 + WT_BM);
+#pragma unroll
+    for (int ks = 0; ks < WT_BM; ks += 32) {
+      bf16x8_t af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = tr_frag(Ds[buf], WT_LDM, ks, wn * 32 + i * 16);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = tr_frag(Xs[buf], WT_LDM, ks, wk * 32 + j * 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (do_db) {
+      const uint16_t* col = &Ds[buf][(wave * 16) * WT_LDM + lane];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) dbacc += to_f<uint16_t>(col[m * WT_LDM]);
+    }
+    if (more) commit(buf ^ 1, m0 + WT_BM);
+    __syncthreads();
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int k = kk0 + wk * 32 + j * 16 + (lane & 15);
+        if (n < g.N && k < g.K) atomicAdd(g.dw + (size_t)n * g.K + k, acc[i][j][r]);
+      }
+  if (do_db) {
+    dbred[wave][lane] = dbacc;
+    __syncthreads();
+    if (tid < 64 && n0 + tid < g.N) atomicAdd(g.db + n0 + tid, dbred[0][tid] + dbred[1][tid] + dbred[2][tid] + dbred[3][tid]);
+  }
+}
+
 // ------------------------------------------------------------------ launch helpers
 template <typename T, int BM, int BN, bool BT, bool LAZY>
 static int launch_gemm(GemmArgs g, hipStream_t s) {
@@ -381,28 +750,64 @@ static int launch_gemm(GemmArgs g, hipStream_t s) {
   return check_launch("edet gemm");
 }
 
-static int pick_bn(int N) {
-  // minimise padded columns; ties go to the wider tile (fewer A re-reads)
-  int best = 128, best_pad = cdiv(N, 128) * 128;
-  for (int bn : {64, 32}) {
-    int pad = cdiv(N, bn) * bn;
-    if (pad < best_pad) { best = bn; best_pad = pad; }
-  }
-  return best;
+template <typename T, int BM, bool LAZY>
+static size_t gemm_r_lds(int K, int KP, int LDC) {
+  return (size_t)(BM + RNB) * (KP + 8) * sizeof(T) + (size_t)BM * LDC * sizeof(T) + 2 * (size_t)LDC * sizeof(float) +
+         (LAZY ? (size_t)K * sizeof(float2) : 0);
 }
 
-template <typename T, bool BT, bool LAZY>
+template <typename T, int BM, bool LAZY>
+static int launch_gemm_r(GemmArgs g, hipStream_t s) {
+  const int KP = cdiv(g.K, 32) * 32;
+  const int ntm = cdiv(g.M, BM);
+  const int nch = cdiv(g.N, RNB);
+  int nsplit = 1;
+  while (nsplit < nch && (long)ntm * nsplit < 1024) nsplit *= 2;
+  if (nsplit > nch) nsplit = nch;
+  int cps = cdiv(nch, nsplit);
+  // narrow the per-block column range until the staged C tile fits
+  while (cps > 1 && gemm_r_lds<T, BM, LAZY>(g.K, KP, cps * RNB) > 150 * 1024) cps = cdiv(cps, 2);
+  nsplit = cdiv(nch, cps);
+  const int LDC = nsplit == 1 ? cdiv(g.N, 8) * 8 : cps * RNB;
+  const size_t lds = gemm_r_lds<T, BM, LAZY>(g.K, KP, LDC);
+  EDET_REQUIRE(lds <= 160 * 1024, "edet gemm_r: tile does not fit LDS (K=%d N=%d)", g.K, g.N);
+  if (ntm == 0) return EDET_OK;
+  // resident blocks per CU from the LDS image; the row-tile workers per split fill that once
+  const int per_cu = max(1, min(8, (int)((160 * 1024) / lds)));
+  const int G = min(ntm, max(1, cdiv(256 * per_cu, nsplit)));
+  hipLaunchKernelGGL((k_gemm_r<T, BM, LAZY>), dim3(G * nsplit), dim3(256), lds, s, g, KP, nsplit, cps, LDC);
+  return check_launch("edet gemm_r");
+}
+
+// K > 512 with one full-N tile (N <= 320): streaming K loop
+template <typename T, bool LAZY>
+static int dispatch_gemm_kloop(GemmArgs g, hipStream_t s) {
+  const int NP = cdiv(g.N, 32) * 32;
+  if (NP <= 64) return launch_gemm<T, 64, 64, true, LAZY>(g, s);
+  if (NP <= 96) return launch_gemm<T, 64, 96, true, LAZY>(g, s);
+  if (NP <= 128) return launch_gemm<T, 64, 128, true, LAZY>(g, s);
+  if (NP <= 192) return launch_gemm<T, 64, 192, true, LAZY>(g, s);
+  if (NP <= 320) return launch_gemm<T, 64, 320, true, LAZY>(g, s);
+  set_error("gemm: K=%d > 512 needs N <= 320 (N=%d)", g.K, g.N);
+  return EDET_EUNSUPPORTED;
+}
+
+template <typename T, bool LAZY>
 static int dispatch_gemm(GemmArgs g, hipStream_t s) {
-  const int bn = pick_bn(g.N);
-  const bool big = (long)cdiv(g.M, 128) * cdiv(g.N, bn) >= 512;
-  if (big) {
-    if (bn == 128) return launch_gemm<T, 128, 128, BT, LAZY>(g, s);
-    if (bn == 64) return launch_gemm<T, 128, 64, BT, LAZY>(g, s);
-    return launch_gemm<T, 128, 32, BT, LAZY>(g, s);
+  // A-resident kernel whenever its LDS image fits (<= 96 KB: >= 1 block per CU with room);
+  // BM = rows per block chosen as the largest that fits.  Otherwise stream K (N <= 320).
+  const int KP = cdiv(g.K, 32) * 32;
+  const int LDCf = cdiv(g.N, 8) * 8;
+  constexpr size_t BUDGET = 96 * 1024;
+  if (g.K <= 512) {
+    if (gemm_r_lds<T, 128, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 128, LAZY>(g, s);
+    if (gemm_r_lds<T, 64, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 64, LAZY>(g, s);
+    // wide N (> 320, beyond the k-loop kernel) splits the columns until the C tile fits
+    if (gemm_r_lds<T, 32, LAZY>(g.K, KP, LDCf) <= BUDGET ||
+        (g.N > 320 && gemm_r_lds<T, 32, LAZY>(g.K, KP, RNB) <= 150 * 1024))
+      return launch_gemm_r<T, 32, LAZY>(g, s);
   }
-  if (bn == 128) return launch_gemm<T, 64, 128, BT, LAZY>(g, s);
-  if (bn == 64) return launch_gemm<T, 64, 64, BT, LAZY>(g, s);
-  return launch_gemm<T, 64, 32, BT, LAZY>(g, s);
+  return dispatch_gemm_kloop<T, LAZY>(g, s);
 }
 
 static bool lazy_is_plain(const edet_lazy* a) {
@@ -432,22 +837,22 @@ int edet_conv1x1_fwd(int dtype, const edet_lazy* a, const edet_pyramid* rows, in
   hipStream_t s = (hipStream_t)stream;
   const bool plain = lazy_is_plain(a);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    return plain ? dispatch_gemm<T, true, false>(g, s) : dispatch_gemm<T, true, true>(g, s);
+    return plain ? dispatch_gemm<T, false>(g, s) : dispatch_gemm<T, true>(g, s);
   });
 }
 
 int edet_conv1x1_dgrad(int dtype, const void* dy, int lddy, const edet_pyramid* rows, int N,
-                       const void* wt, int K, void* dx, int lddx, int accumulate,
+                       const void* wkn, int K, void* dx, int lddx, int accumulate,
                        edet_stream_t stream) {
-  EDET_REQUIRE(dy && rows && wt && dx, "conv1x1_dgrad: null argument");
+  EDET_REQUIRE(dy && rows && wkn && dx, "conv1x1_dgrad: null argument");
   EDET_REQUIRE(lddy % 8 == 0 && K % 8 == 0 && N > 0, "conv1x1_dgrad: need lddy%%8==0, K%%8==0");
   GemmArgs g{};
-  g.a = dy; g.b = wt; g.c = dx; g.bias = nullptr; g.pyr = *rows;
-  g.lda = lddy; g.ldb = K; g.ldc = lddx;
+  g.a = dy; g.b = wkn; g.c = dx; g.bias = nullptr; g.pyr = *rows;
+  g.lda = lddy; g.ldb = cdiv(N, 8) * 8; g.ldc = lddx;
   g.M = pyr_total_rows(*rows); g.K = N; g.N = K;  // GEMM K = conv out channels
   g.accumulate = accumulate; g.has_stats = 0;
   hipStream_t s = (hipStream_t)stream;
-  EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_gemm<T, false, false>(g, s); });
+  EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_gemm<T, false>(g, s); });
 }
 
 int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, int K,
@@ -462,6 +867,20 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
   g.lda = a->ld; g.lddy = lddy; g.M = pyr_total_rows(*rows); g.K = K; g.N = N;
   g.ntn = cdiv(N, 64); g.ntk = cdiv(K, 64);
   const int tiles = g.ntn * g.ntk;
+  hipStream_t s = (hipStream_t)stream;
+  const bool plain = lazy_is_plain(a);
+  if (dtype == EDET_BF16) {
+    // ~1024 blocks, each at least 4 stages of 64 rows (stages never straddle a segment:
+    // segments start on 128-row boundaries)
+    int split = cdiv(1024, tiles);
+    const int max_split = std::max(1, cdiv(g.M, WT_BM * 4));
+    if (split > max_split) split = max_split;
+    g.rows_per = cdiv(cdiv(g.M, split), WT_BM) * WT_BM;
+    split = std::max(1, cdiv(g.M, g.rows_per));
+    if (plain) hipLaunchKernelGGL((k_wgrad_tr<false>), dim3(tiles * split), dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((k_wgrad_tr<true>), dim3(tiles * split), dim3(256), 0, s, g);
+    return check_launch("edet wgrad");
+  }
   int split = cdiv(2048, tiles);
   const int max_split = cdiv(g.M, 32 * 4);  // at least 4 row-chunks per block
   if (split > max_split) split = max_split;
@@ -469,8 +888,6 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
   g.rows_per = cdiv(cdiv(g.M, split), 32) * 32;
   split = cdiv(g.M, g.rows_per);
   if (split < 1) split = 1;
-  hipStream_t s = (hipStream_t)stream;
-  const bool plain = lazy_is_plain(a);
   EDET_DTYPE_DISPATCH(dtype, T, {
     if (plain) hipLaunchKernelGGL((k_wgrad<T, false>), dim3(tiles * split), dim3(256), 0, s, g);
     else hipLaunchKernelGGL((k_wgrad<T, true>), dim3(tiles * split), dim3(256), 0, s, g);

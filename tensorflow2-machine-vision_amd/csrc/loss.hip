@@ -12,7 +12,7 @@
 
 namespace edet {
 
-constexpr int LCLS_ROWS = 32;
+constexpr int LCLS_ROWS = 16;
 constexpr int LBOX_ROWS = 256;
 
 struct LossArgs {
@@ -40,11 +40,36 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return red[0] + red[1] + red[2] + red[3];
 }
 
+// focal loss value and d/dx for one logit (focal_loss.py:42-52, TF sigmoid CE formulation)
+__device__ __forceinline__ void focal_elem(float x, float y, float alpha, float gamma, bool g15, float& fl, float& dfl) {
+  const float z = __expf(-fabsf(x));
+  const float r = 1.f / (1.f + z);
+  const float p = x >= 0.f ? r : z * r;                  // sigmoid(x)
+  const float pt = y * p + (1.f - y) * (1.f - p);
+  const float at = y * alpha + (1.f - y) * (1.f - alpha);
+  const float om = fmaxf(1.f - pt, 0.f);
+  float mod, dmodf;                                      // (1-pt)^g and g*(1-pt)^(g-1)
+  if (g15) {
+    const float sq = sqrtf(om);
+    mod = om * sq;
+    dmodf = 1.5f * sq;
+  } else {
+    const float lg = __logf(om);
+    mod = om > 0.f ? __expf(gamma * lg) : 0.f;
+    dmodf = om > 0.f ? gamma * __expf((gamma - 1.f) * lg) : 0.f;
+  }
+  const float ce = fmaxf(x, 0.f) - x * y + __logf(1.f + z);
+  const float dpt = (2.f * y - 1.f) * p * (1.f - p);
+  fl = at * mod * ce;
+  dfl = at * (-dmodf * dpt * ce + mod * (p - y));
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_loss(LossArgs g) {
   __shared__ float red[4];
   const int tid = threadIdx.x;
   const float npos = *g.npos + 1.f;
+  const bool g15 = g.gamma == 1.5f;
   int b = blockIdx.x;
   if (b < g.nb_cls) {
     int seg, chunk;
@@ -54,34 +79,51 @@ __global__ __launch_bounds__(256) void k_loss(LossArgs g) {
     const int nr = min(LCLS_ROWS, g.p.row_off[seg] + rows - m0);
     const int AN = g.A * g.NC;
     const float inv = 1.f / (npos * (float)rows * (float)AN * g.count_scale);
-    const float gm1 = g.gamma - 1.f;
-    const T* X = (const T*)g.cls;
+    T* X = (T*)g.cls;  // logits; gradient written in place when dcls == cls
     T* D = (T*)g.dcls;
     float s = 0.f;
-    for (int e = tid; e < nr * AN; e += 256) {
-      const int r = e / AN, col = e - r * AN;
-      const int m = m0 + r;
-      const int a = col / g.NC, c = col - a * g.NC;
-      const float x = to_f<T>(X[(size_t)m * g.ldc + col]);
-      const float y = (g.cls_t[(size_t)m * g.A + a] == c) ? 1.f : 0.f;
-      const float p = 1.f / (1.f + expf(-x));
-      const float pt = y * p + (1.f - y) * (1.f - p);
-      const float at = y * g.alpha + (1.f - y) * (1.f - g.alpha);
-      const float om = 1.f - pt;
-      const float mod = powf(om, g.gamma);
-      const float ce = fmaxf(x, 0.f) - x * y + log1pf(expf(-fabsf(x)));
-      s += at * mod * ce;
-      if (D) {
-        const float dpt = (2.f * y - 1.f) * p * (1.f - p);
-        const float dmod = (om > 0.f) ? -g.gamma * powf(om, gm1) * dpt : 0.f;
-        D[(size_t)m * g.ldc + col] = from_f<T>(at * (dmod * ce + mod * (p - y)) * inv);
+    if ((g.ldc & 7) == 0 && (!D || D == X)) {
+      const int nvec = g.ldc / 8;
+      for (int e = tid; e < nr * nvec; e += 256) {
+        const int r = e / nvec, cv = (e - r * nvec) * 8;
+        const int m = m0 + r;
+        T* px = X + (size_t)m * g.ldc + cv;
+        float x[8], d[8];
+        ld8(px, x);
+        const int32_t* tr = g.cls_t + (size_t)m * g.A;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int col = cv + j;
+          d[j] = 0.f;
+          if (col < AN) {
+            const int a = col / g.NC, c = col - a * g.NC;
+            const float y = (tr[a] == c) ? 1.f : 0.f;
+            float fl, dfl;
+            focal_elem(x[j], y, g.alpha, g.gamma, g15, fl, dfl);
+            s += fl;
+            d[j] = dfl * inv;
+          }
+        }
+        if (D) st8(px, d);
       }
-    }
-    if (D && g.ldc > AN) {
-      const int pad = g.ldc - AN;
-      for (int e = tid; e < nr * pad; e += 256) {
-        const int r = e / pad;
-        D[(size_t)(m0 + r) * g.ldc + AN + (e - r * pad)] = from_f<T>(0.f);
+    } else {  // generic strides / separate gradient buffer
+      for (int e = tid; e < nr * AN; e += 256) {
+        const int r = e / AN, col = e - r * AN;
+        const int m = m0 + r;
+        const int a = col / g.NC, c = col - a * g.NC;
+        const float x = to_f<T>(X[(size_t)m * g.ldc + col]);
+        const float y = (g.cls_t[(size_t)m * g.A + a] == c) ? 1.f : 0.f;
+        float fl, dfl;
+        focal_elem(x, y, g.alpha, g.gamma, g15, fl, dfl);
+        s += fl;
+        if (D) D[(size_t)m * g.ldc + col] = from_f<T>(dfl * inv);
+      }
+      if (D && g.ldc > AN) {
+        const int pad = g.ldc - AN;
+        for (int e = tid; e < nr * pad; e += 256) {
+          const int r = e / pad;
+          D[(size_t)(m0 + r) * g.ldc + AN + (e - r * pad)] = from_f<T>(0.f);
+        }
       }
     }
     s = block_sum(s, red);
@@ -99,7 +141,7 @@ __global__ __launch_bounds__(256) void k_loss(LossArgs g) {
   const int nr = min(LBOX_ROWS, g.p.row_off[seg] + rows - m0);
   const int A4 = g.A * 4;
   const float inv = 1.f / (4.f * npos);
-  const T* P = (const T*)g.box;
+  T* P = (T*)g.box;
   T* D = (T*)g.dbox;
   const float dl = g.delta;
   float s = 0.f;

@@ -93,6 +93,32 @@ __global__ void k_dropmask(float* out, int n, float p, uint64_t seed, const int3
   out[i] = floorf(p + u) / p;
 }
 
+// [N][K] fp32 master 1x1 kernels -> [K][ldN] compute-dtype copies (ldN = roundup(N, 8)), used
+// as the B operand of the data-gradient GEMM.  table[e] = {src_off, dst_off, N, K}.
+template <typename T>
+__global__ __launch_bounds__(256) void k_transpose_cast(const float* src, T* dst, const int64_t* table) {
+  __shared__ float tile[32][33];
+  const int64_t* e = table + 4 * blockIdx.y;
+  const int N = (int)e[2], K = (int)e[3];
+  const int tk = cdiv(K, 32);
+  const int tiles = cdiv(N, 32) * tk;
+  if ((int)blockIdx.x >= tiles) return;
+  const int n0 = (blockIdx.x / tk) * 32, k0 = (blockIdx.x % tk) * 32;
+  const float* S = src + e[0];
+  T* D = dst + e[1];
+  const int ldn = cdiv(N, 8) * 8;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int r = ty; r < 32; r += 8) {
+    const int n = n0 + r, k = k0 + tx;
+    tile[r][tx] = (n < N && k < K) ? S[(size_t)n * K + k] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) {
+    const int k = k0 + r, n = n0 + tx;
+    if (k < K && n < ldn) D[(size_t)k * ldn + n] = from_f<T>(n < N ? tile[tx][r] : 0.f);
+  }
+}
+
 static int grid_for(int64_t n) {
   int64_t nb = (n + 255) / 256;
   if (nb > 2048) nb = 2048;
@@ -132,6 +158,17 @@ int edet_cast_f32(int dtype, const float* src, void* dst, int64_t n, edet_stream
   EDET_DTYPE_DISPATCH(dtype, T, {
     hipLaunchKernelGGL(k_cast<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, src, (T*)dst, n);
     return check_launch("edet cast");
+  });
+}
+
+int edet_transpose_cast(int dtype, const float* src, void* dst, const int64_t* table, int n_entries,
+                        int max_tiles, edet_stream_t stream) {
+  EDET_REQUIRE(src && dst && table && n_entries >= 0 && max_tiles >= 0, "transpose_cast: bad argument");
+  if (n_entries == 0 || max_tiles == 0) return EDET_OK;
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(k_transpose_cast<T>, dim3(max_tiles, n_entries), dim3(256), 0, (hipStream_t)stream, src,
+                       (T*)dst, table);
+    return check_launch("edet transpose_cast");
   });
 }
 

@@ -81,7 +81,7 @@ class EfficientDetNet:
             e = sp.expanded_filters
             if sp.expand_ratio != 1:
                 n = next(conv_id)
-                P.add(f"{pre}/{n}/kernel", (e, sp.input_filters), ("normal", math.sqrt(2.0 / e)), True)
+                P.add(f"{pre}/{n}/kernel", (e, sp.input_filters), ("normal", math.sqrt(2.0 / e)), True, pw=True)
                 bns["expand_w"] = f"{pre}/{n}/kernel"
                 bns["bn0"] = P.add_bn(f"{pre}/{next(bn_id)}", e, mom, eps)
                 bns["bn0"].hw = hw[0] * hw[1]
@@ -96,7 +96,8 @@ class EfficientDetNet:
             P.add(f"{pre}/se/conv2d_1/kernel", (e, R), ("normal", math.sqrt(2.0 / e)), True)
             P.add(f"{pre}/se/conv2d_1/bias", (e,), ("const", 0.0), False)
             n = next(conv_id)
-            P.add(f"{pre}/{n}/kernel", (sp.output_filters, e), ("normal", math.sqrt(2.0 / sp.output_filters)), True)
+            P.add(f"{pre}/{n}/kernel", (sp.output_filters, e), ("normal", math.sqrt(2.0 / sp.output_filters)), True,
+                  pw=True)
             bns["project_w"] = f"{pre}/{n}/kernel"
             bns["bn2"] = P.add_bn(f"{pre}/{next(bn_id)}", sp.output_filters, mom, eps)
             bns["bn2"].hw = hw[0] * hw[1]
@@ -123,7 +124,7 @@ class EfficientDetNet:
             pre = f"resample_p{l}"
             rec = {"conv": None}
             if prev_c != F:
-                P.add(f"{pre}/conv2d/kernel", (F, prev_c), ("glorot", prev_c, F), True)
+                P.add(f"{pre}/conv2d/kernel", (F, prev_c), ("glorot", prev_c, F), True, pw=True)
                 P.add(f"{pre}/conv2d/bias", (F,), ("const", 0.0), False)
                 rec["conv"] = pre
                 rec["bn"] = P.add_bn(f"{pre}/bn", F, mom, eps)
@@ -153,7 +154,7 @@ class EfficientDetNet:
                     rr = {"conv": None}
                     if src_c != F:
                         rp = f"{pre}/resample_{k}"
-                        P.add(f"{rp}/conv2d/kernel", (F, src_c), ("glorot", src_c, F), True)
+                        P.add(f"{rp}/conv2d/kernel", (F, src_c), ("glorot", src_c, F), True, pw=True)
                         P.add(f"{rp}/conv2d/bias", (F,), ("const", 0.0), False)
                         rr["conv"] = rp
                         rr["bn"] = P.add_bn(f"{rp}/bn", F, mom, eps)
@@ -161,7 +162,7 @@ class EfficientDetNet:
                     node["resample"].append(rr)
                 op = f"{pre}/op_after_combine"
                 P.add(f"{op}/separable_conv2d/depthwise_kernel", (9, F), ("glorot", 9 * F, 9), True)
-                P.add(f"{op}/separable_conv2d/pointwise_kernel", (F, F), ("glorot", F, F), True)
+                P.add(f"{op}/separable_conv2d/pointwise_kernel", (F, F), ("glorot", F, F), True, pw=True)
                 P.add(f"{op}/separable_conv2d/bias", (F,), ("const", 0.0), False)
                 node["bn"] = P.add_bn(f"{op}/batch_normalization", F, mom, eps)
                 node["bn"].hw = sizes[lvl][0] * sizes[lvl][1]
@@ -177,7 +178,7 @@ class EfficientDetNet:
             for i in range(cfg.box_class_repeats):
                 pre = f"{net}/{tag}-{i}"
                 P.add(f"{pre}/depthwise_kernel", (9, F), ("vs_fan_in", 9 * F), True)
-                P.add(f"{pre}/pointwise_kernel", (F, F), ("vs_fan_in", F), True)
+                P.add(f"{pre}/pointwise_kernel", (F, F), ("vs_fan_in", F), True, pw=True)
                 P.add(f"{pre}/bias", (F,), ("const", 0.0), False)
                 h["convs"].append(pre)
                 lv_bns = []
@@ -188,7 +189,7 @@ class EfficientDetNet:
                 h["bns"].append(lv_bns)
             pre = f"{net}/{tag}-predict"
             P.add(f"{pre}/depthwise_kernel", (9, F), ("vs_fan_in", 9 * F), True)
-            P.add(f"{pre}/pointwise_kernel", (nout, F), ("vs_fan_in", F), True)
+            P.add(f"{pre}/pointwise_kernel", (nout, F), ("vs_fan_in", F), True, pw=True)
             P.add(f"{pre}/bias", (nout,), ("const", bias0), False)
             h["predict"] = pre
             h["nout"] = nout
@@ -497,6 +498,7 @@ class EfficientDetNetTrain(EfficientDetNet):
                vp(self.step_counter), s)
         L.call("edet_opt_apply", vp(P.w), vp(P.g), vp(P.v), vp(P.ema), P.numel, P.n_l2, self.sched, vp(self.scalars),
                self.eng.dt, vp(P.wc) if P.wc is not P.w else None, s)
+        P.refresh_compute_copy(cast=False)  # transposed 1x1 copies for the next dgrad
         cfg = self.cfg
         L.call("edet_bn_update_moving", P.n_bn, vp(P.bn_tstats[0]), vp(P.bn_tstats[1]), vp(P.bn_count),
                float(cfg.batch_norm_momentum), vp(P.bn_mm), vp(P.bn_mv), s)

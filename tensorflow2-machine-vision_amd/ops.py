@@ -110,7 +110,7 @@ def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optio
         L.call("edet_conv1x1_wgrad", eng.dt, x.lazy(), x.pyr.c, K, vp(d), ld, N, vp(P.grad(wname)),
                vp(P.grad(bname) if bname else None), s)
         dx, acc = eng.tape.dst(x)
-        L.call("edet_conv1x1_dgrad", eng.dt, vp(d), ld, x.pyr.c, N, vp(P.wcv(wname)), K, vp(dx), K, acc, s)
+        L.call("edet_conv1x1_dgrad", eng.dt, vp(d), ld, x.pyr.c, N, vp(P.wtv(wname)), K, vp(dx), K, acc, s)
 
     eng.record(bwd)
     return out

@@ -172,12 +172,14 @@ def seg_out(pairs: Sequence[Tuple[torch.Tensor, torch.Tensor]]) -> L.SegOut:
 
 # --------------------------------------------------------------------------- parameters
 class ParamSpec:
-    __slots__ = ("name", "shape", "init", "l2", "offset", "size")
+    __slots__ = ("name", "shape", "init", "l2", "offset", "size", "pw", "toff")
 
-    def __init__(self, name, shape, init, l2):
+    def __init__(self, name, shape, init, l2, pw=False):
         self.name, self.shape, self.init, self.l2 = name, tuple(shape), init, l2
         self.size = int(np.prod(self.shape))
         self.offset = -1
+        self.pw = pw      # 1x1 conv kernel [N][K]: also kept transposed for the dgrad GEMM
+        self.toff = -1
 
 
 class ParamStore:
@@ -195,9 +197,9 @@ class ParamStore:
         self.finalized = False
 
     # ---- registration
-    def add(self, name: str, shape, init, l2: bool) -> str:
+    def add(self, name: str, shape, init, l2: bool, pw: bool = False) -> str:
         assert not self.finalized and name not in self.specs, name
-        self.specs[name] = ParamSpec(name, shape, init, l2)
+        self.specs[name] = ParamSpec(name, shape, init, l2, pw)
         self.order.append(name)
         return name
 
@@ -237,6 +239,20 @@ class ParamStore:
             self.wc = self.w
         else:
             self.wc = torch.empty(self.numel, dtype=compute_dtype, device=device)
+        # transposed compute copies of the 1x1 kernels ([K][roundup(N,8)]) for dgrad
+        toff, table, max_tiles = 0, [], 0
+        for n in names:
+            sp = self.specs[n]
+            if sp.pw:
+                N, K = sp.shape
+                sp.toff = toff
+                ldn = round_up(N, 8)
+                toff = round_up(toff + K * ldn, PARAM_ALIGN)
+                table.append([sp.offset, sp.toff, N, K])
+                max_tiles = max(max_tiles, ((N + 31) // 32) * ((K + 31) // 32))
+        self.wct = torch.empty(max(toff, 1), dtype=compute_dtype, device=device)
+        self.t_table = torch.tensor(np.asarray(table, np.int64).reshape(-1, 4), device=device)
+        self.t_entries, self.t_max_tiles = len(table), max_tiles
         # BN arenas
         nch = sum(bn.C for bn in self.bns)
         self.n_bn = nch
@@ -257,9 +273,12 @@ class ParamStore:
         self.finalized = True
         self.refresh_compute_copy()
 
-    def refresh_compute_copy(self):
-        if self.wc is not self.w:
-            L.call("edet_cast_f32", L.BF16, _vp(self.w), _vp(self.wc), self.numel, stream())
+    def refresh_compute_copy(self, cast: bool = True):
+        dt = L.F32 if self.compute_dtype == torch.float32 else L.BF16
+        if cast and self.wc is not self.w:
+            L.call("edet_cast_f32", dt, _vp(self.w), _vp(self.wc), self.numel, stream())
+        L.call("edet_transpose_cast", dt, _vp(self.w), _vp(self.wct), _vp(self.t_table), self.t_entries,
+               self.t_max_tiles, stream())
 
     # ---- views
     def _sl(self, name):
@@ -277,6 +296,13 @@ class ParamStore:
     def wcv(self, name) -> torch.Tensor:
         sl, shape = self._sl(name)
         return self.wc[sl].view(shape)
+
+    def wtv(self, name) -> torch.Tensor:
+        """Transposed compute copy [K][roundup(N,8)] of a 1x1 kernel."""
+        sp = self.specs[name]
+        N, K = sp.shape
+        ldn = round_up(N, 8)
+        return self.wct[sp.toff: sp.toff + K * ldn].view(K, ldn)
 
     # ---- host round trip (checkpoints, oracle parity)
     def state_dict(self) -> Dict[str, np.ndarray]:

@@ -31,7 +31,9 @@ def pyr_data(rng, pyr, C, dt, scale=1.0):
 # ----------------------------------------------------------------- conv1x1
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("M,K,N,lazy,nseg", [(300, 24, 40, 0, 1), (1000, 96, 144, 1, 1), (777, 64, 729, 2, 1),
-                                            (513, 40, 64, 3, 2), (4096, 192, 1152, 1, 1)])
+                                            (513, 40, 64, 3, 2), (4096, 192, 1152, 1, 1), (700, 480, 80, 1, 1),
+                                            (600, 16, 96, 1, 1), (300, 1152, 320, 1, 1), (260, 320, 1152, 0, 1),
+                                            (640, 672, 112, 0, 1)])
 def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
     rng = np.random.default_rng(M + K + N)
     pyr = Pyr(2, [(13, 11), (7, 5)]) if nseg == 2 else Pyr(1, [(M, 1)])
@@ -53,7 +55,8 @@ def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
 
 
 @pytest.mark.parametrize("dt", DTS)
-@pytest.mark.parametrize("M,N,K,ldy", [(300, 40, 24, 40), (777, 729, 64, 736), (2048, 1152, 192, 1152)])
+@pytest.mark.parametrize("M,N,K,ldy", [(300, 40, 24, 40), (777, 729, 64, 736), (2048, 1152, 192, 1152),
+                                       (500, 320, 1152, 320), (300, 36, 64, 40)])
 def test_conv1x1_dgrad(dt, M, N, K, ldy):
     rng = np.random.default_rng(M * 7 + N)
     pyr = Pyr(1, [(M, 1)])
@@ -61,8 +64,12 @@ def test_conv1x1_dgrad(dt, M, N, K, ldy):
     dy[:, :N] = rnd(rng, M, N)
     dy = g(dy, dt)
     w = g(rnd(rng, N, K, scale=1 / math.sqrt(N)), dt)
+    ldn = (N + 7) // 8 * 8
+    wkn = torch.zeros(K, ldn)
+    wkn[:, :N] = w.float().cpu().t()
+    wkn = g(wkn, dt)  # the transposed compute copy the dgrad GEMM consumes
     dx = g(torch.full((M, K), 0.5), dt)
-    L.call("edet_conv1x1_dgrad", DT[dt], vp(dy), ldy, pyr.c, N, vp(w), K, vp(dx), K, 1, stream())
+    L.call("edet_conv1x1_dgrad", DT[dt], vp(dy), ldy, pyr.c, N, vp(wkn), K, vp(dx), K, 1, stream())
     ref = dy[:, :N].double().cpu() @ w.double().cpu() + 0.5
     close(dx, ref, dt)
 
@@ -484,3 +491,28 @@ def test_dropmask():
     assert vals <= {0.0, 1.25}
     frac = float((o > 0).float().mean())
     assert 0.76 < frac < 0.84
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_transpose_cast(dt):
+    rng = np.random.default_rng(8)
+    shapes = [(729, 64), (24, 144), (1152, 192)]
+    src = torch.zeros(sum(n * k for n, k in shapes) + 64)
+    table, off, toff, outs = [], 0, 0, []
+    for n, k in shapes:
+        w = rnd(rng, n, k)
+        src[off: off + n * k] = w.reshape(-1)
+        ldn = (n + 7) // 8 * 8
+        table.append([off, toff, n, k])
+        outs.append((w, toff, ldn))
+        off += n * k
+        toff += k * ldn
+    dst = torch.full((toff,), 7.0, dtype=TDT[dt], device=DEV)
+    tab = torch.tensor(table, dtype=torch.int64, device=DEV)
+    mt = max(((n + 31) // 32) * ((k + 31) // 32) for n, k in shapes)
+    L.call("edet_transpose_cast", DT[dt], vp(g(src)), vp(dst), vp(tab), len(shapes), mt, stream())
+    for w, o, ldn in outs:
+        n, k = w.shape
+        got = dst[o: o + k * ldn].view(k, ldn).float().cpu()
+        close(got[:, :n], w.t(), dt)
+        assert float(got[:, n:].abs().max() if ldn > n else 0) == 0.0
