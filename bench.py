@@ -83,7 +83,7 @@ def algorithmic_bytes(name, args, es):
     if name == "edet_lazy_bwd_reduce":
         return 2 * rows(args[2]) * args[3] * es
     if name == "edet_lazy_bwd_apply":
-        return (3 + args[9]) * rows(args[2]) * args[3] * es
+        return (3 + args[10]) * rows(args[2]) * args[3] * es
     if name == "edet_detection_loss":
         p, A, NC = args[5], args[6], args[7]
         return rows(p) * A * (2 * NC * es + 2 * 4 * es + 4 + 16)
@@ -185,15 +185,13 @@ def main():
     ap.add_argument("--kernel-timing", type=int, default=1)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+    from tf2mv_amd import dist as dp
+
+    ctx = dp.init_from_env("nccl", dev)  # RCCL over xGMI for N > 1
+    world, rank = ctx.world, ctx.rank
 
     from tf2mv_amd.anchors import Anchors
     from tf2mv_amd.config import efficientnet_b0_blocks, get_efficientdet_config
@@ -202,7 +200,7 @@ def main():
     cfg = get_efficientdet_config(args.model)
     S, B = cfg.image_size, args.batch
     anchors = Anchors(cfg.min_level, cfg.max_level, (S, S), cfg.num_scales, cfg.aspect_ratios, cfg.anchor_scale, device=dev)
-    ar = (lambda t: dist.all_reduce(t)) if world > 1 else None
+    ar = dp.make_allreduce(ctx)
     model = EfficientDetNetTrain(efficientnet_b0_blocks(), cfg, anchors, dtype=args.dtype, device=dev, seed=0,
                                  world_size=world, grad_allreduce=ar, npos_allreduce=ar,
                                  lr_schedule={"warmup_steps": 100, "total_steps": 10000,
@@ -227,39 +225,29 @@ def main():
                 model.train_step(data)
             step = g.replay
         else:
-            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            model.grad_allreduce = None
-            model.npos_allreduce = None
+            # prepare (targets, N+) | N+ all-reduce | forward+loss+backward | gradient
+            # all-reduce | optimizer: the collectives run between the captured graphs
+            g0, g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g0):
+                t_pyr = model.prepare_step(data)
             with torch.cuda.graph(g1):
-                model.forward_backward(data)
+                model.compute_step(data, *t_pyr)
             with torch.cuda.graph(g2):
                 model.apply_gradients()
 
             def step():
+                g0.replay()
+                ar(model.scalars[5:6])
                 g1.replay()
-                dist.all_reduce(model.P.g)
+                ar(model.P.g)
                 g2.replay()
         torch.cuda.synchronize()
         log("[bench] graph captured")
 
     for i in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if dist:
-        tt = torch.tensor([el], device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
+    el = dp.timed(ctx, step, args.steps, torch.cuda.synchronize)
+    el = dp.max_over_ranks(ctx, el, dev)
     value = world * B * args.steps / el
     loss = float(model.scalars[0])
     gnorm = float(model.scalars[3])
@@ -269,8 +257,9 @@ def main():
     kernels = None
     if args.kernel_timing and rank == 0:
         es = 2 if args.dtype == "bf16" else 4
-        if dist:
+        if ctx.distributed:
             model.grad_allreduce = None
+            model.npos_allreduce = None
         with KernelTimer(es) as kt:
             model.train_step(data)
         agg = kt.summary()
@@ -320,9 +309,7 @@ def main():
             "kernels": kernels,
         }
         print(json.dumps(out), flush=True)
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
+    dp.shutdown(ctx)
 
 
 if __name__ == "__main__":

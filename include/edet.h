@@ -66,12 +66,15 @@ typedef struct edet_pyramid {
   int32_t W[EDET_MAX_SEG];
 } edet_pyramid;
 
-/* Training-mode batch normalisation of a raw tensor (per segment). sum/sq are the fp32
+/* Training-mode batch normalisation of a raw tensor (per segment). sum/sq are the fp64
  * per-channel sums of x and x^2 over the segment's rows, produced by the tensor's
- * producer kernel.  y = (x - mean) * rsqrt(var + eps) * gamma + beta, var biased. */
+ * producer kernel (blocks reduce in fp32, then one fp64 atomic per channel: the order of
+ * the cross-block additions no longer reaches the fp32 affine, so forward values are
+ * reproducible run to run, and var = E[x^2] - mean^2 keeps its precision over 2M rows).
+ * y = (x - mean) * rsqrt(var + eps) * gamma + beta, var biased. */
 typedef struct edet_bn {
-  const float* sum[EDET_MAX_SEG];
-  const float* sq[EDET_MAX_SEG];
+  const double* sum[EDET_MAX_SEG];
+  const double* sq[EDET_MAX_SEG];
   const float* gamma[EDET_MAX_SEG];
   const float* beta[EDET_MAX_SEG];
   float eps;
@@ -88,11 +91,17 @@ typedef struct edet_lazy {
   int32_t act;
 } edet_lazy;
 
-/* per-segment fp32 outputs (statistics: sum / sum of squares, or BN gamma/beta grads) */
+/* per-segment fp32 outputs (BN gamma / beta gradients) */
 typedef struct edet_segout {
   float* a[EDET_MAX_SEG];
   float* b[EDET_MAX_SEG];
 } edet_segout;
+
+/* per-segment fp64 BN statistics outputs of a producer: sum and sum of squares */
+typedef struct edet_statout {
+  double* sum[EDET_MAX_SEG];
+  double* sq[EDET_MAX_SEG];
+} edet_statout;
 
 typedef struct edet_fuse_input {
   edet_lazy v;          /* input value (lazy BN of a resampled conv, or a node output) */
@@ -120,7 +129,7 @@ int edet_memcpy_async(void* dst, const void* src, size_t bytes, edet_stream_t st
  * wt is [N][K] in `dtype`.  `stats` (nullable) receives per-segment column sums of y. */
 int edet_conv1x1_fwd(int dtype, const edet_lazy* a, const edet_pyramid* rows, int K,
                      const void* wt, int N, const float* bias, void* y, int ldy,
-                     int accumulate, const edet_segout* stats, edet_stream_t stream);
+                     int accumulate, const edet_statout* stats, edet_stream_t stream);
 /* dx[m][k] = sum_n dy[m][n] * w[n][k]; wkn is the transposed compute copy [K][roundup(N,8)]
  * written by edet_transpose_cast */
 int edet_conv1x1_dgrad(int dtype, const void* dy, int lddy, const edet_pyramid* rows, int N,
@@ -134,7 +143,7 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
 /* ---- depthwise k x k, stride s, TF 'SAME' padding; w is [k*k][C] in `dtype` ---- */
 int edet_dwconv_fwd(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
                     int stride, const void* w, void* y, const edet_pyramid* pout,
-                    const edet_segout* stats, edet_stream_t stream);
+                    const edet_statout* stats, edet_stream_t stream);
 int edet_dwconv_dgrad(int dtype, const void* dy, const edet_pyramid* pout, int C, int k,
                       int stride, const void* w, void* dx, const edet_pyramid* pin,
                       int accumulate, edet_stream_t stream);
@@ -144,32 +153,43 @@ int edet_dwconv_wgrad(int dtype, const edet_lazy* x, const edet_pyramid* pin, in
 
 /* ---- stem: 3x3 s2 SAME, Cin = 3, no bias; w is [3][3][3][Cout] in `dtype` ---- */
 int edet_stem_fwd(int dtype, const void* x, int B, int H, int W, const void* w, int Cout,
-                  void* y, float* sum, float* sq, edet_stream_t stream);
+                  void* y, double* sum, double* sq, edet_stream_t stream);
 int edet_stem_wgrad(int dtype, const void* x, int B, int H, int W, const void* dy, int Cout,
                     float* dw, edet_stream_t stream);
 
 /* ---- lazy-value backward: dx = d v / d x  (BN training backward, swish', SE gate) ----
  * dv_scale [nseg][batch] (nullable) multiplies dv per image (drop-connect);
  * dsq [batch][C] (nullable) is added to d(pre-gate value) (SE squeeze path, already / HW).
- * reduce: grads->a[s] += sum du * xhat (dgamma), grads->b[s] += sum du (dbeta)
- * apply : dx = scale * (du - dbeta/M - xhat * dgamma/M)   (or du when BN is off) */
+ * reduce: acc->dgamma[s] += sum du * xhat, acc->dbeta[s] += sum du   (fp64, zeroed by caller:
+ *         the sums feed every dx of the apply pass, so their cross-block order must not
+ *         reach the bf16 rounding of dx — see edet_bn)
+ * apply : dx = scale * (du - dbeta/M - xhat * dgamma/M)   (or du when BN is off);
+ *         block 0 also adds the fp32 parameter gradients grads->a[s] += dgamma,
+ *         grads->b[s] += dbeta when `grads` is non-NULL */
+typedef struct edet_bngrad64 {
+  double* dgamma[EDET_MAX_SEG];
+  double* dbeta[EDET_MAX_SEG];
+} edet_bngrad64;
 int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, int C,
                          const void* dv, const float* dv_scale, const float* dsq,
-                         const edet_segout* grads, edet_stream_t stream);
+                         const edet_bngrad64* acc, edet_stream_t stream);
 int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, int C,
                         const void* dv, const float* dv_scale, const float* dsq,
-                        const edet_segout* grads, void* dx, int accumulate,
-                        edet_stream_t stream);
+                        const edet_bngrad64* acc, const edet_segout* grads, void* dx,
+                        int accumulate, edet_stream_t stream);
 
 /* ---- squeeze-excitation ---- */
-int edet_se_squeeze(int dtype, const edet_lazy* x, int B, int HW, int C, float* s,
-                    edet_stream_t stream);            /* s += mean_hw v(x)  (zeroed s) */
-int edet_se_fwd(int B, int C, int R, const float* s, const float* w1, const float* b1,
+/* s += mean_hw v(x) into a zeroed fp64 [B][C] (fp64 cross-block sums: the squeeze feeds the
+ * forward, so it is kept reproducible like the BN statistics) */
+int edet_se_squeeze(int dtype, const edet_lazy* x, int B, int HW, int C, double* s,
+                    edet_stream_t stream);
+int edet_se_fwd(int B, int C, int R, const double* s, const float* w1, const float* b1,
                 const float* w2, const float* b2, float* z1, float* gate, edet_stream_t stream);
+/* dgate += sum_hw dv * v(x) into a zeroed fp64 [B][C] (feeds dx through se_bwd -> dsq) */
 int edet_gate_grad(int dtype, const edet_lazy* x, int B, int HW, int C, const void* dv,
-                   float* dgate, edet_stream_t stream); /* dgate += sum_hw dv * v(x) */
-int edet_se_bwd(int B, int C, int R, int HW, const float* s, const float* z1,
-                const float* gate, const float* dgate, const float* w1, const float* w2,
+                   double* dgate, edet_stream_t stream);
+int edet_se_bwd(int B, int C, int R, int HW, const double* s, const float* z1,
+                const float* gate, const double* dgate, const float* w1, const float* w2,
                 float* dw1, float* db1, float* dw2, float* db2, float* dsq,
                 edet_stream_t stream);
 
@@ -237,8 +257,8 @@ int edet_transpose_cast(int dtype, const float* src, void* dst, const int64_t* t
                         int max_tiles, edet_stream_t stream);
 /* inference-mode BN: express moving mean/var as the sums the lazy loaders expect */
 int edet_bn_inference_stats(int64_t n, const float* mmean, const float* mvar, const float* count,
-                            float* sum, float* sq, edet_stream_t stream);
-int edet_bn_update_moving(int64_t n, const float* sum, const float* sq, const float* count,
+                            double* sum, double* sq, edet_stream_t stream);
+int edet_bn_update_moving(int64_t n, const double* sum, const double* sq, const float* count,
                           float momentum, float* mmean, float* mvar, edet_stream_t stream);
 int edet_dropmask(float* out, int n, float survival, uint64_t seed, const int32_t* step,
                   edet_stream_t stream);

@@ -225,8 +225,13 @@ class RefEfficientDet:
         return weight_decay * sum((v ** 2).sum() / 2 for k, v in self.p.items() if pat.match(k))
 
     def detection_loss(self, box_pred, cls_pred, y_box, y_cls_onehot, y_mask, alpha=0.25, gamma=1.5,
-                       with_l2=True):
-        npos = sum(torch.as_tensor(np.asarray(m), dtype=self.dtype).sum() for m in y_mask) + 1.0
+                       with_l2=True, npos_sum=None, count_scale=1.0):
+        """_get_loss (efficientdet_net_train.py:41-52).  Data-parallel form (not in the
+        reference, which trains on one device): ``npos_sum`` = the all-reduced mask count and
+        ``count_scale`` = world size, so the replicas' losses sum to the global-batch loss."""
+        if npos_sum is None:
+            npos_sum = sum(torch.as_tensor(np.asarray(m), dtype=self.dtype).sum() for m in y_mask)
+        npos = torch.as_tensor(npos_sum, dtype=self.dtype) + 1.0
         loss = self.l2_loss() if with_l2 else torch.zeros((), dtype=self.dtype)
         parts = []
         for l in range(len(box_pred)):
@@ -245,7 +250,7 @@ class RefEfficientDet:
             at = yc * alpha + (1 - yc) * (1 - alpha)
             mod = (1.0 - pt) ** gamma
             ce = torch.clamp(x, min=0) - x * yc + torch.log1p(torch.exp(-x.abs()))
-            lf = (at * mod * ce / npos).sum() / x.numel()
+            lf = (at * mod * ce / npos).sum() / (x.numel() * count_scale)
             parts.append((lf.detach(), lb.detach()))
             loss = loss + lb * 50.0 + lf
         return loss, parts

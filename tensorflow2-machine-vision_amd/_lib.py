@@ -46,6 +46,14 @@ class SegOut(ctypes.Structure):
     _fields_ = [("a", c_void_p * MAX_SEG), ("b", c_void_p * MAX_SEG)]
 
 
+class StatOut(ctypes.Structure):
+    _fields_ = [("sum", c_void_p * MAX_SEG), ("sq", c_void_p * MAX_SEG)]
+
+
+class BnGrad64(ctypes.Structure):
+    _fields_ = [("dgamma", c_void_p * MAX_SEG), ("dbeta", c_void_p * MAX_SEG)]
+
+
 class FuseInput(ctypes.Structure):
     _fields_ = [("v", Lazy), ("dx", c_void_p), ("H", c_int32), ("W", c_int32),
                 ("mode", c_int32), ("accumulate", c_int32)]
@@ -59,8 +67,8 @@ class Sched(ctypes.Structure):
 
 
 P = c_void_p
-PPyr, PLazy, PSeg, PFuse, PSched = (POINTER(Pyramid), POINTER(Lazy), POINTER(SegOut),
-                                    POINTER(FuseInput), POINTER(Sched))
+PPyr, PLazy, PSeg, PStat, PBnG, PFuse, PSched = (POINTER(Pyramid), POINTER(Lazy), POINTER(SegOut), POINTER(StatOut),
+                                                 POINTER(BnGrad64), POINTER(FuseInput), POINTER(Sched))
 
 # name -> argtypes (all return int unless listed in _RESTYPE)
 SIGNATURES = {
@@ -68,16 +76,16 @@ SIGNATURES = {
     "edet_abi_version": [],
     "edet_memset_async": [P, c_int, c_size_t, P],
     "edet_memcpy_async": [P, P, c_size_t, P],
-    "edet_conv1x1_fwd": [c_int, PLazy, PPyr, c_int, P, c_int, P, P, c_int, c_int, PSeg, P],
+    "edet_conv1x1_fwd": [c_int, PLazy, PPyr, c_int, P, c_int, P, P, c_int, c_int, PStat, P],
     "edet_conv1x1_dgrad": [c_int, P, c_int, PPyr, c_int, P, c_int, P, c_int, c_int, P],
     "edet_conv1x1_wgrad": [c_int, PLazy, PPyr, c_int, P, c_int, c_int, P, P, P],
-    "edet_dwconv_fwd": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, P, PPyr, PSeg, P],
+    "edet_dwconv_fwd": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, P, PPyr, PStat, P],
     "edet_dwconv_dgrad": [c_int, P, PPyr, c_int, c_int, c_int, P, P, PPyr, c_int, P],
     "edet_dwconv_wgrad": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, PPyr, P, P],
     "edet_stem_fwd": [c_int, P, c_int, c_int, c_int, P, c_int, P, P, P, P],
     "edet_stem_wgrad": [c_int, P, c_int, c_int, c_int, P, c_int, P, P],
-    "edet_lazy_bwd_reduce": [c_int, PLazy, PPyr, c_int, P, P, P, PSeg, P],
-    "edet_lazy_bwd_apply": [c_int, PLazy, PPyr, c_int, P, P, P, PSeg, P, c_int, P],
+    "edet_lazy_bwd_reduce": [c_int, PLazy, PPyr, c_int, P, P, P, PBnG, P],
+    "edet_lazy_bwd_apply": [c_int, PLazy, PPyr, c_int, P, P, P, PBnG, PSeg, P, c_int, P],
     "edet_se_squeeze": [c_int, PLazy, c_int, c_int, c_int, P, P],
     "edet_se_fwd": [c_int, c_int, c_int, P, P, P, P, P, P, P, P],
     "edet_gate_grad": [c_int, PLazy, c_int, c_int, c_int, P, P, P],

@@ -40,19 +40,21 @@ struct LArgs {
   edet_lazy lz;
   edet_lazy res;
   edet_pyramid p;
-  edet_segout grads;
+  edet_bngrad64 acc;   // fp64 dgamma / dbeta accumulators (reduce -> apply)
+  edet_segout grads;   // fp32 parameter gradients (apply, block of chunk 0 per segment)
+  int has_grads;
   const void* dv;
   void* dx;
   const float* dv_scale;
   const float* dsq;
-  float* out;  // se_squeeze / gate_grad output [batch][C]
+  double* out64;  // se_squeeze / gate_grad output [batch][C]
   int C, accumulate, hw, chunks_per_img;
   RowGeom geo;
 };
 
 // per-channel tables in dynamic LDS: af (sc, sh), mr (mean, rstd), gb (dgamma/M, dbeta/M)
 __device__ __forceinline__ void load_tables(const edet_lazy& lz, int seg, float inv, int C, float2* af, float2* mr,
-                                            float2* gb, const edet_segout* grads) {
+                                            float2* gb, const edet_bngrad64* acc) {
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float2 a = make_float2(1.f, 0.f), b = make_float2(0.f, 1.f);
     if (lz.bn.enabled) {
@@ -61,7 +63,9 @@ __device__ __forceinline__ void load_tables(const edet_lazy& lz, int seg, float 
     }
     af[c] = a;
     if (mr) mr[c] = b;
-    if (gb) gb[c] = lz.bn.enabled ? make_float2(grads->a[seg][c] * inv, grads->b[seg][c] * inv) : make_float2(0.f, 0.f);
+    if (gb)
+      gb[c] = lz.bn.enabled ? make_float2((float)(acc->dgamma[seg][c] * (double)inv), (float)(acc->dbeta[seg][c] * (double)inv))
+                            : make_float2(0.f, 0.f);
   }
 }
 
@@ -116,8 +120,8 @@ __device__ __forceinline__ void flush_reduce(const LArgs& g, const RowGeom& geo,
   for (int c = tid; c < C; c += blockDim.x) {
     float ss = 0.f, qq = 0.f;
     for (int i = 0; i < geo.R; ++i) { ss += red[i * C + c]; qq += red[(geo.R + i) * C + c]; }
-    atomicAdd(g.grads.b[seg] + c, ss);  // dbeta
-    atomicAdd(g.grads.a[seg] + c, qq);  // dgamma
+    atomicAdd(g.acc.dbeta[seg] + c, (double)ss);
+    atomicAdd(g.acc.dgamma[seg] + c, (double)qq);
   }
   __syncthreads();
 }
@@ -182,7 +186,12 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g) {
   int seg, chunk;
   chunk_lookup(g.p, geo.CH, blockIdx.x, seg, chunk);
   const int rows = seg_rows(g.p, seg);
-  load_tables(g.lz, seg, 1.f / (float)rows, C, af, mr, gb, &g.grads);
+  load_tables(g.lz, seg, 1.f / (float)rows, C, af, mr, gb, &g.acc);
+  if (g.has_grads && chunk == 0)  // one writer per segment: fp32 parameter gradients
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      g.grads.a[seg][c] += (float)g.acc.dgamma[seg][c];
+      g.grads.b[seg][c] += (float)g.acc.dbeta[seg][c];
+    }
   __syncthreads();
   if (rr >= geo.R) return;
   const int off = g.p.row_off[seg];
@@ -257,23 +266,23 @@ __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
     }
   }
   __syncthreads();
-  const float scale = GATEGRAD ? 1.f : 1.f / (float)g.hw;
   for (int c = tid; c < C; c += blockDim.x) {
     float ss = 0.f;
     for (int i = 0; i < geo.R; ++i) ss += red[i * C + c];
-    atomicAdd(g.out + (size_t)n * C + c, ss * scale);
+    if constexpr (GATEGRAD) atomicAdd(g.out64 + (size_t)n * C + c, (double)ss);
+    else atomicAdd(g.out64 + (size_t)n * C + c, (double)ss / (double)g.hw);
   }
 }
 
 // SE excite: z1 = W1 s + b1 ; gate = sigmoid(W2 swish(z1) + b2)   (layers/se.py:36-39)
-__global__ __launch_bounds__(256) void k_se_fwd(int C, int R, const float* s, const float* w1,
+__global__ __launch_bounds__(256) void k_se_fwd(int C, int R, const double* s, const float* w1,
                                                 const float* b1, const float* w2, const float* b2,
                                                 float* z1, float* gate) {
   extern __shared__ float sh[];
   float* ss = sh;       // [C]
   float* s1 = sh + C;   // [R]
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int c = tid; c < C; c += 256) ss[c] = s[(size_t)n * C + c];
+  for (int c = tid; c < C; c += 256) ss[c] = (float)s[(size_t)n * C + c];
   __syncthreads();
   for (int r = wave; r < R; r += 4) {
     float a = 0.f;
@@ -293,8 +302,8 @@ __global__ __launch_bounds__(256) void k_se_fwd(int C, int R, const float* s, co
   }
 }
 
-__global__ __launch_bounds__(256) void k_se_bwd(int C, int R, int HW, const float* s, const float* z1,
-                                                const float* gate, const float* dgate, const float* w1,
+__global__ __launch_bounds__(256) void k_se_bwd(int C, int R, int HW, const double* s, const float* z1,
+                                                const float* gate, const double* dgate, const float* w1,
                                                 const float* w2, float* dw1, float* db1, float* dw2,
                                                 float* db2, float* dsq) {
   extern __shared__ float sh[];
@@ -304,9 +313,9 @@ __global__ __launch_bounds__(256) void k_se_bwd(int C, int R, int HW, const floa
   float* dz1 = s1 + R;       // [R]
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int c = tid; c < C; c += 256) {
-    ss[c] = s[(size_t)n * C + c];
+    ss[c] = (float)s[(size_t)n * C + c];
     const float gv = gate[(size_t)n * C + c];
-    const float d = dgate[(size_t)n * C + c] * gv * (1.f - gv);
+    const float d = (float)dgate[(size_t)n * C + c] * gv * (1.f - gv);
     dz2[c] = d;
     atomicAdd(db2 + c, d);
   }
@@ -388,25 +397,25 @@ __global__ __launch_bounds__(256) void k_residual(LArgs g) {
 
 // Keras BatchNormalization moving statistics: m -= (m - batch) * (1 - momentum), with the
 // Bessel-corrected batch variance that FusedBatchNormV3 returns in training mode.
-__global__ void k_bn_update(int64_t n, const float* sum, const float* sq, const float* count,
+__global__ void k_bn_update(int64_t n, const double* sum, const double* sq, const float* count,
                             float momentum, float* mmean, float* mvar) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float cnt = count[i];
-  const float mean = sum[i] / cnt;
-  const float var = fmaxf(sq[i] / cnt - mean * mean, 0.f);
-  const float unb = var * cnt / fmaxf(cnt - 1.f, 1.f);
-  mmean[i] -= (mmean[i] - mean) * (1.f - momentum);
+  const double cnt = count[i];
+  const double mean = sum[i] / cnt;
+  const double var = fmax(sq[i] / cnt - mean * mean, 0.0);
+  const float unb = (float)(var * cnt / fmax(cnt - 1.0, 1.0));
+  mmean[i] -= (mmean[i] - (float)mean) * (1.f - momentum);
   mvar[i] -= (mvar[i] - unb) * (1.f - momentum);
 }
 
-__global__ void k_bn_infer_stats(int64_t n, const float* mm, const float* mv, const float* count, float* sum,
-                                 float* sq) {
+__global__ void k_bn_infer_stats(int64_t n, const float* mm, const float* mv, const float* count, double* sum,
+                                 double* sq) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float c = count[i], m = mm[i];
+  const double c = count[i], m = mm[i];
   sum[i] = m * c;
-  sq[i] = (mv[i] + m * m) * c;
+  sq[i] = ((double)mv[i] + m * m) * c;
 }
 
 static int lazy_checks(const edet_lazy* x, const edet_pyramid* p, int C) {
@@ -427,13 +436,13 @@ static dim3 row_block(const RowGeom& geo) { return dim3(geo.TPR * geo.R); }
 
 int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, int C,
                          const void* dv, const float* dv_scale, const float* dsq,
-                         const edet_segout* grads, edet_stream_t stream) {
+                         const edet_bngrad64* acc, edet_stream_t stream) {
   int rc = lazy_checks(x, p, C);
   if (rc) return rc;
-  EDET_REQUIRE(dv && grads && x->bn.enabled, "lazy_bwd_reduce: needs dv, grads and an enabled BN");
+  EDET_REQUIRE(dv && acc && x->bn.enabled, "lazy_bwd_reduce: needs dv, acc and an enabled BN");
   EDET_REQUIRE(dsq == nullptr || p->nseg == 1, "lazy_bwd_reduce: dsq needs one segment");
   LArgs g{};
-  g.lz = *x; g.p = *p; g.grads = *grads; g.dv = dv; g.dv_scale = dv_scale; g.dsq = dsq; g.C = C;
+  g.lz = *x; g.p = *p; g.acc = *acc; g.dv = dv; g.dv_scale = dv_scale; g.dsq = dsq; g.C = C;
   g.geo = row_geom(C);
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 2 * C * sizeof(float2) + 2 * (size_t)g.geo.R * C * sizeof(float);
@@ -446,15 +455,17 @@ int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, i
 
 int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, int C,
                         const void* dv, const float* dv_scale, const float* dsq,
-                        const edet_segout* grads, void* dx, int accumulate,
-                        edet_stream_t stream) {
+                        const edet_bngrad64* acc, const edet_segout* grads, void* dx,
+                        int accumulate, edet_stream_t stream) {
   int rc = lazy_checks(x, p, C);
   if (rc) return rc;
   EDET_REQUIRE(dv && dx, "lazy_bwd_apply: null dv/dx");
-  EDET_REQUIRE(!x->bn.enabled || grads, "lazy_bwd_apply: BN needs the reduced grads");
+  EDET_REQUIRE(!x->bn.enabled || acc, "lazy_bwd_apply: BN needs the reduced fp64 sums");
   EDET_REQUIRE(dsq == nullptr || p->nseg == 1, "lazy_bwd_apply: dsq needs one segment");
   LArgs g{};
-  g.lz = *x; g.p = *p; if (grads) g.grads = *grads; g.dv = dv; g.dx = dx; g.dv_scale = dv_scale;
+  g.lz = *x; g.p = *p; g.dv = dv; g.dx = dx; g.dv_scale = dv_scale;
+  if (acc) g.acc = *acc;
+  if (grads && x->bn.enabled) { g.grads = *grads; g.has_grads = 1; }
   g.dsq = dsq; g.C = C; g.accumulate = accumulate;
   g.geo = row_geom(C);
   const int nb = total_chunks(*p, g.geo.CH);
@@ -466,13 +477,13 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
 }
 
 static int img_reduce(int dtype, bool gategrad, const edet_lazy* x, int B, int HW, int C,
-                      const void* dv, float* out, hipStream_t s) {
-  EDET_REQUIRE(x && out && x->x && (!gategrad || dv), "se reduce: null argument");
+                      const void* dv, double* out64, hipStream_t s) {
+  EDET_REQUIRE(x && out64 && x->x && (!gategrad || dv), "se reduce: null argument");
   EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0 && C <= 8 * 256 * RVPT, "se reduce: need C%%8==0");
   LArgs g{};
   g.lz = *x; g.lz.gate = nullptr;  // the pre-gate value
   g.p.nseg = 1; g.p.batch = B; g.p.row_off[0] = 0; g.p.H[0] = HW; g.p.W[0] = 1;
-  g.dv = dv; g.out = out; g.C = C; g.hw = HW;
+  g.dv = dv; g.out64 = out64; g.C = C; g.hw = HW;
   g.geo = row_geom(C);
   g.chunks_per_img = cdiv(HW, g.geo.CH);
   const int nb = B * g.chunks_per_img;
@@ -484,17 +495,17 @@ static int img_reduce(int dtype, bool gategrad, const edet_lazy* x, int B, int H
   });
 }
 
-int edet_se_squeeze(int dtype, const edet_lazy* x, int B, int HW, int C, float* s,
+int edet_se_squeeze(int dtype, const edet_lazy* x, int B, int HW, int C, double* s,
                     edet_stream_t stream) {
   return img_reduce(dtype, false, x, B, HW, C, nullptr, s, (hipStream_t)stream);
 }
 
 int edet_gate_grad(int dtype, const edet_lazy* x, int B, int HW, int C, const void* dv,
-                   float* dgate, edet_stream_t stream) {
+                   double* dgate, edet_stream_t stream) {
   return img_reduce(dtype, true, x, B, HW, C, dv, dgate, (hipStream_t)stream);
 }
 
-int edet_se_fwd(int B, int C, int R, const float* s, const float* w1, const float* b1,
+int edet_se_fwd(int B, int C, int R, const double* s, const float* w1, const float* b1,
                 const float* w2, const float* b2, float* z1, float* gate, edet_stream_t stream) {
   EDET_REQUIRE(s && w1 && b1 && w2 && b2 && z1 && gate && B > 0 && C > 0 && R > 0,
                "se_fwd: bad argument");
@@ -503,8 +514,8 @@ int edet_se_fwd(int B, int C, int R, const float* s, const float* w1, const floa
   return check_launch("edet se_fwd");
 }
 
-int edet_se_bwd(int B, int C, int R, int HW, const float* s, const float* z1,
-                const float* gate, const float* dgate, const float* w1, const float* w2,
+int edet_se_bwd(int B, int C, int R, int HW, const double* s, const float* z1,
+                const float* gate, const double* dgate, const float* w1, const float* w2,
                 float* dw1, float* db1, float* dw2, float* db2, float* dsq,
                 edet_stream_t stream) {
   EDET_REQUIRE(s && z1 && gate && dgate && w1 && w2 && dw1 && db1 && dw2 && db2 && dsq,
@@ -534,7 +545,7 @@ int edet_residual_fwd(int dtype, const edet_lazy* x, const edet_lazy* res,
 }
 
 int edet_bn_inference_stats(int64_t n, const float* mmean, const float* mvar, const float* count,
-                            float* sum, float* sq, edet_stream_t stream) {
+                            double* sum, double* sq, edet_stream_t stream) {
   EDET_REQUIRE(mmean && mvar && count && sum && sq, "bn_inference_stats: null argument");
   if (n <= 0) return EDET_OK;
   hipLaunchKernelGGL(k_bn_infer_stats, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n,
@@ -542,7 +553,7 @@ int edet_bn_inference_stats(int64_t n, const float* mmean, const float* mvar, co
   return check_launch("edet bn_inference_stats");
 }
 
-int edet_bn_update_moving(int64_t n, const float* sum, const float* sq, const float* count,
+int edet_bn_update_moving(int64_t n, const double* sum, const double* sq, const float* count,
                           float momentum, float* mmean, float* mvar, edet_stream_t stream) {
   EDET_REQUIRE(sum && sq && count && mmean && mvar, "bn_update_moving: null argument");
   if (n <= 0) return EDET_OK;

@@ -138,17 +138,17 @@ __host__ __device__ __forceinline__ int pyr_total_rows(const edet_pyramid& p) {
 // Per-channel affine of the lazy BN for segment `seg`: v = x * sc + sh.
 __device__ __forceinline__ float2 bn_affine(const edet_bn& bn, int seg, int c, float inv_count) {
   if (!bn.enabled) return make_float2(1.f, 0.f);
-  float mean = bn.sum[seg][c] * inv_count;
-  float var = fmaxf(bn.sq[seg][c] * inv_count - mean * mean, 0.f);
-  float r = rsqrtf(var + bn.eps);
-  float sc = bn.gamma[seg][c] * r;
-  return make_float2(sc, bn.beta[seg][c] - mean * sc);
+  const double mean = bn.sum[seg][c] * (double)inv_count;
+  const double var = fmax(bn.sq[seg][c] * (double)inv_count - mean * mean, 0.0);
+  const float r = rsqrtf((float)var + bn.eps);
+  const float sc = bn.gamma[seg][c] * r;
+  return make_float2(sc, bn.beta[seg][c] - (float)mean * sc);
 }
 // mean / rstd (for x-hat in backward)
 __device__ __forceinline__ float2 bn_mean_rstd(const edet_bn& bn, int seg, int c, float inv_count) {
-  float mean = bn.sum[seg][c] * inv_count;
-  float var = fmaxf(bn.sq[seg][c] * inv_count - mean * mean, 0.f);
-  return make_float2(mean, rsqrtf(var + bn.eps));
+  const double mean = bn.sum[seg][c] * (double)inv_count;
+  const double var = fmax(bn.sq[seg][c] * (double)inv_count - mean * mean, 0.0);
+  return make_float2((float)mean, rsqrtf((float)var + bn.eps));
 }
 
 __device__ __forceinline__ float lazy_apply(float x, float2 af, int act) {

@@ -26,7 +26,7 @@ struct DwArgs {
   float* dw;
   edet_lazy lz;
   edet_pyramid pin, pout;
-  edet_segout stats;
+  edet_statout stats;
   int C, ncb, accumulate, has_stats;
   int tiles_per_wg, tiles_total;
 };
@@ -130,8 +130,8 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
           float ss = 0.f, qq = 0.f;
 #pragma unroll
           for (int i = 0; i < 8; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
-          atomicAdd(g.stats.a[cur_seg] + c0 + tid, ss);
-          atomicAdd(g.stats.b[cur_seg] + c0 + tid, qq);
+          atomicAdd(g.stats.sum[cur_seg] + c0 + tid, (double)(ss));
+          atomicAdd(g.stats.sq[cur_seg] + c0 + tid, (double)(qq));
         }
       }
       s = 0.f;
@@ -192,8 +192,8 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
       float ss = 0.f, qq = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
-      atomicAdd(g.stats.a[cur_seg] + c0 + tid, ss);
-      atomicAdd(g.stats.b[cur_seg] + c0 + tid, qq);
+      atomicAdd(g.stats.sum[cur_seg] + c0 + tid, (double)(ss));
+      atomicAdd(g.stats.sq[cur_seg] + c0 + tid, (double)(qq));
     }
   }
 }
@@ -396,7 +396,7 @@ extern "C" {
 
 int edet_dwconv_fwd(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
                     int stride, const void* w, void* y, const edet_pyramid* pout,
-                    const edet_segout* stats, edet_stream_t stream) {
+                    const edet_statout* stats, edet_stream_t stream) {
   EDET_REQUIRE(x && w && y, "dwconv_fwd: null argument");
   EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0, "dwconv_fwd: need C%%8==0 and ld%%8==0");
   int rc = check_pyrs(pin, pout, k, stride);

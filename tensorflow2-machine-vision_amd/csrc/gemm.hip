@@ -27,7 +27,7 @@ struct GemmArgs {
   const float* bias;
   edet_lazy lz;
   edet_pyramid pyr;
-  edet_segout stats;
+  edet_statout stats;
   int lda, ldb, ldc, M, K, N;
   int accumulate, has_stats, ntm, ntn;
 };
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   __shared__ __attribute__((aligned(16))) T As[BM * GLDK];
   __shared__ __attribute__((aligned(16))) T Bs[BN * GLDK];
-  __shared__ float red[2][BN];
+  __shared__ float red[2][2][BN];  // [sum|sq][wm][col]: one writer each, summed in fixed order
   extern __shared__ float2 xf[];  // [K] lazy affine per input channel (LAZY only)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -86,8 +86,6 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     const float inv = 1.f / (float)seg_rows(g.pyr, seg);
     for (int k = tid; k < g.K; k += 256) xf[k] = bn_affine(g.lz.bn, seg, k, inv);
   }
-  if (g.has_stats)
-    for (int i = tid; i < 2 * BN; i += 256) (&red[0][0])[i] = 0.f;
   __syncthreads();
 
   floatx4 acc[FM][FN];
@@ -213,16 +211,16 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
       s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
       q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
       if (lane < 16) {
-        atomicAdd(&red[0][wn * WN + j * 16 + lane], s);
-        atomicAdd(&red[1][wn * WN + j * 16 + lane], q);
+        red[0][wm][wn * WN + j * 16 + lane] = s;
+        red[1][wm][wn * WN + j * 16 + lane] = q;
       }
     }
     __syncthreads();
     for (int i = tid; i < BN; i += 256) {
       const int col = col0 + i;
       if (col < g.N) {
-        atomicAdd(g.stats.a[seg] + col, red[0][i]);
-        atomicAdd(g.stats.b[seg] + col, red[1][i]);
+        atomicAdd(g.stats.sum[seg] + col, (double)(red[0][0][i] + red[0][1][i]));
+        atomicAdd(g.stats.sq[seg] + col, (double)(red[1][0][i] + red[1][1][i]));
       }
     }
   }
@@ -245,8 +243,11 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   T* As = reinterpret_cast<T*>(smem);
   T* Bs = As + BM * LDA;
   T* Cs = Bs + RNB * LDA;                                 // [BM][LDC] (this split's columns)
-  float* red = reinterpret_cast<float*>(Cs + BM * LDC);   // [2][LDC] per-block BN partials
-  float2* xf = reinterpret_cast<float2*>(red + 2 * LDC);  // [K] (LAZY)
+  // per-block BN partials [sum|sq][wm][LDC]: each entry has exactly one writer lane, and the
+  // two wm halves are added in a fixed order at the flush (LDS float atomics would make the
+  // block partial depend on wave timing, and BN statistics must be reproducible)
+  float* red = reinterpret_cast<float*>(Cs + BM * LDC);
+  float2* xf = reinterpret_cast<float2*>(red + 4 * LDC);  // [K] (LAZY)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -263,7 +264,7 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   if (ch_begin >= ch_end) return;
   const int cbase = ch_begin * RNB;                      // first column of this split
   const int ncols = min(N, ch_end * RNB) - cbase;         // valid columns of this split
-  for (int c = tid; c < 2 * LDC; c += 256) red[c] = 0.f;
+  for (int c = tid; c < 4 * LDC; c += 256) red[c] = 0.f;
   int cur_seg = -1;
 
   for (int tm = wt; tm < ntm; tm += G) {
@@ -276,10 +277,9 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
     __syncthreads();
     if (cur_seg >= 0 && g.has_stats)
       for (int c = tid; c < ncols; c += 256) {
-        atomicAdd(g.stats.a[cur_seg] + cbase + c, red[c]);
-        atomicAdd(g.stats.b[cur_seg] + cbase + c, red[LDC + c]);
-        red[c] = 0.f;
-        red[LDC + c] = 0.f;
+        atomicAdd(g.stats.sum[cur_seg] + cbase + c, (double)(red[c] + red[LDC + c]));
+        atomicAdd(g.stats.sq[cur_seg] + cbase + c, (double)(red[2 * LDC + c] + red[3 * LDC + c]));
+        red[c] = red[LDC + c] = red[2 * LDC + c] = red[3 * LDC + c] = 0.f;
       }
     if constexpr (LAZY) {
       const float inv = 1.f / (float)seg_rows(g.pyr, seg);
@@ -385,8 +385,8 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
         s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
         q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
         if (lane < 16 && col < N) {
-          atomicAdd(&red[col - cbase], s);
-          atomicAdd(&red[LDC + col - cbase], q);
+          red[wm * LDC + col - cbase] += s;
+          red[(2 + wm) * LDC + col - cbase] += q;
         }
       }
     }
@@ -430,8 +430,8 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   __syncthreads();
   if (cur_seg >= 0 && g.has_stats)
     for (int c = tid; c < ncols; c += 256) {
-      atomicAdd(g.stats.a[cur_seg] + cbase + c, red[c]);
-      atomicAdd(g.stats.b[cur_seg] + cbase + c, red[LDC + c]);
+      atomicAdd(g.stats.sum[cur_seg] + cbase + c, (double)(red[c] + red[LDC + c]));
+      atomicAdd(g.stats.sq[cur_seg] + cbase + c, (double)(red[2 * LDC + c] + red[3 * LDC + c]));
     }
 }
 
@@ -752,7 +752,7 @@ static int launch_gemm(GemmArgs g, hipStream_t s) {
 
 template <typename T, int BM, bool LAZY>
 static size_t gemm_r_lds(int K, int KP, int LDC) {
-  return (size_t)(BM + RNB) * (KP + 8) * sizeof(T) + (size_t)BM * LDC * sizeof(T) + 2 * (size_t)LDC * sizeof(float) +
+  return (size_t)(BM + RNB) * (KP + 8) * sizeof(T) + (size_t)BM * LDC * sizeof(T) + 4 * (size_t)LDC * sizeof(float) +
          (LAZY ? (size_t)K * sizeof(float2) : 0);
 }
 
@@ -822,7 +822,7 @@ extern "C" {
 
 int edet_conv1x1_fwd(int dtype, const edet_lazy* a, const edet_pyramid* rows, int K,
                      const void* wt, int N, const float* bias, void* y, int ldy,
-                     int accumulate, const edet_segout* stats, edet_stream_t stream) {
+                     int accumulate, const edet_statout* stats, edet_stream_t stream) {
   EDET_REQUIRE(a && rows && wt && y, "conv1x1_fwd: null argument");
   EDET_REQUIRE(K > 0 && N > 0 && a->ld % 8 == 0 && K % 8 == 0 && K <= 8192,
                "conv1x1_fwd: need K%%8==0, lda%%8==0 (K=%d lda=%d)", K, a->ld);

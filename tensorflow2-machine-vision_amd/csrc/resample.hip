@@ -15,12 +15,11 @@ namespace edet {
 // ------------------------------------------------------------------ stem
 template <typename T>
 __global__ __launch_bounds__(256) void k_stem_fwd(const T* x, int B, int H, int W, const T* w, int Cout,
-                                                  T* y, float* sum, float* sq) {
+                                                  T* y, double* sum, double* sq) {
   __shared__ float ws[27 * 64];
-  __shared__ float red[2][64];
-  const int tid = threadIdx.x, lane = tid & 63;
+  __shared__ float red[2][4][64];  // [sum|sq][wave][channel]: fixed-order block reduction
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < 27 * Cout; i += 256) ws[i] = to_f<T>(w[i]);
-  if (tid < 128) (&red[0][0])[tid] = 0.f;
   __syncthreads();
   const int OH = cdiv(H, 2), OW = cdiv(W, 2);
   const int pt = same_pad(H, 3, 2), pl = same_pad(W, 3, 2);
@@ -60,13 +59,13 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const T* x, int B, int H, int 
     for (int j = 0; j < 8; ++j) {
       const float a = valid ? acc[j] : 0.f;
       const float s = wave_sum(a), q = wave_sum(a * a);
-      if (lane == 0) { atomicAdd(&red[0][co0 + j], s); atomicAdd(&red[1][co0 + j], q); }
+      if (lane == 0) { red[0][wave][co0 + j] = s; red[1][wave][co0 + j] = q; }
     }
   }
   __syncthreads();
   if (tid < Cout) {
-    atomicAdd(sum + tid, red[0][tid]);
-    atomicAdd(sq + tid, red[1][tid]);
+    atomicAdd(sum + tid, (double)((red[0][0][tid] + red[0][1][tid]) + (red[0][2][tid] + red[0][3][tid])));
+    atomicAdd(sq + tid, (double)((red[1][0][tid] + red[1][1][tid]) + (red[1][2][tid] + red[1][3][tid])));
   }
 }
 
@@ -390,7 +389,7 @@ using namespace edet;
 extern "C" {
 
 int edet_stem_fwd(int dtype, const void* x, int B, int H, int W, const void* w, int Cout,
-                  void* y, float* sum, float* sq, edet_stream_t stream) {
+                  void* y, double* sum, double* sq, edet_stream_t stream) {
   EDET_REQUIRE(x && w && y && sum && sq, "stem_fwd: null argument");
   EDET_REQUIRE(Cout % 8 == 0 && Cout <= 64, "stem_fwd: Cout must be a multiple of 8, <= 64");
   const long px = (long)B * cdiv(H, 2) * cdiv(W, 2);

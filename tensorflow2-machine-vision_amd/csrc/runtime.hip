@@ -29,7 +29,7 @@ extern "C" {
 
 const char* edet_last_error(void) { return edet::g_err; }
 
-int edet_abi_version(void) { return 1; }
+int edet_abi_version(void) { return 2; }
 
 int edet_memset_async(void* p, int value, size_t bytes, edet_stream_t stream) {
   if (bytes == 0) return EDET_OK;

@@ -332,6 +332,9 @@ class EfficientDetNet:
 
     def _forward(self, inputs, training: bool, masks: Optional[Dict[str, torch.Tensor]] = None):
         eng, P = self.eng, self.P
+        if eng.device.type != "cuda":
+            raise RuntimeError("this model was built host-only (structure and parameters); the "
+                               "EfficientDet compute path runs only on the GPU through libedet")
         x = self._prepare_input(inputs)
         B = x.shape[0]
         assert (x.shape[1], x.shape[2]) == self.level_hw_input, "input size must match the config image_size"
@@ -459,9 +462,11 @@ class EfficientDetNetTrain(EfficientDetNet):
         return {"class_net": m[0], "box_net": m[1]}
 
     # ------------------------------------------------------------------ step
-    def forward_backward(self, data):
-        """Zero accumulators, forward, loss (fused fwd+bwd), backward.  No optimizer."""
-        eng, P = self.eng, self.P
+    def prepare_step(self, data):
+        """Zero the per-step accumulators, build the targets and count this replica's positive
+        anchors into scalars[5].  Split from the compute so a data-parallel step can all-reduce
+        N+ between the two (and capture each half in its own graph)."""
+        P = self.P
         x = data[0]
         B = x.shape[0]
         s = stream()
@@ -475,12 +480,19 @@ class EfficientDetNetTrain(EfficientDetNet):
         for seg in range(pyr.nseg):
             sl = pyr.seg_slice(seg)
             L.call("edet_count_positives", vp(t.mask[sl]), pyr.seg_rows(seg) * self.A, vp(self.scalars[5:6]), s)
-        if self.npos_allreduce is not None:
-            self.npos_allreduce(self.scalars[5:6])
-        masks = self._make_masks(B)
+        return t, pyr
+
+    def compute_step(self, data, t, pyr):
+        """Forward, fused loss (fwd+bwd) and backward with N+ already global in scalars[5]."""
+        eng = self.eng
+        x = data[0]
+        s = stream()
+        masks = self._make_masks(x.shape[0])
         eng.tape = Tape(eng, getattr(self, "grad_trace", None))
         cls, box, pyr2 = self._forward(x, True, masks)
-        # fused focal + Huber loss: gradients are written in place over the logits
+        # fused focal + Huber loss: gradients are written in place over the logits.  The focal
+        # mean runs over this replica's elements, so it is scaled by world_size to make the
+        # replicas' sum the global-batch mean (SURVEY 8e).
         L.call("edet_detection_loss", eng.dt, vp(cls.raw), cls.ld, vp(box.raw), box.ld, pyr.c, self.A, self.NC,
                vp(t.cls), vp(t.box), vp(self.scalars[5:6]), float(self.cfg.alpha), float(self.cfg.gamma), 0.1, 50.0,
                float(self.world_size), vp(cls.raw), vp(box.raw), vp(self.scalars[0:1]), vp(self.level_parts), s)
@@ -490,6 +502,14 @@ class EfficientDetNetTrain(EfficientDetNet):
         eng.tape = None
         eng.training = False
         return t
+
+    def forward_backward(self, data):
+        """Zero accumulators, targets, N+ (all-reduced when data-parallel), forward, loss,
+        backward.  No optimizer."""
+        t, pyr = self.prepare_step(data)
+        if self.npos_allreduce is not None:
+            self.npos_allreduce(self.scalars[5:6])
+        return self.compute_step(data, t, pyr)
 
     def apply_gradients(self):
         P = self.P

@@ -21,13 +21,13 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from . import _lib as L
-from .runtime import Act, BNParam, Engine, GradRec, ParamStore, Pyr, SERec, memset0, seg_out, stream, vp
+from .runtime import Act, BNParam, Engine, GradRec, ParamStore, Pyr, SERec, memset0, seg_out, stat_out, stream, vp
 
 
 def _stats_out(eng: Engine, bns: Optional[List[BNParam]]):
     if bns is None or not eng.training:
         return None
-    return seg_out([(bn.tsum, bn.tsq) for bn in bns])
+    return stat_out([(bn.tsum, bn.tsq) for bn in bns])
 
 
 def _bn_grads(bns: List[BNParam]):
@@ -46,17 +46,22 @@ def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor
         se = out.se
         B = out.pyr.batch
         HW = out.pyr.H * out.pyr.W
-        dgate = eng.zeros_f32(B, out.C)
+        dgate = torch.zeros((B, out.C), dtype=torch.float64, device=eng.device)
         L.call("edet_gate_grad", eng.dt, lz, B, HW, out.C, vp(rec.t), vp(dgate), s)
         dsq = torch.empty((B, out.C), dtype=torch.float32, device=eng.device)
         L.call("edet_se_bwd", B, out.C, se.R, HW, vp(se.s), vp(se.z1), vp(se.gate), vp(dgate),
                vp(se.w1), vp(se.w2), vp(se.dw1), vp(se.db1), vp(se.dw2), vp(se.db2), vp(dsq), s)
-    grads = None
+    grads = acc = None
     if out.bns is not None:
         grads = _bn_grads(out.bns)
-        L.call("edet_lazy_bwd_reduce", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), grads, s)
+        # fp64 dgamma/dbeta sums (edet_bngrad64): their order must not reach the rounding of dx
+        acc_t = torch.zeros((2, len(out.bns), out.C), dtype=torch.float64, device=eng.device)
+        acc = L.BnGrad64()
+        for i in range(len(out.bns)):
+            acc.dgamma[i], acc.dbeta[i] = acc_t[0, i].data_ptr(), acc_t[1, i].data_ptr()
+        L.call("edet_lazy_bwd_reduce", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, s)
     dx = eng.empty(out.pyr.rows, out.C)
-    L.call("edet_lazy_bwd_apply", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), grads,
+    L.call("edet_lazy_bwd_apply", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, grads,
            vp(dx), 0, s)
     return dx, out.C
 
@@ -71,7 +76,7 @@ def stem(eng: Engine, P: ParamStore, x: torch.Tensor, wname: str, bn: BNParam) -
     if eng.training:
         L.call("edet_stem_fwd", eng.dt, vp(x), B, H, W, vp(P.wcv(wname)), Cout, vp(y), vp(bn.tsum), vp(bn.tsq), stream())
     else:
-        scratch = eng.zeros_f32(2, Cout)
+        scratch = torch.zeros((2, Cout), dtype=torch.float64, device=eng.device)
         L.call("edet_stem_fwd", eng.dt, vp(x), B, H, W, vp(P.wcv(wname)), Cout, vp(y), vp(scratch[0]),
                vp(scratch[1]), stream())
     out = Act(y, pyr, Cout, [bn], L.ACT_SWISH, training=eng.training, name="stem")
@@ -148,7 +153,7 @@ def squeeze_excite(eng: Engine, P: ParamStore, x: Act, prefix: str, R: int):
     B, C = x.pyr.batch, x.C
     HW = x.pyr.H * x.pyr.W
     s = stream()
-    svec = eng.zeros_f32(B, C)
+    svec = torch.zeros((B, C), dtype=torch.float64, device=eng.device)  # fp64 squeeze (edet.h)
     L.call("edet_se_squeeze", eng.dt, x.lazy(), B, HW, C, vp(svec), s)
     z1 = torch.empty((B, R), dtype=torch.float32, device=eng.device)
     gate = torch.empty((B, C), dtype=torch.float32, device=eng.device)

@@ -170,6 +170,15 @@ def seg_out(pairs: Sequence[Tuple[torch.Tensor, torch.Tensor]]) -> L.SegOut:
     return so
 
 
+def stat_out(pairs: Sequence[Tuple[torch.Tensor, torch.Tensor]]) -> L.StatOut:
+    """Per-segment fp64 (sum, sum of squares) BN statistics destinations of a producer."""
+    so = L.StatOut()
+    for i, (a, b) in enumerate(pairs):
+        assert a.dtype == torch.float64 and b.dtype == torch.float64
+        so.sum[i], so.sq[i] = a.data_ptr(), b.data_ptr()
+    return so
+
+
 # --------------------------------------------------------------------------- parameters
 class ParamSpec:
     __slots__ = ("name", "shape", "init", "l2", "offset", "size", "pw", "toff")
@@ -259,8 +268,9 @@ class ParamStore:
         self.bn_mm = torch.zeros(max(nch, 1), device=device)
         self.bn_mv = torch.ones(max(nch, 1), device=device)
         self.bn_count = torch.ones(max(nch, 1), device=device)
-        self.bn_tstats = torch.zeros(2, max(nch, 1), device=device)
-        self.bn_istats = torch.zeros(2, max(nch, 1), device=device)
+        # fp64 statistics arenas (see edet_bn in include/edet.h)
+        self.bn_tstats = torch.zeros(2, max(nch, 1), dtype=torch.float64, device=device)
+        self.bn_istats = torch.zeros(2, max(nch, 1), dtype=torch.float64, device=device)
         o = 0
         for bn in self.bns:
             sl = slice(o, o + bn.C)
@@ -271,7 +281,10 @@ class ParamStore:
             bn.isum, bn.isq = self.bn_istats[0, sl], self.bn_istats[1, sl]
             o += bn.C
         self.finalized = True
-        self.refresh_compute_copy()
+        if torch.device(device).type == "cuda":
+            self.refresh_compute_copy()
+        # else: host-only store (model structure + initial parameters for CPU tools/tests);
+        # the model refuses to run its compute path on it.
 
     def refresh_compute_copy(self, cast: bool = True):
         dt = L.F32 if self.compute_dtype == torch.float32 else L.BF16

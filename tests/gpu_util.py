@@ -63,12 +63,33 @@ def make_bn(x, pyr: Pyr, C, rng, shift=0.0):
     xc = x[:, :C].double().cpu()
     for s in range(pyr.nseg):
         v = xc[pyr.seg_slice(s)]
-        su = v.sum(0).float().to(DEV)
-        sq = (v * v).sum(0).float().to(DEV)
+        su = v.sum(0).to(DEV)  # fp64 statistics arena (edet_bn.sum / sq)
+        sq = (v * v).sum(0).to(DEV)
         ga = torch.tensor(rng.uniform(0.5, 1.5, C), dtype=torch.float32, device=DEV)
         be = torch.tensor(rng.uniform(-0.5, 0.5, C) + shift, dtype=torch.float32, device=DEV)
         segs.append((su, sq, ga, be))
     return segs
+
+
+def zeros64(*shape):
+    return torch.zeros(shape, dtype=torch.float64, device=DEV)
+
+
+def stat_out(pairs):
+    so = L.StatOut()
+    for i, (a, b) in enumerate(pairs):
+        assert a.dtype == torch.float64 and b.dtype == torch.float64
+        so.sum[i], so.sq[i] = a.data_ptr(), b.data_ptr()
+    return so
+
+
+def bngrad64(nseg, C):
+    """fp64 dgamma / dbeta accumulators [2][nseg][C] and their edet_bngrad64 descriptor."""
+    t = torch.zeros((2, nseg, C), dtype=torch.float64, device=DEV)
+    d = L.BnGrad64()
+    for i in range(nseg):
+        d.dgamma[i], d.dbeta[i] = t[0, i].data_ptr(), t[1, i].data_ptr()
+    return t, d
 
 
 def seg_out(pairs):

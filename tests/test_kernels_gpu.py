@@ -13,7 +13,7 @@ import torch.nn.functional as Fn
 
 from tf2mv_amd import _lib as L
 from tf2mv_amd.runtime import Pyr, stream, vp
-from gpu_util import DEV, DT, TDT, LazyDesc, close, g, make_bn, seg_out, zeros
+from gpu_util import DEV, DT, TDT, LazyDesc, bngrad64, close, g, make_bn, seg_out, stat_out, zeros, zeros64
 
 pytestmark = pytest.mark.gpu
 DTS = ["f32", "bf16"]
@@ -44,8 +44,8 @@ def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
     w = g(rnd(rng, N, K, scale=1 / math.sqrt(K)), dt)
     b = g(rnd(rng, N), "f32")
     y = torch.empty(pyr.rows, N, dtype=TDT[dt], device=DEV)
-    st = [(zeros(N), zeros(N)) for _ in range(nseg)]
-    L.call("edet_conv1x1_fwd", DT[dt], lz.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, seg_out(st), stream())
+    st = [(zeros64(N), zeros64(N)) for _ in range(nseg)]
+    L.call("edet_conv1x1_fwd", DT[dt], lz.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, stat_out(st), stream())
     ref = lz.cpu_value() @ w.double().cpu().t() + b.double().cpu()
     for s in range(nseg):
         sl = pyr.seg_slice(s)
@@ -139,8 +139,8 @@ def test_dwconv_fwd_bwd(dt, k, s, H, W, C, lazy, nseg):
     lz = LazyDesc(x, pin, C, bn=bn, act=1 if lazy in (1, 3) else 0, gate=gate)
     w = g(rnd(rng, k * k, C, scale=0.3), dt)
     y = torch.empty(pout.rows, C, dtype=TDT[dt], device=DEV)
-    st = [(zeros(C), zeros(C)) for _ in range(nseg)]
-    L.call("edet_dwconv_fwd", DT[dt], lz.c, pin.c, C, k, s, vp(w), vp(y), pout.c, seg_out(st), stream())
+    st = [(zeros64(C), zeros64(C)) for _ in range(nseg)]
+    L.call("edet_dwconv_fwd", DT[dt], lz.c, pin.c, C, k, s, vp(w), vp(y), pout.c, stat_out(st), stream())
     v = lz.cpu_value().requires_grad_(True)
     wr = w.double().cpu().requires_grad_(True)
     ref = dw_ref(v, pin, k, s, wr)
@@ -182,9 +182,12 @@ def test_lazy_backward(dt, C, act, gate, dsq, scale, nseg):
     sc = g(torch.tensor(rng.choice([0.0, 1.25], size=(nseg, B)), dtype=torch.float32), "f32") if scale else None
     grads = [(zeros(C), zeros(C)) for _ in range(nseg)]
     so = seg_out(grads)
-    L.call("edet_lazy_bwd_reduce", DT[dt], lz.c, pyr.c, C, vp(dv), vp(sc), vp(dsqt), so, stream())
+    acc_t, acc = bngrad64(nseg, C)
+    L.call("edet_lazy_bwd_reduce", DT[dt], lz.c, pyr.c, C, vp(dv), vp(sc), vp(dsqt), acc, stream())
     dx = torch.empty(pyr.rows, C, dtype=TDT[dt], device=DEV)
-    L.call("edet_lazy_bwd_apply", DT[dt], lz.c, pyr.c, C, vp(dv), vp(sc), vp(dsqt), so, vp(dx), 0, stream())
+    L.call("edet_lazy_bwd_apply", DT[dt], lz.c, pyr.c, C, vp(dv), vp(sc), vp(dsqt), acc, so, vp(dx), 0, stream())
+    for sg in range(nseg):  # fp32 parameter gradients are the fp64 sums, written once
+        assert torch.equal(grads[sg][0], acc_t[0, sg].float()) and torch.equal(grads[sg][1], acc_t[1, sg].float())
     # reference: autograd through BN(train, batch stats recomputed) -> act -> gate, with dsq term
     xc = x.double().cpu()
     for sg in range(nseg):
@@ -223,7 +226,7 @@ def test_squeeze_excite(dt):
     lz = LazyDesc(x, pyr, C, bn=bn, act=1)
     w1, b1 = g(rnd(rng, R, C, scale=0.2)), g(rnd(rng, R, scale=0.1))
     w2, b2 = g(rnd(rng, C, R, scale=0.3)), g(rnd(rng, C, scale=0.1))
-    s = zeros(B, C)
+    s = zeros64(B, C)
     L.call("edet_se_squeeze", DT[dt], lz.c, B, H * W, C, vp(s), stream())
     z1, gate = zeros(B, R), zeros(B, C)
     L.call("edet_se_fwd", B, C, R, vp(s), vp(w1), vp(b1), vp(w2), vp(b2), vp(z1), vp(gate), stream())
@@ -236,7 +239,7 @@ def test_squeeze_excite(dt):
     gr = torch.sigmoid((zr * torch.sigmoid(zr)) @ W2.t() + B2)
     close(gate, gr.detach(), dt)
     # backward given dgate
-    dgate = g(rnd(rng, B, C))
+    dgate = rnd(rng, B, C).double().to(DEV)  # fp64 gate-gradient accumulator (edet_gate_grad)
     dws = [zeros(R, C), zeros(R), zeros(C, R), zeros(C)]
     dsq = zeros(B, C)
     L.call("edet_se_bwd", B, C, R, H * W, vp(s), vp(z1), vp(gate), vp(dgate), vp(w1), vp(w2), vp(dws[0]), vp(dws[1]),
@@ -247,7 +250,7 @@ def test_squeeze_excite(dt):
     close(dsq, sr.grad / (H * W), "f32", rtol=1e-4, atol=1e-5)
     # gate grad: sum_hw dv * v
     dv = pyr_data(rng, pyr, C, dt)
-    dg = zeros(B, C)
+    dg = zeros64(B, C)
     L.call("edet_gate_grad", DT[dt], lz.c, B, H * W, C, vp(dv), vp(dg), stream())
     close(dg, (dv.double().cpu() * v).view(B, H * W, C).sum(1), dt, scale=8)
 
@@ -354,7 +357,7 @@ def test_stem(dt):
     w = g(rnd(rng, 3, 3, 3, Co, scale=0.3), dt)
     OH, OW = (H + 1) // 2, (W + 1) // 2
     y = torch.empty(B * OH * OW, Co, dtype=TDT[dt], device=DEV)
-    su, sq = zeros(Co), zeros(Co)
+    su, sq = zeros64(Co), zeros64(Co)
     L.call("edet_stem_fwd", DT[dt], vp(x), B, H, W, vp(w), Co, vp(y), vp(su), vp(sq), stream())
     xc = x.double().cpu().permute(0, 3, 1, 2)
     ph, pw = max((OH - 1) * 2 + 3 - H, 0), max((OW - 1) * 2 + 3 - W, 0)
@@ -466,7 +469,8 @@ def test_optimizer_step():
 def test_bn_moving_update_and_inference_stats():
     rng = np.random.default_rng(4)
     n = 300
-    su, sq = g(rnd(rng, n) * 50), g(torch.rand(n) * 500 + 2500)
+    su = (rnd(rng, n) * 50).double().to(DEV)  # fp64 statistics arena
+    sq = (torch.rand(n) * 500 + 2500).double().to(DEV)
     cnt = g(torch.full((n,), 100.0))
     mm, mv = g(rnd(rng, n)), g(torch.rand(n) + 0.5)
     MM, MV = mm.double().cpu(), mv.double().cpu()
@@ -475,7 +479,7 @@ def test_bn_moving_update_and_inference_stats():
     var = sq.double().cpu() / 100 - mean ** 2
     close(mm, MM - (MM - mean) * 0.01, "f32", rtol=1e-5)
     close(mv, MV - (MV - var * 100 / 99) * 0.01, "f32", rtol=1e-5)
-    s2, q2 = zeros(n), zeros(n)
+    s2, q2 = zeros64(n), zeros64(n)
     L.call("edet_bn_inference_stats", n, vp(mm), vp(mv), vp(cnt), vp(s2), vp(q2), stream())
     m2 = s2.double().cpu() / 100
     close(m2, mm, "f32", rtol=1e-6)

@@ -14,7 +14,7 @@ import torch
 
 from tf2mv_amd import _lib as L
 from tf2mv_amd.runtime import Pyr, stream, vp
-from gpu_util import DEV, DT, TDT, LazyDesc, close, g, make_bn, seg_out, zeros
+from gpu_util import DEV, DT, TDT, LazyDesc, bngrad64, close, g, make_bn, seg_out, stat_out, zeros, zeros64
 
 pytestmark = pytest.mark.gpu
 DTS = ["f32", "bf16"]
@@ -48,8 +48,8 @@ def test_conv1x1_fwd_large(dt, kind, K, N, lazy):
     ys, sts = [], []
     for _ in range(2):
         y = torch.full((pyr.rows, N), float("nan"), dtype=TDT[dt], device=DEV)
-        st = [(zeros(N), zeros(N)) for _ in range(pyr.nseg)]
-        L.call("edet_conv1x1_fwd", DT[dt], lz.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, seg_out(st), stream())
+        st = [(zeros64(N), zeros64(N)) for _ in range(pyr.nseg)]
+        L.call("edet_conv1x1_fwd", DT[dt], lz.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, stat_out(st), stream())
         ys.append(y)
         sts.append(st)
     torch.cuda.synchronize()
@@ -122,8 +122,8 @@ def test_dwconv_fwd_large(dt, k, s, kind, C, lazy):
     ys, sts = [], []
     for _ in range(2):
         y = torch.full((pout.rows, C), float("nan"), dtype=TDT[dt], device=DEV)
-        st = [(zeros(C), zeros(C)) for _ in range(pin.nseg)]
-        L.call("edet_dwconv_fwd", DT[dt], lz.c, pin.c, C, k, s, vp(w), vp(y), pout.c, seg_out(st), stream())
+        st = [(zeros64(C), zeros64(C)) for _ in range(pin.nseg)]
+        L.call("edet_dwconv_fwd", DT[dt], lz.c, pin.c, C, k, s, vp(w), vp(y), pout.c, stat_out(st), stream())
         ys.append(y)
         sts.append(st)
     torch.cuda.synchronize()
@@ -147,9 +147,10 @@ def test_lazy_bwd_large(dt, kind, C, act):
     lz = LazyDesc(x, pyr, C, bn=bn, act=act)
     dv = g(rnd(rng, pyr.rows, C), dt)
     grads = [(zeros(C), zeros(C)) for _ in range(pyr.nseg)]  # (dgamma, dbeta)
-    L.call("edet_lazy_bwd_reduce", DT[dt], lz.c, pyr.c, C, vp(dv), None, None, seg_out(grads), stream())
+    acc_t, acc = bngrad64(pyr.nseg, C)
+    L.call("edet_lazy_bwd_reduce", DT[dt], lz.c, pyr.c, C, vp(dv), None, None, acc, stream())
     dx = torch.full((pyr.rows, C), float("nan"), dtype=TDT[dt], device=DEV)
-    L.call("edet_lazy_bwd_apply", DT[dt], lz.c, pyr.c, C, vp(dv), None, None, seg_out(grads), vp(dx), 0, stream())
+    L.call("edet_lazy_bwd_apply", DT[dt], lz.c, pyr.c, C, vp(dv), None, None, acc, seg_out(grads), vp(dx), 0, stream())
     torch.cuda.synchronize()
     xc = x.double().cpu().requires_grad_(True)
     dvc = dv.double().cpu()

@@ -160,45 +160,51 @@ def test_train_step_reference_format_equals_compact():
         assert float((a - b).norm()) <= 1e-3 * float(a.norm()) + 1e-6 * float(g1.norm()), k
 
 
-def test_train_step_bf16_close_to_fp32_oracle():
-    """bf16 storage vs the fp64 oracle.  The EfficientDet gradient at initialisation is very
-    sensitive: the fp32 GPU path itself moves to cosine 0.84-0.87 (median per-tensor change
-    ~50 %) under a 2^-9 relative input perturbation or bf16-rounded weights
-    (scripts/debug_bf16b.py, recorded in DESIGN.md).  So bf16 is held to: loss within 3 %,
-    the loss-adjacent predict-layer gradients within 5 % (cosine), whole-gradient cosine
-    above 0.5 and per-tensor gradient norms within a factor 1.6 for tensors carrying >= 1e-3
-    of the largest norm (conv biases before BN have analytically zero gradient: excluded)."""
-    m, anchors = _train_model("bf16")
-    x, boxes, cls, n = synth(5)
-    t, yb, yc, ym = make_targets(m, anchors, boxes, cls, n)
-    fm = fixed_masks(m)
-    m.fixed_masks = {"class_net": torch.tensor(fm[0]).cuda(), "box_net": torch.tensor(fm[1]).cuda()}
-    sd0 = m.state_dict()
-    ref = RefEfficientDet(m, sd0)
-    loss_r, gn_r, _, grads_r, _, _ = ref_train_step(ref, x, yb, yc, ym, {"class_net": fm[0], "box_net": fm[1]}, lr=0.01)
-    out = m.train_step((torch.tensor(x).cuda(), t))
-    loss = float(out["loss"])
-    assert np.isfinite(loss) and abs(loss - float(loss_r)) / float(loss_r) < 3e-2, (loss, float(loss_r))
-    g = m.P.grads_dict()
-    gg = {k: g[k].ravel().astype(np.float64) + (4e-5 * sd0[k].ravel() if m.P.specs[k].l2 else 0) for k in grads_r}
-    gr = {k: grads_r[k].numpy().ravel() for k in grads_r}
+def _bf16_round(a):
+    return torch.tensor(np.asarray(a, np.float32)).to(torch.bfloat16).float().numpy()
 
-    def cos(keys):
-        a = np.concatenate([gg[k] for k in keys]); b = np.concatenate([gr[k] for k in keys])
+
+def test_train_step_bf16_within_fp32_noise_floor():
+    """bf16 storage vs the fp32 path (itself pinned to the fp64 oracle by
+    test_train_step_parity_fp32).  The EfficientDet gradient at initialisation is chaotic: the
+    fp32 path run on bf16-ROUNDED weights and input -- the smallest perturbation bf16 storage
+    implies (2^-9 relative) -- already moves the gradient (cosine ~0.85, median per-tensor
+    change ~50 %, scripts/debug_bf16b.py).  That run defines the noise floor; the
+    bf16 step must stay within a small multiple of it, its loss within 3x the floor's loss
+    change (or 0.2 %), and the loss-adjacent predict-layer gradients likewise (and cosine > 0.95)."""
+    x, boxes, cls, n = synth(5)
+
+    def run(dtype, sd=None, xin=x):
+        m, anchors = _train_model(dtype)  # same seed: identical fp32 master weights
+        if sd is not None:
+            m.load_state_dict(sd)
+        t, *_ = make_targets(m, anchors, boxes, cls, n)
+        fm = fixed_masks(m)
+        m.fixed_masks = {"class_net": torch.tensor(fm[0]).cuda(), "box_net": torch.tensor(fm[1]).cuda()}
+        m.forward_backward((torch.tensor(xin).cuda(), t))
+        torch.cuda.synchronize()
+        return float(m.scalars[0]), m.P.grads_dict(), m
+
+    l32, g32, m32 = run("f32")
+    sd = m32.state_dict()
+    sdr = {k: (_bf16_round(v) if not (k.endswith("moving_mean") or k.endswith("moving_variance")) else v)
+           for k, v in sd.items()}
+    l32r, g32r, _ = run("f32", sdr, _bf16_round(x))
+    l16, g16, _ = run("bf16")
+    keys = list(g32)
+
+    def cos(ga, gb, ks):
+        a = np.concatenate([ga[k].ravel() for k in ks]).astype(np.float64)
+        b = np.concatenate([gb[k].ravel() for k in ks]).astype(np.float64)
         return float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
 
-    pred = [k for k in gr if "predict/pointwise_kernel" in k or "predict/bias" in k]
-    assert cos(pred) > 0.95, cos(pred)
-    assert cos(list(gr)) > 0.5, cos(list(gr))
-    gmax = max(np.linalg.norm(v) for v in gr.values())
-    bad = []
-    for k in gr:
-        nr = np.linalg.norm(gr[k])
-        if nr >= 1e-3 * gmax and not k.endswith("/bias"):
-            ratio = np.linalg.norm(gg[k]) / nr
-            if not (1 / 1.6 < ratio < 1.6):
-                bad.append((k, ratio))
-    assert not bad, bad
+    floor = 1.0 - cos(g32r, g32, keys)
+    dev = 1.0 - cos(g16, g32, keys)
+    assert dev <= 3.0 * floor + 0.02, (dev, floor)
+    assert abs(l16 - l32) / l32 <= max(3.0 * abs(l32r - l32) / l32, 2e-3), (l16, l32, l32r)
+    pred = [k for k in keys if "predict/pointwise_kernel" in k or "predict/bias" in k]
+    c16, c32r = cos(g16, g32, pred), cos(g32r, g32, pred)
+    assert c16 > 0.95 and 1.0 - c16 <= 3.0 * (1.0 - c32r) + 0.01, (c16, c32r)
 
 
 def test_training_reduces_loss_bf16():
@@ -208,3 +214,60 @@ def test_training_reduces_loss_bf16():
     xs = torch.tensor(x).cuda()
     losses = [float(m.train_step((xs, t))["loss"]) for _ in range(8)]
     assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
+
+
+def test_dp_two_identical_replicas_equal_double_batch():
+    """Data-parallel math on the HIP path: a world-size-2 replica whose N+ and
+    gradient all-reduces see two identical replicas (x2) must equal the single-GPU step on the
+    doubled batch [x, x] (identical shards -> per-replica BN == full-batch BN).  The real
+    two-process collective plumbing is covered over gloo in tests/test_dp_gloo.py."""
+    c = cfg()
+    anchors = Anchors(c.min_level, c.max_level, (SIZE, SIZE), c.num_scales, c.aspect_ratios, c.anchor_scale)
+    x, boxes, cls, n = synth(6)
+    fm = torch.tensor(np.ones((2, c.box_class_repeats - 1, 5, B), np.float32))
+    dbl = lambda t: t.mul_(2.0)  # noqa: E731  (SUM over two identical replicas)
+    rep = EfficientDetNetTrain(efficientnet_b0_blocks(), c, anchors, dtype="f32", seed=1, world_size=2,
+                               grad_allreduce=dbl, npos_allreduce=dbl, lr_schedule={"fixed_lr": 0.01})
+    full = EfficientDetNetTrain(efficientnet_b0_blocks(), c, anchors, dtype="f32", seed=1,
+                                lr_schedule={"fixed_lr": 0.01})
+    rep.fixed_masks = {"class_net": fm[0].cuda(), "box_net": fm[1].cuda()}
+    full.fixed_masks = {"class_net": torch.cat([fm[0], fm[0]], -1).cuda(), "box_net": torch.cat([fm[1], fm[1]], -1).cuda()}
+    t1 = anchors.generate_targets_batched(torch.tensor(boxes), torch.tensor(cls), torch.tensor(n))
+    t2 = anchors.generate_targets_batched(torch.tensor(np.concatenate([boxes, boxes])),
+                                          torch.tensor(np.concatenate([cls, cls])), torch.tensor(np.concatenate([n, n])))
+    rep.forward_backward((torch.tensor(x).cuda(), t1))
+    rep.grad_allreduce(rep.P.g)
+    full.forward_backward((torch.tensor(np.concatenate([x, x])).cuda(), t2))
+    torch.cuda.synchronize()
+    l_rep, l_full = 2 * float(rep.scalars[0]), float(full.scalars[0])
+    assert abs(l_rep - l_full) <= 1e-5 * abs(l_full), (l_rep, l_full)
+    assert float(rep.scalars[5]) == float(full.scalars[5])  # global N+
+    ga, gb = rep.P.grads_dict(), full.P.grads_dict()
+    gmax = max(np.linalg.norm(v) for v in gb.values())
+    bad = [k for k in gb if np.linalg.norm(ga[k] - gb[k]) > 1e-3 * np.linalg.norm(gb[k]) + 1e-6 * gmax]
+    assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_forward_is_reproducible(dtype):
+    """Every forward reduction that feeds later layers (BN statistics, SE squeeze) sums across
+    blocks in fp64, so two identical steps produce bit-identical forward values (loss,
+    statistics); before, 1-ulp atomics-order noise flipped max-pool near-ties between runs and
+    moved the gradient by percents.  Weight gradients still use fp32 atomics: close, not equal."""
+    m, anchors = _train_model(dtype)
+    x, boxes, cls, n = synth(4)
+    t, *_ = make_targets(m, anchors, boxes, cls, n)
+    m.fixed_masks = {k: torch.ones(2, 5, B).cuda() for k in ("class_net", "box_net")}
+    sd0 = m.state_dict()
+    xs = torch.tensor(x).cuda()
+    outs = []
+    for _ in range(3):
+        m.load_state_dict(sd0)
+        m.train_step((xs, t))
+        torch.cuda.synchronize()
+        outs.append((m.P.bn_tstats.clone(), m.level_parts.clone(), m.P.g.clone()))
+    for st, parts, g in outs[1:]:
+        # fp64 cross-block order noise (~1e-16) is all that may differ in the statistics
+        assert float(((st - outs[0][0]).abs() / (outs[0][0].abs() + 1e-30)).max()) < 1e-12
+        assert torch.allclose(parts[:5], outs[0][1][:5], rtol=1e-6, atol=0)
+        assert float((g - outs[0][2]).norm()) <= 1e-4 * float(outs[0][2].norm())
