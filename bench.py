@@ -96,6 +96,34 @@ def algorithmic_bytes(name, args, es):
     return None
 
 
+def shape_tag(name, args):
+    """Short description of a launch's problem size (per-call detail table)."""
+    def rows(p):
+        p = getattr(p, "_obj", p)
+        return sum(p.batch * p.H[i] * p.W[i] for i in range(p.nseg))
+
+    def lazy(lz):
+        lz = getattr(lz, "_obj", lz)
+        return ("bn" if lz.bn.enabled else "") + ("+sw" if lz.act else "") + ("+g" if lz.gate else "")
+
+    try:
+        if name == "edet_conv1x1_fwd":
+            return f"M={rows(args[2])} K={args[3]} N={args[5]} {lazy(args[1])}"
+        if name == "edet_conv1x1_dgrad":
+            return f"M={rows(args[3])} N={args[4]} K={args[6]} acc={args[9]}"
+        if name == "edet_conv1x1_wgrad":
+            return f"M={rows(args[2])} K={args[3]} N={args[6]} {lazy(args[1])}"
+        if name in ("edet_dwconv_fwd", "edet_dwconv_wgrad"):
+            return f"in={rows(args[2])} C={args[3]} k={args[4]} s={args[5]}"
+        if name == "edet_dwconv_dgrad":
+            return f"out={rows(args[2])} C={args[3]} k={args[4]} s={args[5]}"
+        if name in ("edet_lazy_bwd_reduce", "edet_lazy_bwd_apply"):
+            return f"M={rows(args[2])} C={args[3]} {lazy(args[1])}"
+    except Exception:  # noqa: BLE001
+        pass
+    return ""
+
+
 class KernelTimer:
     """Wraps _lib.call: HIP events on the launch stream around every libedet kernel call."""
 
@@ -115,7 +143,7 @@ class KernelTimer:
             s.record()
             r = self.orig(name, *args)
             e.record()
-            self.rec.append((name, s, e, algorithmic_bytes(name, args, self.es)))
+            self.rec.append((name, s, e, algorithmic_bytes(name, args, self.es), shape_tag(name, args)))
             return r
 
         L.call = timed
@@ -127,10 +155,22 @@ class KernelTimer:
     def __exit__(self, *exc):
         self.L.call = self.orig
 
+    def detail(self, path, top=60):
+        """Per-call table (slowest first): name, shape, us, achieved GB/s."""
+        torch.cuda.synchronize()
+        rows = []
+        for name, s, e, b, tag in self.rec:
+            ms = s.elapsed_time(e)
+            rows.append((ms, name, tag, (b / (ms * 1e6)) if (b and ms > 0) else None))
+        rows.sort(reverse=True)
+        with open(path, "w") as f:
+            for ms, name, tag, gbs in rows[:top]:
+                f.write(f"{ms * 1e3:9.1f} us  {name:24s} {tag:40s} {'' if gbs is None else f'{gbs:8.1f} GB/s'}\n")
+
     def summary(self):
         torch.cuda.synchronize()
         agg = {}
-        for name, s, e, b in self.rec:
+        for name, s, e, b, _ in self.rec:
             ms = s.elapsed_time(e)
             a = agg.setdefault(name, [0, 0.0, 0.0, True])
             a[0] += 1
@@ -263,6 +303,8 @@ def main():
         with KernelTimer(es) as kt:
             model.train_step(data)
         agg = kt.summary()
+        if os.environ.get("EDET_KERNEL_DETAIL"):
+            kt.detail(os.environ["EDET_KERNEL_DETAIL"])
         total_ms = sum(a[1] for a in agg.values())
         top = sorted(agg.items(), key=lambda kv: -kv[1][1])
         kernels = {k: {"calls": a[0], "ms": round(a[1], 4), "GBps": (round(a[2] / (a[1] * 1e6), 1) if a[3] and a[1] > 0 else None)}

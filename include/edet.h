@@ -190,8 +190,8 @@ int edet_gate_grad(int dtype, const edet_lazy* x, int B, int HW, int C, const vo
                    double* dgate, edet_stream_t stream);
 int edet_se_bwd(int B, int C, int R, int HW, const double* s, const float* z1,
                 const float* gate, const double* dgate, const float* w1, const float* w2,
-                float* dw1, float* db1, float* dw2, float* db2, float* dsq,
-                edet_stream_t stream);
+                float* dw1, float* db1, float* dw2, float* db2, float* dsq, float* dz1,
+                edet_stream_t stream); /* dz1: [B][R] scratch; weight grads accumulate (+=) */
 
 /* ---- heads: out = v(x) * scale[seg][n] + v(res) (drop-connect + residual) ---- */
 int edet_residual_fwd(int dtype, const edet_lazy* x, const edet_lazy* res,

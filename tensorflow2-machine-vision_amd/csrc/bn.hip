@@ -274,82 +274,99 @@ __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
   }
 }
 
-// SE excite: z1 = W1 s + b1 ; gate = sigmoid(W2 swish(z1) + b2)   (layers/se.py:36-39)
-__global__ __launch_bounds__(256) void k_se_fwd(int C, int R, const double* s, const float* w1,
-                                                const float* b1, const float* w2, const float* b2,
-                                                float* z1, float* gate) {
-  extern __shared__ float sh[];
-  float* ss = sh;       // [C]
-  float* s1 = sh + C;   // [R]
-  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int c = tid; c < C; c += 256) ss[c] = (float)s[(size_t)n * C + c];
-  __syncthreads();
-  for (int r = wave; r < R; r += 4) {
-    float a = 0.f;
-    for (int c = lane; c < C; c += 64) a += w1[(size_t)r * C + c] * ss[c];
-    a = wave_sum(a);
-    if (lane == 0) {
-      const float z = a + b1[r];
-      z1[(size_t)n * R + r] = z;
-      s1[r] = z / (1.f + expf(-z));
-    }
+// SE excite: z1 = W1 s + b1 ; gate = sigmoid(W2 swish(z1) + b2)   (layers/se.py:36-39).
+// The excite is tiny (B x C x R MACs) but was one block per image; it is now spread over the
+// chip: one wave per (n, r) dot product over C, then one thread per (n, c) over R.  Every
+// output (including the weight gradients) has exactly one writer: no atomics, reproducible.
+
+// z1[n][r] = sum_c w1[r][c] s[n][c] + b1[r]     (one wave per (n, r))
+__global__ __launch_bounds__(256) void k_se_reduce_c(int B, int C, int R, const double* s, const float* w1,
+                                                     const float* b1, float* z1) {
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= B * R) return;
+  const int n = item / R, r = item - n * R;
+  float a = 0.f;
+  for (int c = lane; c < C; c += 64) a += w1[(size_t)r * C + c] * (float)s[(size_t)n * C + c];
+  a = wave_sum(a);
+  if (lane == 0) z1[item] = a + b1[r];
+}
+
+// gate[n][c] = sigmoid(sum_r w2[c][r] swish(z1[n][r]) + b2[c])   (one thread per (n, c))
+__global__ __launch_bounds__(256) void k_se_excite(int B, int C, int R, const float* z1, const float* w2,
+                                                   const float* b2, float* gate) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * C) return;
+  const int n = idx / C, c = idx - n * C;
+  float a = b2[c];
+  for (int r = 0; r < R; ++r) {
+    const float z = z1[(size_t)n * R + r];
+    a += w2[(size_t)c * R + r] * (z * sigmoidf_(z));
   }
-  __syncthreads();
-  for (int c = tid; c < C; c += 256) {
-    float a = b2[c];
-    for (int r = 0; r < R; ++r) a += w2[(size_t)c * R + r] * s1[r];
-    gate[(size_t)n * C + c] = 1.f / (1.f + expf(-a));
+  gate[idx] = sigmoidf_(a);
+}
+
+// backward, pass 1: dz1[n][r] = swish'(z1) * sum_c dz2[n][c] w2[c][r],
+// dz2 = dgate * g (1 - g)   (one wave per (n, r))
+__global__ __launch_bounds__(256) void k_se_dz1(int B, int C, int R, const float* z1, const float* gate,
+                                                const double* dgate, const float* w2, float* dz1) {
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= B * R) return;
+  const int n = item / R, r = item - n * R;
+  float a = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    const float gv = gate[(size_t)n * C + c];
+    a += (float)dgate[(size_t)n * C + c] * gv * (1.f - gv) * w2[(size_t)c * R + r];
+  }
+  a = wave_sum(a);
+  if (lane == 0) {
+    const float z = z1[item];
+    const float sg = sigmoidf_(z);
+    dz1[item] = a * sg * (1.f + z * (1.f - sg));
   }
 }
 
-__global__ __launch_bounds__(256) void k_se_bwd(int C, int R, int HW, const double* s, const float* z1,
-                                                const float* gate, const double* dgate, const float* w1,
-                                                const float* w2, float* dw1, float* db1, float* dw2,
-                                                float* db2, float* dsq) {
-  extern __shared__ float sh[];
-  float* ss = sh;            // [C] squeeze input
-  float* dz2 = sh + C;       // [C]
-  float* s1 = sh + 2 * C;    // [R]
-  float* dz1 = s1 + R;       // [R]
-  const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int c = tid; c < C; c += 256) {
-    ss[c] = (float)s[(size_t)n * C + c];
-    const float gv = gate[(size_t)n * C + c];
-    const float d = (float)dgate[(size_t)n * C + c] * gv * (1.f - gv);
-    dz2[c] = d;
-    atomicAdd(db2 + c, d);
-  }
-  for (int r = tid; r < R; r += 256) {
-    const float z = z1[(size_t)n * R + r];
-    s1[r] = z / (1.f + expf(-z));
-  }
-  __syncthreads();
-  for (int e = tid; e < C * R; e += 256) {
-    const int c = e / R, r = e - c * R;
-    atomicAdd(dw2 + e, dz2[c] * s1[r]);
-  }
-  for (int r = wave; r < R; r += 4) {
-    float a = 0.f;
-    for (int c = lane; c < C; c += 64) a += dz2[c] * w2[(size_t)c * R + r];
-    a = wave_sum(a);
-    if (lane == 0) {
+// backward, pass 2 (one thread per element of the largest output):
+//   dw2[c][r] += sum_n dz2[n][c] swish(z1[n][r])     dw1[r][c] += sum_n dz1[n][r] s[n][c]
+//   db2[c]    += sum_n dz2[n][c]                     db1[r]    += sum_n dz1[n][r]
+//   dsq[n][c]  = sum_r dz1[n][r] w1[r][c] / HW
+__global__ __launch_bounds__(256) void k_se_wgrad(int B, int C, int R, int HW, const double* s, const float* z1,
+                                                  const float* gate, const double* dgate, const float* dz1,
+                                                  const float* w1, float* dw1, float* db1, float* dw2, float* db2,
+                                                  float* dsq) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx < C * R) {
+    const int c = idx / R, r = idx - c * R;
+    float a2 = 0.f, a1 = 0.f;
+    for (int n = 0; n < B; ++n) {
+      const float gv = gate[(size_t)n * C + c];
+      const float d2 = (float)dgate[(size_t)n * C + c] * gv * (1.f - gv);
       const float z = z1[(size_t)n * R + r];
-      const float sg = 1.f / (1.f + expf(-z));
-      const float d = a * sg * (1.f + z * (1.f - sg));
-      dz1[r] = d;
-      atomicAdd(db1 + r, d);
+      a2 += d2 * (z * sigmoidf_(z));
+      a1 += dz1[(size_t)n * R + r] * (float)s[(size_t)n * C + c];
     }
+    dw2[(size_t)c * R + r] += a2;
+    dw1[(size_t)r * C + c] += a1;
   }
-  __syncthreads();
-  for (int e = tid; e < R * C; e += 256) {
-    const int r = e / C, c = e - r * C;
-    atomicAdd(dw1 + e, dz1[r] * ss[c]);
-  }
-  const float inv_hw = 1.f / (float)HW;
-  for (int c = tid; c < C; c += 256) {
+  if (idx < B * C) {
+    const int n = idx / C, c = idx - n * C;
     float a = 0.f;
-    for (int r = 0; r < R; ++r) a += dz1[r] * w1[(size_t)r * C + c];
-    dsq[(size_t)n * C + c] = a * inv_hw;
+    for (int r = 0; r < R; ++r) a += dz1[(size_t)n * R + r] * w1[(size_t)r * C + c];
+    dsq[idx] = a / (float)HW;
+  }
+  if (idx < C) {
+    float a = 0.f;
+    for (int n = 0; n < B; ++n) {
+      const float gv = gate[(size_t)n * C + idx];
+      a += (float)dgate[(size_t)n * C + idx] * gv * (1.f - gv);
+    }
+    db2[idx] += a;
+  }
+  if (idx < R) {
+    float a = 0.f;
+    for (int n = 0; n < B; ++n) a += dz1[(size_t)n * R + idx];
+    db1[idx] += a;
   }
 }
 
@@ -509,19 +526,23 @@ int edet_se_fwd(int B, int C, int R, const double* s, const float* w1, const flo
                 const float* w2, const float* b2, float* z1, float* gate, edet_stream_t stream) {
   EDET_REQUIRE(s && w1 && b1 && w2 && b2 && z1 && gate && B > 0 && C > 0 && R > 0,
                "se_fwd: bad argument");
-  hipLaunchKernelGGL(k_se_fwd, dim3(B), dim3(256), (C + R) * sizeof(float), (hipStream_t)stream, C, R, s,
-                     w1, b1, w2, b2, z1, gate);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_se_reduce_c, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, s, w1, b1, z1);
+  hipLaunchKernelGGL(k_se_excite, dim3(cdiv(B * C, 256)), dim3(256), 0, st, B, C, R, z1, w2, b2, gate);
   return check_launch("edet se_fwd");
 }
 
 int edet_se_bwd(int B, int C, int R, int HW, const double* s, const float* z1,
                 const float* gate, const double* dgate, const float* w1, const float* w2,
-                float* dw1, float* db1, float* dw2, float* db2, float* dsq,
+                float* dw1, float* db1, float* dw2, float* db2, float* dsq, float* dz1,
                 edet_stream_t stream) {
-  EDET_REQUIRE(s && z1 && gate && dgate && w1 && w2 && dw1 && db1 && dw2 && db2 && dsq,
+  EDET_REQUIRE(s && z1 && gate && dgate && w1 && w2 && dw1 && db1 && dw2 && db2 && dsq && dz1,
                "se_bwd: null argument");
-  hipLaunchKernelGGL(k_se_bwd, dim3(B), dim3(256), (2 * C + 2 * R) * sizeof(float), (hipStream_t)stream,
-                     C, R, HW, s, z1, gate, dgate, w1, w2, dw1, db1, dw2, db2, dsq);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_se_dz1, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, z1, gate, dgate, w2, dz1);
+  const int n = std::max(C * R, B * C);
+  hipLaunchKernelGGL(k_se_wgrad, dim3(cdiv(n, 256)), dim3(256), 0, st, B, C, R, HW, s, z1, gate, dgate, dz1, w1,
+                     dw1, db1, dw2, db2, dsq);
   return check_launch("edet se_bwd");
 }
 

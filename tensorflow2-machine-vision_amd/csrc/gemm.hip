@@ -13,6 +13,8 @@
 // Tiling: 256 threads = 4 waves in a 2x2 arrangement, BM x BN output tile, K staged in
 // chunks of 32 through LDS (register-staged so the lazy transform can be applied), bf16
 // math on v_mfma_f32_16x16x32_bf16, fp32 math on v_mfma_f32_16x16x4_f32 (exact f32).
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace edet {
@@ -62,13 +64,21 @@ __device__ __forceinline__ bf16x8_t lds_frag_bf16(const uint16_t* p) {
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-template <typename T, int BM, int BN, bool BT, bool LAZY>
+// K-streaming GEMM for K > 512 (the MBConv project convs, K = 480 ... 1152, N <= 320): one
+// block owns a BM x BN tile with the whole N, and walks K in 32-wide chunks.  Software
+// pipelined: chunk k+1 is fetched global -> registers while chunk k's MFMAs run, LDS is
+// double-buffered, one barrier per chunk (the unpipelined loop exposed the full load latency
+// 36 times per tile: 150 GB/s at M = 8192).  B is the [N][K] weight (k contiguous).
+template <typename T, int BM, int BN, bool LAZY>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-  __shared__ __attribute__((aligned(16))) T As[BM * GLDK];
-  __shared__ __attribute__((aligned(16))) T Bs[BN * GLDK];
+  constexpr int AV = (BM * (GBK / 8) + 255) / 256, BV = (BN * (GBK / 8) + 255) / 256;
+  using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
+  constexpr int VW = sizeof(T) == 2 ? 1 : 2;  // 16-byte words per 8 elements
+  __shared__ __attribute__((aligned(16))) T As[2][BM * GLDK];
+  __shared__ __attribute__((aligned(16))) T Bs[2][BN * GLDK];
   __shared__ float red[2][2][BN];  // [sum|sq][wm][col]: one writer each, summed in fixed order
-  extern __shared__ float2 xf[];  // [K] lazy affine per input channel (LAZY only)
+  extern __shared__ float2 xf[];   // [K] lazy affine per input channel (LAZY only)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -88,76 +98,100 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   }
   __syncthreads();
 
+  const T* A = (const T*)g.a;
+  const T* B = (const T*)g.b;
+  V ra[AV][VW], rb[BV][VW];
+  // global -> registers (raw); invalid lanes hold zeros
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < AV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v >> 2, kv = (v & 3) * 8, grow = row0 + r, gk = k0 + kv;
+#pragma unroll
+      for (int w = 0; w < VW; ++w) ra[u][w] = V{};
+      if (v < BM * 4 && grow < g.M && gk < g.K) {
+        const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + gk);
+#pragma unroll
+        for (int w = 0; w < VW; ++w) ra[u][w] = src[w];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < BV; ++u) {
+      const int v = tid + u * 256;
+      const int n = v >> 2, kv = (v & 3) * 8, gn = col0 + n, gk = k0 + kv;
+#pragma unroll
+      for (int w = 0; w < VW; ++w) rb[u][w] = V{};
+      if (v < BN * 4 && gn < g.N && gk < g.K) {
+        const V* src = reinterpret_cast<const V*>(B + (size_t)gn * g.ldb + gk);
+#pragma unroll
+        for (int w = 0; w < VW; ++w) rb[u][w] = src[w];
+      }
+    }
+  };
+  // registers -> LDS buffer, lazy transform of A on the way
+  auto commit = [&](int buf, int k0) {
+#pragma unroll
+    for (int u = 0; u < AV; ++u) {
+      const int v = tid + u * 256;
+      if (v < BM * 4) {
+        const int r = v >> 2, kv = (v & 3) * 8;
+        T* dst = &As[buf][r * GLDK + kv];
+        if constexpr (LAZY) {
+          const int grow = row0 + r, gk = k0 + kv;
+          const T* e = reinterpret_cast<const T*>(&ra[u][0]);
+          float vals[8];
+          const float* gp = (g.lz.gate && grow < g.M) ? g.lz.gate + (size_t)((grow - seg_off) / hw) * g.K : nullptr;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float x = 0.f;
+            if (grow < g.M && gk + j < g.K) {
+              x = lazy_apply(to_f<T>(e[j]), xf[gk + j], g.lz.act);
+              if (gp) x *= gp[gk + j];
+            }
+            vals[j] = x;
+          }
+          st8(dst, vals);
+        } else {
+#pragma unroll
+          for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(dst)[w] = ra[u][w];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < BV; ++u) {
+      const int v = tid + u * 256;
+      if (v < BN * 4) {
+        const int n = v >> 2, kv = (v & 3) * 8;
+#pragma unroll
+        for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(&Bs[buf][n * GLDK + kv])[w] = rb[u][w];
+      }
+    }
+  };
+
   floatx4 acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  const T* A = (const T*)g.a;
-  const T* B = (const T*)g.b;
-
-  for (int k0 = 0; k0 < g.K; k0 += GBK) {
-    // ---- stage A (BM x 32): lazy transform applied here
-    for (int v = tid; v < BM * (GBK / 8); v += 256) {
-      const int r = v >> 2, kv = (v & 3) * 8;
-      const int grow = row0 + r, gk = k0 + kv, nk = g.K - gk;
-      T* dst = &As[r * GLDK + kv];
-      if (grow < g.M && nk > 0) {
-        if constexpr (LAZY) {
-          float vals[8];
-          ld8m(A + (size_t)grow * g.lda + gk, nk, vals);
-          const float* gp = g.lz.gate ? g.lz.gate + (size_t)((grow - seg_off) / hw) * g.K : nullptr;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            if (j < nk) {
-              float2 af = xf[gk + j];
-              float u = lazy_apply(vals[j], af, g.lz.act);
-              if (gp) u *= gp[gk + j];
-              vals[j] = u;
-            }
-          }
-          st8(dst, vals);
-        } else {
-          cp8(dst, A + (size_t)grow * g.lda + gk, nk);
-        }
-      } else {
-        zero8(dst);
-      }
-    }
-    // ---- stage B as Bs[n][k]
-    if constexpr (BT) {  // B is [N][ldb], k contiguous
-      for (int v = tid; v < BN * (GBK / 8); v += 256) {
-        const int n = v >> 2, kv = (v & 3) * 8;
-        const int gn = col0 + n, gk = k0 + kv, nk = g.K - gk;
-        T* dst = &Bs[n * GLDK + kv];
-        if (gn < g.N && nk > 0) cp8(dst, B + (size_t)gn * g.ldb + gk, nk);
-        else zero8(dst);
-      }
-    } else {  // B is [K][ldb], n contiguous: transpose into LDS
-      for (int v = tid; v < GBK * (BN / 8); v += 256) {
-        const int kk = v / (BN / 8), nv = (v - kk * (BN / 8)) * 8;
-        const int gk = k0 + kk, gn = col0 + nv, nn = g.N - gn;
-        float vals[8];
-        if (gk < g.K && nn > 0) ld8m(B + (size_t)gk * g.ldb + gn, nn, vals);
-        else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) vals[j] = 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) Bs[(nv + j) * GLDK + kk] = from_f<T>(vals[j]);
-      }
-    }
-    __syncthreads();
-
+  const int nk = cdiv(g.K, GBK);
+  fetch(0);
+  commit(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) fetch((kt + 1) * GBK);
+    const T* Ab = As[buf];
+    const T* Bb = Bs[buf];
     if constexpr (sizeof(T) == 2) {
       bf16x8_t af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
-        af[i] = lds_frag_bf16(&As[(wm * WM + i * 16 + (lane & 15)) * GLDK + 8 * (lane >> 4)]);
+        af[i] = lds_frag_bf16(&Ab[(wm * WM + i * 16 + (lane & 15)) * GLDK + 8 * (lane >> 4)]);
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        bfr[j] = lds_frag_bf16(&Bs[(wn * WN + j * 16 + (lane & 15)) * GLDK + 8 * (lane >> 4)]);
+        bfr[j] = lds_frag_bf16(&Bb[(wn * WN + j * 16 + (lane & 15)) * GLDK + 8 * (lane >> 4)]);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -168,9 +202,9 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
       for (int s = 0; s < GBK / 4; ++s) {
         float af[FM], bfr[FN];
 #pragma unroll
-        for (int i = 0; i < FM; ++i) af[i] = As[(wm * WM + i * 16 + (lane & 15)) * GLDK + 4 * s + (lane >> 4)];
+        for (int i = 0; i < FM; ++i) af[i] = Ab[(wm * WM + i * 16 + (lane & 15)) * GLDK + 4 * s + (lane >> 4)];
 #pragma unroll
-        for (int j = 0; j < FN; ++j) bfr[j] = Bs[(wn * WN + j * 16 + (lane & 15)) * GLDK + 4 * s + (lane >> 4)];
+        for (int j = 0; j < FN; ++j) bfr[j] = Bb[(wn * WN + j * 16 + (lane & 15)) * GLDK + 4 * s + (lane >> 4)];
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -178,6 +212,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     }
+    if (more) commit(buf ^ 1, (kt + 1) * GBK);
     __syncthreads();
   }
 
@@ -248,6 +283,7 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   // block partial depend on wave timing, and BN statistics must be reproducible)
   float* red = reinterpret_cast<float*>(Cs + BM * LDC);
   float2* xf = reinterpret_cast<float2*>(red + 4 * LDC);  // [K] (LAZY)
+  float* gt = reinterpret_cast<float*>(xf + (LAZY ? g.K : 0));  // [2][K] SE gate rows (LAZY)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -288,34 +324,66 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
     cur_seg = seg;
     __syncthreads();
   }
-  // ---- A tile (once per row tile)
+  // ---- SE gate rows of this tile's images in LDS (a tile spans <= 2 images when hw >= BM)
+  const bool gate_lds = LAZY && g.lz.gate != nullptr && hw >= BM;
+  const int n_lo = (row0 - seg_off) / hw;
+  if (gate_lds) {
+    for (int k = tid; k < 2 * K; k += 256) {
+      const int n = n_lo + (k >= K);
+      gt[k] = (n < g.pyr.batch) ? g.lz.gate[(size_t)n * K + (k >= K ? k - K : k)] : 0.f;
+    }
+    __syncthreads();
+  }
+  // ---- A tile (once per row tile); UNR vector loads in flight per thread before any use
   const T* A = (const T*)g.a;
   const int kv8 = KP / 8;
-  for (int v = tid; v < BM * kv8; v += 256) {
-    const int r = v / kv8, kv = (v - r * kv8) * 8;
-    const int grow = row0 + r, nk = K - kv;
-    T* dst = &As[r * LDA + kv];
-    if (grow < g.M && nk > 0) {
-      if constexpr (LAZY) {
-        float vals[8];
-        ld8m(A + (size_t)grow * g.lda + kv, nk, vals);
-        const float* gp = g.lz.gate ? g.lz.gate + (size_t)((grow - seg_off) / hw) * K : nullptr;
+  {
+    using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
+    constexpr int VW = sizeof(T) == 2 ? 1 : 2, UNR = 4;
+    for (int v0 = tid; v0 < BM * kv8; v0 += 256 * UNR) {
+      V raw[UNR][VW];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if (j < nk) {
-            float u = lazy_apply(vals[j], xf[kv + j], g.lz.act);
-            if (gp) u *= gp[kv + j];
-            vals[j] = u;
-          } else {
-            vals[j] = 0.f;
-          }
+      for (int u = 0; u < UNR; ++u) {
+        const int v = v0 + u * 256;
+        const int r = v / kv8, kv = (v - r * kv8) * 8;
+        const int grow = row0 + r;
+#pragma unroll
+        for (int w = 0; w < VW; ++w) raw[u][w] = V{};
+        if (v < BM * kv8 && grow < g.M && kv < K) {  // K % 8 == 0: whole vectors
+          const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + kv);
+#pragma unroll
+          for (int w = 0; w < VW; ++w) raw[u][w] = src[w];
         }
-        st8(dst, vals);
-      } else {
-        cp8(dst, A + (size_t)grow * g.lda + kv, nk);
       }
-    } else {
-      zero8(dst);
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int v = v0 + u * 256;
+        if (v >= BM * kv8) break;
+        const int r = v / kv8, kv = (v - r * kv8) * 8;
+        const int grow = row0 + r;
+        T* dst = &As[r * LDA + kv];
+        if constexpr (LAZY) {
+          const T* e = reinterpret_cast<const T*>(&raw[u][0]);
+          float vals[8];
+          const bool live = grow < g.M && kv < K;
+          const int img = (grow - seg_off) / hw;
+          const float* gp = nullptr;
+          if (live && g.lz.gate) gp = gate_lds ? gt + (img - n_lo) * K : g.lz.gate + (size_t)img * K;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float x = 0.f;
+            if (live) {
+              x = lazy_apply(to_f<T>(e[j]), xf[kv + j], g.lz.act);
+              if (gp) x *= gp[kv + j];
+            }
+            vals[j] = x;
+          }
+          st8(dst, vals);
+        } else {
+#pragma unroll
+          for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(dst)[w] = raw[u][w];
+        }
+      }
     }
   }
   const T* B = (const T*)g.b;
@@ -739,21 +807,21 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
 }
 
 // ------------------------------------------------------------------ launch helpers
-template <typename T, int BM, int BN, bool BT, bool LAZY>
+template <typename T, int BM, int BN, bool LAZY>
 static int launch_gemm(GemmArgs g, hipStream_t s) {
   g.ntm = cdiv(g.M, BM);
   g.ntn = cdiv(g.N, BN);
   const int nwg = g.ntm * g.ntn;
   if (nwg == 0) return EDET_OK;
   const size_t dyn = LAZY ? (size_t)g.K * sizeof(float2) : 0;
-  hipLaunchKernelGGL((k_gemm<T, BM, BN, BT, LAZY>), dim3(nwg), dim3(256), dyn, s, g);
+  hipLaunchKernelGGL((k_gemm<T, BM, BN, LAZY>), dim3(nwg), dim3(256), dyn, s, g);
   return check_launch("edet gemm");
 }
 
 template <typename T, int BM, bool LAZY>
 static size_t gemm_r_lds(int K, int KP, int LDC) {
   return (size_t)(BM + RNB) * (KP + 8) * sizeof(T) + (size_t)BM * LDC * sizeof(T) + 4 * (size_t)LDC * sizeof(float) +
-         (LAZY ? (size_t)K * sizeof(float2) : 0);
+         (LAZY ? (size_t)K * (sizeof(float2) + 2 * sizeof(float)) : 0);
 }
 
 template <typename T, int BM, bool LAZY>
@@ -783,11 +851,20 @@ static int launch_gemm_r(GemmArgs g, hipStream_t s) {
 template <typename T, bool LAZY>
 static int dispatch_gemm_kloop(GemmArgs g, hipStream_t s) {
   const int NP = cdiv(g.N, 32) * 32;
-  if (NP <= 64) return launch_gemm<T, 64, 64, true, LAZY>(g, s);
-  if (NP <= 96) return launch_gemm<T, 64, 96, true, LAZY>(g, s);
-  if (NP <= 128) return launch_gemm<T, 64, 128, true, LAZY>(g, s);
-  if (NP <= 192) return launch_gemm<T, 64, 192, true, LAZY>(g, s);
-  if (NP <= 320) return launch_gemm<T, 64, 320, true, LAZY>(g, s);
+  // BM = 32 when 64-row tiles would leave the chip under-filled
+  if (cdiv(g.M, 64) < 512) {
+    if (NP <= 64) return launch_gemm<T, 32, 64, LAZY>(g, s);
+    if (NP <= 96) return launch_gemm<T, 32, 96, LAZY>(g, s);
+    if (NP <= 128) return launch_gemm<T, 32, 128, LAZY>(g, s);
+    if (NP <= 192) return launch_gemm<T, 32, 192, LAZY>(g, s);
+    if (NP <= 320) return launch_gemm<T, 32, 320, LAZY>(g, s);
+  } else {
+    if (NP <= 64) return launch_gemm<T, 64, 64, LAZY>(g, s);
+    if (NP <= 96) return launch_gemm<T, 64, 96, LAZY>(g, s);
+    if (NP <= 128) return launch_gemm<T, 64, 128, LAZY>(g, s);
+    if (NP <= 192) return launch_gemm<T, 64, 192, LAZY>(g, s);
+    if (NP <= 320) return launch_gemm<T, 64, 320, LAZY>(g, s);
+  }
   set_error("gemm: K=%d > 512 needs N <= 320 (N=%d)", g.K, g.N);
   return EDET_EUNSUPPORTED;
 }

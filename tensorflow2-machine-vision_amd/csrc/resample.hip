@@ -101,10 +101,17 @@ __global__ __launch_bounds__(256) void k_stem_wgrad(const T* x, int B, int H, in
       }
       patch[px][k] = v;
     }
-    for (int e = tid; e < 64 * Cout; e += 256) {
-      const int px = e / Cout, co = e - px * Cout;
+    for (int e = tid; e < 64 * (Cout / 8); e += 256) {  // 16-byte vectors of dy
+      const int px = e / (Cout / 8), co = (e - px * (Cout / 8)) * 8;
       const long p = p0 + px;
-      dys[px][co] = (p < p_end) ? to_f<T>(dy[(size_t)p * Cout + co]) : 0.f;
+      float v[8];
+      if (p < p_end) ld8(dy + (size_t)p * Cout + co, v);
+      else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dys[px][co + j] = v[j];
     }
     __syncthreads();
 #pragma unroll
@@ -165,6 +172,16 @@ __device__ __forceinline__ void pool_window(const edet_lazy& lz, const float2* a
   }
 }
 
+// per-channel lazy-BN affine of each input, once per block into LDS (was recomputed per
+// element: four global loads plus the fp64 mean/var per channel per pixel)
+__device__ __forceinline__ void load_affine(const edet_lazy& lz, int C, float inv, float2* tab) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) tab[c] = bn_affine(lz.bn, 0, c, inv);
+}
+__device__ __forceinline__ void affine8_lds(const float2* tab, int c, float2* af) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) af[j] = tab[c + j];
+}
+
 __device__ __forceinline__ void affine8(const edet_lazy& lz, int c, int C, float inv, float2* af) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) af[j] = (c + j < C) ? bn_affine(lz.bn, 0, c + j, inv) : make_float2(1.f, 0.f);
@@ -172,6 +189,9 @@ __device__ __forceinline__ void affine8(const edet_lazy& lz, int c, int C, float
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_maxpool_fwd(edet_lazy lz, int B, int H, int W, int C, T* y) {
+  extern __shared__ float2 aft[];  // [C]
+  load_affine(lz, C, 1.f / (float)(B * H * W), aft);
+  __syncthreads();
   const int OH = cdiv(H, 2), OW = cdiv(W, 2), nv = C / 8;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (long)B * OH * OW * nv) return;
@@ -181,7 +201,7 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(edet_lazy lz, int B, int H,
   const int rem = (int)(pix - (long)n * OH * OW);
   const int oy = rem / OW, ox = rem - oy * OW;
   float2 af[8];
-  affine8(lz, cv * 8, C, 1.f / (float)(B * H * W), af);
+  affine8_lds(aft, cv * 8, af);
   float best[8];
   int arg[8];
   pool_window<T>(lz, af, (size_t)n * H * W, H, W, same_pad(H, 3, 2), same_pad(W, 3, 2), oy, ox, cv * 8, 8, best, arg);
@@ -214,6 +234,9 @@ __device__ __forceinline__ void pool_bwd_gather(const edet_lazy& lz, const float
 template <typename T>
 __global__ __launch_bounds__(256) void k_maxpool_bwd(edet_lazy lz, int B, int H, int W, int C, const T* dy, T* dx,
                                                      int accumulate) {
+  extern __shared__ float2 aft[];  // [C]
+  load_affine(lz, C, 1.f / (float)(B * H * W), aft);
+  __syncthreads();
   const int OH = cdiv(H, 2), OW = cdiv(W, 2), nv = C / 8;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (long)B * H * W * nv) return;
@@ -223,7 +246,7 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(edet_lazy lz, int B, int H,
   const int rem = (int)(pix - (long)n * H * W);
   const int iy = rem / W, ix = rem - iy * W;
   float2 af[8];
-  affine8(lz, cv * 8, C, 1.f / (float)(B * H * W), af);
+  affine8_lds(aft, cv * 8, af);
   float d[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) d[j] = 0.f;
@@ -268,6 +291,10 @@ __device__ __forceinline__ float fuse_denom(const float* w, int n_in) {
 
 template <typename T>
 __global__ __launch_bounds__(256) void k_fuse_fwd(FuseArgs g) {
+  extern __shared__ float2 aft[];  // [n_in][C]
+  for (int i = 0; i < g.n_in; ++i)
+    load_affine(g.in[i].v, g.C, 1.f / (float)(g.B * g.in[i].H * g.in[i].W), aft + i * g.C);
+  __syncthreads();
   const int nv = g.C / 8;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (long)g.B * g.H * g.W * nv) return;
@@ -281,7 +308,7 @@ __global__ __launch_bounds__(256) void k_fuse_fwd(FuseArgs g) {
   for (int i = 0; i < g.n_in; ++i) {
     const edet_fuse_input& fi = g.in[i];
     float2 af[8];
-    affine8(fi.v, cv * 8, g.C, 1.f / (float)(g.B * fi.H * fi.W), af);
+    affine8_lds(aft + i * g.C, cv * 8, af);
     float v[8];
     fuse_input_value<T>(fi, af, n, h, w, g.H, g.W, cv * 8, v);
     const float wi = g.w[i];
@@ -297,15 +324,21 @@ __global__ __launch_bounds__(256) void k_fuse_fwd(FuseArgs g) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_fuse_bwd(FuseArgs g) {
   __shared__ float red[3][4];
+  extern __shared__ float2 aft[];  // [n_in][C]
+  for (int i = 0; i < g.n_in; ++i)
+    load_affine(g.in[i].v, g.C, 1.f / (float)(g.B * g.in[i].H * g.in[i].W), aft + i * g.C);
+  __syncthreads();
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nv = g.C / 8;
   const float den = fuse_denom(g.w, g.n_in);
   int b = blockIdx.x;
   if (b < g.nb_w) {
-    // weight gradient: dw_i = sum dF * (v_i - F) / den
-    const long idx = (long)b * 256 + tid;
+    // weight gradient: dw_i = sum dF * (v_i - F) / den.  A bounded grid (<= 256 blocks)
+    // walks the pixels and keeps partials in registers: one block per 256 vectors put
+    // thousands of same-address atomics on the 3 weights.
     float part[3] = {0.f, 0.f, 0.f};
-    if (idx < (long)g.B * g.H * g.W * nv) {
+    const long total = (long)g.B * g.H * g.W * nv;
+    for (long idx = (long)b * 256 + tid; idx < total; idx += (long)g.nb_w * 256) {
       const int cv = (int)(idx % nv);
       const long pix = idx / nv;
       const int n = (int)(pix / ((long)g.H * g.W));
@@ -317,13 +350,13 @@ __global__ __launch_bounds__(256) void k_fuse_bwd(FuseArgs g) {
       for (int i = 0; i < g.n_in; ++i) {
         const edet_fuse_input& fi = g.in[i];
         float2 af[8];
-        affine8(fi.v, cv * 8, g.C, 1.f / (float)(g.B * fi.H * fi.W), af);
+        affine8_lds(aft + i * g.C, cv * 8, af);
         float v[8];
         fuse_input_value<T>(fi, af, n, h, w, g.H, g.W, cv * 8, v);
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += dF[j] * (v[j] - F[j]);
-        part[i] = s / den;
+        part[i] += s / den;
       }
     }
     for (int i = 0; i < g.n_in; ++i) {
@@ -376,7 +409,7 @@ __global__ __launch_bounds__(256) void k_fuse_bwd(FuseArgs g) {
     }
   } else {
     float2 af[8];
-    affine8(fi.v, cv * 8, g.C, 1.f / (float)(g.B * Hi * Wi), af);
+    affine8_lds(aft + i * g.C, cv * 8, af);
     pool_bwd_gather<T>(fi.v, af, dF, (size_t)n * Hi * Wi, o0, Hi, Wi, g.H, g.W, g.C, iy, ix, cv * 8, wn, d);
   }
   acc8m((T*)fi.dx + (size_t)pix * g.C + cv * 8, 8, d, fi.accumulate);
@@ -406,7 +439,7 @@ int edet_stem_wgrad(int dtype, const void* x, int B, int H, int W, const void* d
   EDET_REQUIRE(x && dy && dw, "stem_wgrad: null argument");
   EDET_REQUIRE(Cout % 8 == 0 && Cout <= 64, "stem_wgrad: Cout must be a multiple of 8, <= 64");
   const long px = (long)B * cdiv(H, 2) * cdiv(W, 2);
-  long per = (px + 2047) / 2048;
+  long per = (px + 2047) / 2048;  // latency-bound: 512 blocks measured 1.4x slower
   per = ((per + 63) / 64) * 64;
   if (per < 64) per = 64;
   const int nb = (int)((px + per - 1) / per);
@@ -424,7 +457,7 @@ int edet_maxpool_fwd(int dtype, const edet_lazy* x, int B, int H, int W, int C, 
   const long n = (long)B * cdiv(H, 2) * cdiv(W, 2) * (C / 8);
   const int nb = (int)((n + 255) / 256);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_maxpool_fwd<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, *x, B, H, W, C, (T*)y);
+    if (nb) hipLaunchKernelGGL(k_maxpool_fwd<T>, dim3(nb), dim3(256), C * sizeof(float2), (hipStream_t)stream, *x, B, H, W, C, (T*)y);
     return check_launch("edet maxpool_fwd");
   });
 }
@@ -436,7 +469,7 @@ int edet_maxpool_bwd(int dtype, const edet_lazy* x, int B, int H, int W, int C,
   const long n = (long)B * H * W * (C / 8);
   const int nb = (int)((n + 255) / 256);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_maxpool_bwd<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, *x, B, H, W, C,
+    if (nb) hipLaunchKernelGGL(k_maxpool_bwd<T>, dim3(nb), dim3(256), C * sizeof(float2), (hipStream_t)stream, *x, B, H, W, C,
                                (const T*)dy, (T*)dx, accumulate);
     return check_launch("edet maxpool_bwd");
   });
@@ -471,7 +504,7 @@ int edet_bifpn_fuse_fwd(int dtype, int n_in, const edet_fuse_input* ins, const f
   const long n = (long)B * H * W * (C / 8);
   const int nb = (int)((n + 255) / 256);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_fuse_fwd<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, g);
+    if (nb) hipLaunchKernelGGL(k_fuse_fwd<T>, dim3(nb), dim3(256), n_in * C * sizeof(float2), (hipStream_t)stream, g);
     return check_launch("edet bifpn_fuse_fwd");
   });
 }
@@ -485,14 +518,14 @@ int edet_bifpn_fuse_bwd(int dtype, int n_in, const edet_fuse_input* ins, const f
   EDET_REQUIRE(out && dout && dw, "bifpn_fuse_bwd: null argument");
   for (int i = 0; i < n_in; ++i) EDET_REQUIRE(ins[i].dx, "bifpn_fuse_bwd: input %d has no dx", i);
   g.fused = out; g.dout = dout; g.dw = dw;
-  g.nb_w = (int)(((long)B * H * W * (C / 8) + 255) / 256);
+  g.nb_w = (int)std::min<long>(256, ((long)B * H * W * (C / 8) + 255) / 256);
   int nb = g.nb_w;
   for (int i = 0; i < n_in; ++i) {
     g.nb_in[i] = (int)(((long)B * ins[i].H * ins[i].W * (C / 8) + 255) / 256);
     nb += g.nb_in[i];
   }
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_fuse_bwd<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, g);
+    if (nb) hipLaunchKernelGGL(k_fuse_bwd<T>, dim3(nb), dim3(256), n_in * C * sizeof(float2), (hipStream_t)stream, g);
     return check_launch("edet bifpn_fuse_bwd");
   });
 }

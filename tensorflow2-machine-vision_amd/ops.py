@@ -49,8 +49,9 @@ def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor
         dgate = torch.zeros((B, out.C), dtype=torch.float64, device=eng.device)
         L.call("edet_gate_grad", eng.dt, lz, B, HW, out.C, vp(rec.t), vp(dgate), s)
         dsq = torch.empty((B, out.C), dtype=torch.float32, device=eng.device)
+        dz1 = torch.empty((B, se.R), dtype=torch.float32, device=eng.device)
         L.call("edet_se_bwd", B, out.C, se.R, HW, vp(se.s), vp(se.z1), vp(se.gate), vp(dgate),
-               vp(se.w1), vp(se.w2), vp(se.dw1), vp(se.db1), vp(se.dw2), vp(se.db2), vp(dsq), s)
+               vp(se.w1), vp(se.w2), vp(se.dw1), vp(se.db1), vp(se.dw2), vp(se.db2), vp(dsq), vp(dz1), s)
     grads = acc = None
     if out.bns is not None:
         grads = _bn_grads(out.bns)

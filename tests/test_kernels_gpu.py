@@ -243,7 +243,7 @@ def test_squeeze_excite(dt):
     dws = [zeros(R, C), zeros(R), zeros(C, R), zeros(C)]
     dsq = zeros(B, C)
     L.call("edet_se_bwd", B, C, R, H * W, vp(s), vp(z1), vp(gate), vp(dgate), vp(w1), vp(w2), vp(dws[0]), vp(dws[1]),
-           vp(dws[2]), vp(dws[3]), vp(dsq), stream())
+           vp(dws[2]), vp(dws[3]), vp(dsq), vp(zeros(B, R)), stream())
     (gr * dgate.double().cpu()).sum().backward()
     for a, b in zip(dws, (W1.grad, B1.grad, W2.grad, B2.grad)):
         close(a, b, "f32", rtol=1e-4, atol=1e-4)
