@@ -182,6 +182,103 @@ class KernelTimer:
         return agg
 
 
+# C-ABI entry points that launch exactly one device kernel: their probe-measured launch
+# durations are directly comparable with the rocprofv3 summary of that kernel
+ONE_TO_ONE = {"edet_lazy_bwd_apply": "k_lazy_bwd_apply", "edet_lazy_bwd_reduce": "k_lazy_bwd_reduce",
+              "edet_detection_loss": "k_loss", "edet_stem_fwd": "k_stem_fwd", "edet_stem_wgrad": "k_stem_wgrad"}
+
+
+class ProbeTimer:
+    """Wraps every launch of one C-ABI function with edet_probe begin/end on its stream.  The
+    probes are ordinary kernels, so they can be captured into the step's HIP graph (timing
+    events cannot): replaying K captured steps accumulates each launch's duration on the GPU's
+    constant-rate wall clock."""
+
+    def __init__(self, func, es, max_calls=1024):
+        from tf2mv_amd import _lib as L
+        self.L, self.func, self.es = L, func, es
+        self.slots = torch.zeros(max_calls * 3, dtype=torch.int64, device="cuda")
+        self.max_calls = max_calls
+        self.bytes = []
+        self.orig = L.call
+
+    def __enter__(self):
+        import ctypes
+        L = self.L
+
+        def probed(name, *args):
+            if name != self.func:
+                return self.orig(name, *args)
+            i = len(self.bytes)
+            assert i < self.max_calls
+            slot = ctypes.c_void_p(self.slots.data_ptr() + 24 * i)
+            st = args[-1]  # every entry point takes its stream last
+            self.orig("edet_probe", slot, 0, st)
+            r = self.orig(name, *args)
+            self.orig("edet_probe", slot, 1, st)
+            self.bytes.append(algorithmic_bytes(name, args, self.es))
+            return r
+
+        L.call = probed
+        import tf2mv_amd.ops, tf2mv_amd.model, tf2mv_amd.runtime, tf2mv_amd.anchors  # noqa
+        for mod in (tf2mv_amd.ops, tf2mv_amd.model, tf2mv_amd.runtime, tf2mv_amd.anchors):
+            mod.L.call = probed
+        return self
+
+    def __exit__(self, *exc):
+        self.L.call = self.orig
+
+    def result(self):
+        import ctypes
+        torch.cuda.synchronize()
+        khz = ctypes.c_int(0)
+        self.orig("edet_wall_clock_khz", ctypes.byref(khz))
+        n = len(self.bytes)
+        sl = self.slots.view(-1, 3)[:n].cpu()
+        launches = int(sl[:, 2].sum())
+        ticks = int(sl[:, 1].sum())
+        avg_us = ticks / max(launches, 1) / (khz.value / 1000.0)
+        bpl = sum(self.bytes) / max(n, 1)
+        return {"launches": launches, "avg_launch_us": avg_us, "bytes_per_launch": bpl,
+                "achieved_GBps": bpl / avg_us * 1e-3 if avg_us > 0 else None, "clock_khz": khz.value}
+
+
+def probe_roofline(model, data, func, steps, es):
+    """Average launch duration of ``func`` over ``steps`` replays of a captured step graph that
+    carries the probes, and the algorithmic bytes per launch."""
+    pt = ProbeTimer(func, es)
+    with pt:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            model.train_step(data)
+    g.replay()  # warm
+    torch.cuda.synchronize()
+    pt.slots.zero_()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    torch.cuda.synchronize()
+    r = pt.result()
+    r["ms_per_step"] = (time.perf_counter() - t0) / steps * 1e3
+    del g
+    return r
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC summary (two passes,
+    FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction; scripts/pmc_traffic.py), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        k = d.get("kernels", {}).get(kernel)
+        return None if k is None else float(k["traffic_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def cpu_baseline(model, seconds=12.0):
     """Oracle fp32 train step (forward + loss + backward) on the host cores, 1 image/iteration."""
     from oracle.ref_model import RefEfficientDet
@@ -313,13 +410,23 @@ def main():
         for k, a in top[:12]:
             log(f"   {k:28s} calls={a[0]:4d} ms={a[1]:8.3f} share={a[1] / total_ms * 100:5.1f}%"
                 + (f" {a[2] / (a[1] * 1e6):8.1f} GB/s" if a[3] else ""))
-        dom = next((kv for kv in top if kv[1][3]), None)
-        if dom is not None:
-            name, (calls, ms, byts, _) = dom
-            ach = byts / (ms * 1e6)
-            roofline = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                        "bytes_per_launch": round(byts / calls), "avg_launch_us": round(ms / calls * 1e3, 2)}
+        # dominant single-kernel entry point (1:1 with a device kernel, so the probe average
+        # is comparable with the rocprofv3 summary of the same command)
+        dom = next((kv for kv in top if kv[0] in ONE_TO_ONE and kv[1][3]), None)
+        if dom is not None and args.graph:
+            name = dom[0]
+            pr = probe_roofline(model, data, name, args.steps, es)
+            kname = ONE_TO_ONE[name]
+            ach = pr["achieved_GBps"]
+            traffic = pmc_traffic(kname)
+            roofline = {"bound": "hbm", "kernel": kname, "entry_point": name, "achieved": round(ach, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                        "traffic": None if traffic is None else round(traffic),
+                        "bytes_per_launch": round(pr["bytes_per_launch"]), "avg_launch_us": round(pr["avg_launch_us"], 2),
+                        "launches": pr["launches"], "timing": "wall-clock probes in the captured step graph, "
+                        f"{args.steps} replays ({pr['ms_per_step']:.2f} ms/step with probes)"}
+            log(f"[bench] roofline {kname}: {pr['launches']} launches, avg {pr['avg_launch_us']:.2f} us, "
+                f"{pr['bytes_per_launch'] / 1e6:.2f} MB/launch -> {ach:.1f} GB/s")
 
     cpu = None
     if args.cpu_baseline and rank == 0 and world == 1:

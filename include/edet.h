@@ -124,6 +124,10 @@ const char* edet_last_error(void);
 int edet_abi_version(void);
 int edet_memset_async(void* p, int value, size_t bytes, edet_stream_t stream);
 int edet_memcpy_async(void* dst, const void* src, size_t bytes, edet_stream_t stream);
+/* launch-duration probe (measurement): end = 0 stores the wall clock in slot[0]; end = 1 adds
+ * (now - slot[0]) to slot[1] and 1 to slot[2].  Capturable in HIP graphs. */
+int edet_probe(uint64_t* slot, int end, edet_stream_t stream);
+int edet_wall_clock_khz(int* khz);
 
 /* ---- pointwise (1x1) convolution: y[m][n] = sum_k v(a)[m][k] * wt[n][k] + bias[n] ----
  * wt is [N][K] in `dtype`.  `stats` (nullable) receives per-segment column sums of y. */

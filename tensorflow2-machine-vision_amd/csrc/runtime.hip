@@ -23,6 +23,19 @@ int check_launch(const char* what) {
   return EDET_OK;
 }
 
+// Launch-duration probe: a single-thread kernel reading the constant-rate wall clock.  Placed
+// before and after a launch on the same stream (also inside captured HIP graphs, where timing
+// events are unavailable), it accumulates the launch's duration: slot = {t0, sum(t1-t0), n}.
+__global__ void k_probe(unsigned long long* slot, int end) {
+  const unsigned long long t = wall_clock64();
+  if (!end) {
+    slot[0] = t;
+  } else {
+    slot[1] += t - slot[0];
+    slot[2] += 1;
+  }
+}
+
 }  // namespace edet
 
 extern "C" {
@@ -30,6 +43,24 @@ extern "C" {
 const char* edet_last_error(void) { return edet::g_err; }
 
 int edet_abi_version(void) { return 2; }
+
+int edet_probe(uint64_t* slot, int end, edet_stream_t stream) {
+  EDET_REQUIRE(slot, "probe: null slot");
+  hipLaunchKernelGGL(edet::k_probe, dim3(1), dim3(1), 0, (hipStream_t)stream, (unsigned long long*)slot, end);
+  return edet::check_launch("edet probe");
+}
+
+int edet_wall_clock_khz(int* khz) {
+  EDET_REQUIRE(khz, "wall_clock_khz: null");
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(khz, hipDeviceAttributeWallClockRate, dev);
+  if (e != hipSuccess) {
+    edet::set_error("wall clock rate: %s", hipGetErrorString(e));
+    return EDET_EHIP;
+  }
+  return EDET_OK;
+}
 
 int edet_memset_async(void* p, int value, size_t bytes, edet_stream_t stream) {
   if (bytes == 0) return EDET_OK;
