@@ -124,6 +124,11 @@ const char* edet_last_error(void);
 int edet_abi_version(void);
 int edet_memset_async(void* p, int value, size_t bytes, edet_stream_t stream);
 int edet_memcpy_async(void* dst, const void* src, size_t bytes, edet_stream_t stream);
+/* Register device scratch used by split reductions (weight gradients write per-split partials
+ * and sum them in a fixed order instead of issuing atomics).  The buffer must stay valid while
+ * kernels that may use it are queued; NULL unregisters (atomics fallback).  Not thread-safe:
+ * one registered workspace per process. */
+int edet_set_workspace(void* ptr, size_t bytes);
 /* launch-duration probe (measurement): end = 0 stores the wall clock in slot[0]; end = 1 adds
  * (now - slot[0]) to slot[1] and 1 to slot[2].  Capturable in HIP graphs. */
 int edet_probe(uint64_t* slot, int end, edet_stream_t stream);

@@ -76,6 +76,7 @@ SIGNATURES = {
     "edet_abi_version": [],
     "edet_memset_async": [P, c_int, c_size_t, P],
     "edet_memcpy_async": [P, P, c_size_t, P],
+    "edet_set_workspace": [P, c_size_t],
     "edet_probe": [P, c_int, P],
     "edet_wall_clock_khz": [P],
     "edet_conv1x1_fwd": [c_int, PLazy, PPyr, c_int, P, c_int, P, P, c_int, c_int, PStat, P],

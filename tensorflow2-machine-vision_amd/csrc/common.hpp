@@ -14,6 +14,10 @@ namespace edet {
 // ------------------------------------------------------------------ error reporting
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// registered scratch (edet_set_workspace) if it holds n floats, else nullptr
+float* workspace_f32(size_t n_floats);
+// out[i] += sum_s part[s*n + i], fixed order
+int sum_partials(const float* part, int S, long n, float* out, hipStream_t st);
 
 #define EDET_REQUIRE(cond, ...)            \
   do {                                     \

@@ -29,6 +29,7 @@ struct DwArgs {
   edet_statout stats;
   int C, ncb, accumulate, has_stats;
   int tiles_per_wg, tiles_total;
+  float* part;  // wgrad: per-chunk partials [chunks][K*K][C] (null: atomics)
 };
 
 // tiles over a pyramid's spatial extent (per channel block)
@@ -338,7 +339,8 @@ __global__ __launch_bounds__(256) void k_dw_wgrad(DwArgs g) {
       float s = 0.f;
 #pragma unroll
       for (int rr = 0; rr < 8; ++rr) s += lds[(i * 8 + rr) * DCB + cc];
-      atomicAdd(g.dw + (size_t)i * g.C + c0 + cc, s);
+      if (g.part) g.part[((size_t)chunk * K * K + i) * g.C + c0 + cc] = s;
+      else atomicAdd(g.dw + (size_t)i * g.C + c0 + cc, s);
     }
   }
 }
@@ -507,7 +509,11 @@ static int launch_dw(int which, DwArgs g, hipStream_t s) {
     if (chunks < 1) chunks = 1;
     g.tiles_per_wg = cdiv(g.tiles_total, chunks);
     chunks = cdiv(g.tiles_total, g.tiles_per_wg);
+    g.part = nullptr;  // K*K*C is small: atomics measured faster than a 2048-way partial sum
     if (g.tiles_total) hipLaunchKernelGGL((k_dw_wgrad<T, K, S>), dim3(chunks * g.ncb), dim3(256), 0, s, g);
+    int rc = check_launch("edet dwconv");
+    if (rc || !g.part || !g.tiles_total) return rc;
+    return sum_partials(g.part, chunks, (long)K * K * g.C, g.dw, s);
   }
   return check_launch("edet dwconv");
 }

@@ -509,6 +509,7 @@ struct WgradArgs {
   const void* dy;
   float* dw;
   float* db;
+  float* part;  // non-null: per-split partials [split][N][K] then [split][N] (no atomics)
   edet_lazy lz;
   edet_pyramid pyr;
   int lda, lddy, M, K, N;
@@ -723,6 +724,9 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
       }
     }
   };
+  // SE gate of this thread's 8 columns, cached per image (the image changes every hw rows)
+  int gimg[2] = {-1, -1};
+  float gcache[2][8];
   auto commit = [&](int buf, int m0) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -733,14 +737,24 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
         if (rseg[h] >= 0) {
           const int row = m0 + r, sg = rseg[h];
           const uint16_t* t = reinterpret_cast<const uint16_t*>(&x);
-          const float* gp = g.lz.gate ? g.lz.gate + (size_t)((row - g.pyr.row_off[sg]) / (g.pyr.H[sg] * g.pyr.W[sg])) * g.K + kk0 + lc : nullptr;
+          if (g.lz.gate) {
+            const int img = (row - g.pyr.row_off[sg]) / (g.pyr.H[sg] * g.pyr.W[sg]);
+            if (img != gimg[h]) {
+              gimg[h] = img;
+              const int nk = g.K - (kk0 + lc);
+              if (nk >= 8) ld8(g.lz.gate + (size_t)img * g.K + kk0 + lc, gcache[h]);
+              else
+#pragma unroll
+                for (int j = 0; j < 8; ++j) gcache[h][j] = j < nk ? g.lz.gate[(size_t)img * g.K + kk0 + lc + j] : 0.f;
+            }
+          }
           uint16_t o[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             float u = 0.f;
             if (kk0 + lc + j < g.K) {
               u = lazy_apply(to_f<uint16_t>(t[j]), xf[sg][lc + j], g.lz.act);
-              if (gp) u *= gp[j];
+              if (g.lz.gate) u *= gcache[h][j];
             }
             o[j] = from_f<uint16_t>(u);
           }
@@ -797,12 +811,19 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + wn * 32 + i * 16 + (lane >> 4) * 4 + r;
         const int k = kk0 + wk * 32 + j * 16 + (lane & 15);
-        if (n < g.N && k < g.K) atomicAdd(g.dw + (size_t)n * g.K + k, acc[i][j][r]);
+        if (n < g.N && k < g.K) {
+          if (g.part) g.part[((size_t)split * g.N + n) * g.K + k] = acc[i][j][r];
+          else atomicAdd(g.dw + (size_t)n * g.K + k, acc[i][j][r]);
+        }
       }
   if (do_db) {
     dbred[wave][lane] = dbacc;
     __syncthreads();
-    if (tid < 64 && n0 + tid < g.N) atomicAdd(g.db + n0 + tid, dbred[0][tid] + dbred[1][tid] + dbred[2][tid] + dbred[3][tid]);
+    if (tid < 64 && n0 + tid < g.N) {
+      const float v = dbred[0][tid] + dbred[1][tid] + dbred[2][tid] + dbred[3][tid];
+      if (g.part) g.part[(size_t)gridDim.x / (g.ntn * g.ntk) * g.N * g.K + (size_t)split * g.N + n0 + tid] = v;
+      else atomicAdd(g.db + n0 + tid, v);
+    }
   }
 }
 
@@ -952,11 +973,22 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
     int split = cdiv(1024, tiles);
     const int max_split = std::max(1, cdiv(g.M, WT_BM * 4));
     if (split > max_split) split = max_split;
+    // large weights (N*K >= 16K, the MBConv expand/project and head convs at small M): at
+    // most 32 splits write plain partials that one fixed-order pass sums (split x N x K
+    // atomics were millions per launch); small weights keep the atomics and full split
+    const bool use_part = (long)N * K >= 16384 && workspace_f32(0) != nullptr;
+    if (use_part && split > 32) split = 32;
     g.rows_per = cdiv(cdiv(g.M, split), WT_BM) * WT_BM;
     split = std::max(1, cdiv(g.M, g.rows_per));
+    const size_t nw = (size_t)split * N * K, nb = dbias ? (size_t)split * N : 0;
+    g.part = (use_part && split > 1) ? workspace_f32(nw + nb) : nullptr;
     if (plain) hipLaunchKernelGGL((k_wgrad_tr<false>), dim3(tiles * split), dim3(256), 0, s, g);
     else hipLaunchKernelGGL((k_wgrad_tr<true>), dim3(tiles * split), dim3(256), 0, s, g);
-    return check_launch("edet wgrad");
+    int rc = check_launch("edet wgrad");
+    if (rc || !g.part) return rc;
+    rc = sum_partials(g.part, split, (long)N * K, dwt, s);
+    if (!rc && dbias) rc = sum_partials(g.part + nw, split, N, dbias, s);
+    return rc;
   }
   int split = cdiv(2048, tiles);
   const int max_split = cdiv(g.M, 32 * 4);  // at least 4 row-chunks per block

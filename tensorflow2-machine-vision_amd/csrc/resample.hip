@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const T* x, int B, int H, int 
 // dw[kh][kw][ci][co] += sum_pixels x_patch * dy
 template <typename T>
 __global__ __launch_bounds__(256) void k_stem_wgrad(const T* x, int B, int H, int W, const T* dy, int Cout,
-                                                    float* dw, long px_per_wg) {
+                                                    float* dw, long px_per_wg, float* part) {
   __shared__ float patch[64][28];
   __shared__ float dys[64][65];
   const int tid = threadIdx.x;
@@ -129,7 +129,10 @@ __global__ __launch_bounds__(256) void k_stem_wgrad(const T* x, int B, int H, in
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     const int j = tid + i * 256;
-    if (j < NOUT) atomicAdd(dw + j, acc[i]);
+    if (j < NOUT) {
+      if (part) part[(size_t)blockIdx.x * NOUT + j] = acc[i];
+      else atomicAdd(dw + j, acc[i]);
+    }
   }
 }
 
@@ -443,10 +446,13 @@ int edet_stem_wgrad(int dtype, const void* x, int B, int H, int W, const void* d
   per = ((per + 63) / 64) * 64;
   if (per < 64) per = 64;
   const int nb = (int)((px + per - 1) / per);
+  float* part = nullptr;  // 27*Cout weights over 2048 blocks: atomics measured faster
   EDET_DTYPE_DISPATCH(dtype, T, {
     if (nb) hipLaunchKernelGGL(k_stem_wgrad<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const T*)x, B, H, W,
-                               (const T*)dy, Cout, dw, per);
-    return check_launch("edet stem_wgrad");
+                               (const T*)dy, Cout, dw, per, part);
+    int rc = check_launch("edet stem_wgrad");
+    if (rc || !part || !nb) return rc;
+    return sum_partials(part, nb, 27L * Cout, dw, (hipStream_t)stream);
   });
 }
 

@@ -23,6 +23,34 @@ int check_launch(const char* what) {
   return EDET_OK;
 }
 
+// Caller-registered scratch for split reductions (weight gradients): blocks write partial
+// results with plain stores, one reduce kernel sums them in a fixed order.  The library still
+// allocates nothing; without a (large enough) workspace the kernels fall back to atomics.
+static void* g_ws = nullptr;
+static size_t g_ws_bytes = 0;
+float* workspace_f32(size_t n_floats) {
+  return (g_ws && n_floats * sizeof(float) <= g_ws_bytes) ? (float*)g_ws : nullptr;
+}
+
+// out[i] += sum_{s < S} part[s * n + i]   (fixed order)
+__global__ __launch_bounds__(256) void k_sum_partials(const float* part, int S, long n, float* out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
+  int s = 0;
+  for (; s + 8 <= S; s += 8)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += part[(size_t)(s + u) * n + i];
+  for (; s < S; ++s) a[0] += part[(size_t)s * n + i];
+  out[i] += ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
+int sum_partials(const float* part, int S, long n, float* out, hipStream_t st) {
+  if (n <= 0) return EDET_OK;
+  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, S, n, out);
+  return check_launch("edet sum_partials");
+}
+
 // Launch-duration probe: a single-thread kernel reading the constant-rate wall clock.  Placed
 // before and after a launch on the same stream (also inside captured HIP graphs, where timing
 // events are unavailable), it accumulates the launch's duration: slot = {t0, sum(t1-t0), n}.
@@ -43,6 +71,12 @@ extern "C" {
 const char* edet_last_error(void) { return edet::g_err; }
 
 int edet_abi_version(void) { return 2; }
+
+int edet_set_workspace(void* ptr, size_t bytes) {
+  edet::g_ws = ptr;
+  edet::g_ws_bytes = ptr ? bytes : 0;
+  return EDET_OK;
+}
 
 int edet_probe(uint64_t* slot, int end, edet_stream_t stream) {
   EDET_REQUIRE(slot, "probe: null slot");

@@ -282,6 +282,7 @@ class ParamStore:
             o += bn.C
         self.finalized = True
         if torch.device(device).type == "cuda":
+            ensure_workspace(device)
             self.refresh_compute_copy()
         # else: host-only store (model structure + initial parameters for CPU tools/tests);
         # the model refuses to run its compute path on it.
@@ -427,6 +428,26 @@ class Tape:
 
 
 # --------------------------------------------------------------------------- engine
+_WORKSPACE = {}
+WORKSPACE_BYTES = 64 << 20
+
+
+def ensure_workspace(device) -> torch.Tensor:
+    """Register the library's split-reduction scratch (edet_set_workspace) for this process.
+    Allocated once per device and never freed, so the registered pointer cannot dangle; the
+    weight-gradient kernels use it instead of atomics (deterministic sums)."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    ws = _WORKSPACE.get(idx)
+    if ws is None:
+        ws = torch.empty(WORKSPACE_BYTES, dtype=torch.uint8, device=dev)
+        _WORKSPACE[idx] = ws
+    L.call("edet_set_workspace", _vp(ws), WORKSPACE_BYTES)
+    return ws
+
+
 def stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 

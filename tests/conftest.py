@@ -20,3 +20,17 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(params=["partials", "atomics"])
+def workspace_mode(request):
+    """Weight-gradient kernels with the registered split-reduction workspace (fixed-order
+    partial sums) and without it (atomics fallback)."""
+    from tf2mv_amd import _lib as L
+    from tf2mv_amd.runtime import ensure_workspace
+    if request.param == "atomics":
+        L.call("edet_set_workspace", None, 0)
+    else:
+        ensure_workspace("cuda")
+    yield request.param
+    ensure_workspace("cuda")

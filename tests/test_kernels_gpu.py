@@ -128,7 +128,7 @@ def dw_ref(v, pyr_in, k, s, w):  # v: fp64 [rows, C] values; returns [rows_out, 
 @pytest.mark.parametrize("k,s,H,W,C,lazy,nseg", [(3, 1, 16, 16, 32, 0, 1), (3, 2, 17, 13, 96, 1, 1),
                                                  (5, 2, 20, 9, 144, 1, 1), (5, 1, 11, 12, 40, 2, 1),
                                                  (3, 1, 9, 9, 64, 3, 2)])
-def test_dwconv_fwd_bwd(dt, k, s, H, W, C, lazy, nseg):
+def test_dwconv_fwd_bwd(dt, k, s, H, W, C, lazy, nseg, workspace_mode):
     rng = np.random.default_rng(k * 100 + s * 10 + H)
     B = 2
     pin = Pyr(B, [(H, W), ((H + 1) // 2, (W + 1) // 2)]) if nseg == 2 else Pyr(B, [(H, W)])
@@ -350,7 +350,7 @@ def test_residual(dt):
 
 
 @pytest.mark.parametrize("dt", DTS)
-def test_stem(dt):
+def test_stem(dt, workspace_mode):
     rng = np.random.default_rng(9)
     B, H, W, Co = 2, 21, 18, 32
     x = g(torch.rand(B, H, W, 3), dt)

@@ -65,8 +65,8 @@ def test_conv1x1_fwd_large(dt, kind, K, N, lazy):
 
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("kind,K,N,lazy", [((8, (128, 128)), 16, 96, 2), ((8, (64, 64)), 144, 24, 1),
-                                           ("p5", 64, 64, 3), ("p5", 64, 36, 0)])
-def test_conv1x1_wgrad_large(dt, kind, K, N, lazy):
+                                           ("p5", 64, 64, 3), ("p5", 64, 36, 0), ((4, (64, 64)), 672, 112, 1)])
+def test_conv1x1_wgrad_large(dt, kind, K, N, lazy, workspace_mode):
     rng = np.random.default_rng(K * 7 + N)
     pyr = make_pyr(kind)
     x = g(rnd(rng, pyr.rows, K), dt)
