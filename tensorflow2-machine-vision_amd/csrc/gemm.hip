@@ -974,10 +974,10 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
     const int max_split = std::max(1, cdiv(g.M, WT_BM * 4));
     if (split > max_split) split = max_split;
     // large weights (N*K >= 16K, the MBConv expand/project and head convs at small M): at
-    // most 32 splits write plain partials that one fixed-order pass sums (split x N x K
+    // most 128 splits write plain partials that one fixed-order pass sums (split x N x K
     // atomics were millions per launch); small weights keep the atomics and full split
     const bool use_part = (long)N * K >= 16384 && workspace_f32(0) != nullptr;
-    if (use_part && split > 32) split = 32;
+    if (use_part && split > 128) split = 128;
     g.rows_per = cdiv(cdiv(g.M, split), WT_BM) * WT_BM;
     split = std::max(1, cdiv(g.M, g.rows_per));
     const size_t nw = (size_t)split * N * K, nb = dbias ? (size_t)split * N : 0;
