@@ -155,17 +155,18 @@ class KernelTimer:
     def __exit__(self, *exc):
         self.L.call = self.orig
 
-    def detail(self, path, top=60):
+    def detail(self, path, top=2000):
         """Per-call table (slowest first): name, shape, us, achieved GB/s."""
         torch.cuda.synchronize()
         rows = []
         for name, s, e, b, tag in self.rec:
             ms = s.elapsed_time(e)
-            rows.append((ms, name, tag, (b / (ms * 1e6)) if (b and ms > 0) else None))
+            rows.append((ms, name, tag, (b / (ms * 1e6)) if (b and ms > 0) else None, b or 0))
         rows.sort(reverse=True)
         with open(path, "w") as f:
-            for ms, name, tag, gbs in rows[:top]:
-                f.write(f"{ms * 1e3:9.1f} us  {name:24s} {tag:40s} {'' if gbs is None else f'{gbs:8.1f} GB/s'}\n")
+            for ms, name, tag, gbs, b in rows[:top]:
+                g = "" if gbs is None else f"{gbs:8.1f} GB/s"
+                f.write(f"{ms * 1e3:9.1f} us  {name:24s} {tag:40s} {g:14s} {b:12d} B\n")
 
     def summary(self):
         torch.cuda.synchronize()

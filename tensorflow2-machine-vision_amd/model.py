@@ -339,6 +339,7 @@ class EfficientDetNet:
         B = x.shape[0]
         assert (x.shape[1], x.shape[2]) == self.level_hw_input, "input size must match the config image_size"
         self._set_counts(B)
+        eng.begin_scratch()
         eng.training = training
         if not training:
             L.call("edet_bn_inference_stats", P.n_bn, vp(P.bn_mm), vp(P.bn_mv), vp(P.bn_count),

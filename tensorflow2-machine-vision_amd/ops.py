@@ -46,7 +46,7 @@ def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor
         se = out.se
         B = out.pyr.batch
         HW = out.pyr.H * out.pyr.W
-        dgate = torch.zeros((B, out.C), dtype=torch.float64, device=eng.device)
+        dgate = eng.zeros64(B, out.C)
         L.call("edet_gate_grad", eng.dt, lz, B, HW, out.C, vp(rec.t), vp(dgate), s)
         dsq = torch.empty((B, out.C), dtype=torch.float32, device=eng.device)
         dz1 = torch.empty((B, se.R), dtype=torch.float32, device=eng.device)
@@ -56,7 +56,7 @@ def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor
     if out.bns is not None:
         grads = _bn_grads(out.bns)
         # fp64 dgamma/dbeta sums (edet_bngrad64): their order must not reach the rounding of dx
-        acc_t = torch.zeros((2, len(out.bns), out.C), dtype=torch.float64, device=eng.device)
+        acc_t = eng.zeros64(2, len(out.bns), out.C)
         acc = L.BnGrad64()
         for i in range(len(out.bns)):
             acc.dgamma[i], acc.dbeta[i] = acc_t[0, i].data_ptr(), acc_t[1, i].data_ptr()
@@ -77,7 +77,7 @@ def stem(eng: Engine, P: ParamStore, x: torch.Tensor, wname: str, bn: BNParam) -
     if eng.training:
         L.call("edet_stem_fwd", eng.dt, vp(x), B, H, W, vp(P.wcv(wname)), Cout, vp(y), vp(bn.tsum), vp(bn.tsq), stream())
     else:
-        scratch = torch.zeros((2, Cout), dtype=torch.float64, device=eng.device)
+        scratch = eng.zeros64(2, Cout)
         L.call("edet_stem_fwd", eng.dt, vp(x), B, H, W, vp(P.wcv(wname)), Cout, vp(y), vp(scratch[0]),
                vp(scratch[1]), stream())
     out = Act(y, pyr, Cout, [bn], L.ACT_SWISH, training=eng.training, name="stem")
@@ -154,7 +154,7 @@ def squeeze_excite(eng: Engine, P: ParamStore, x: Act, prefix: str, R: int):
     B, C = x.pyr.batch, x.C
     HW = x.pyr.H * x.pyr.W
     s = stream()
-    svec = torch.zeros((B, C), dtype=torch.float64, device=eng.device)  # fp64 squeeze (edet.h)
+    svec = eng.zeros64(B, C)  # fp64 squeeze (edet.h)
     L.call("edet_se_squeeze", eng.dt, x.lazy(), B, HW, C, vp(svec), s)
     z1 = torch.empty((B, R), dtype=torch.float32, device=eng.device)
     gate = torch.empty((B, C), dtype=torch.float32, device=eng.device)

@@ -462,9 +462,41 @@ class Engine:
         self.device = torch.device(device)
         self.training = False
         self.tape: Optional[Tape] = None
+        # fp64 accumulators (SE squeeze / gate gradient, BN-backward sums) are bump-allocated
+        # from one arena zeroed by a single memset per forward (begin_scratch) instead of one
+        # fill kernel each
+        self._s64: Optional[torch.Tensor] = None
+        self._s64_off = 0
+        self._s64_need = 1 << 20
+        self._s64_hw = 0  # high-water mark over all steps: the extent the memset must cover
+        self._s64_overflow = []
 
     def empty(self, rows: int, C: int, dtype=None) -> torch.Tensor:
         return torch.empty((rows, C), dtype=dtype or self.tdtype, device=self.device)
+
+    def begin_scratch(self):
+        """Start of a forward: rewind the fp64 arena and zero it (one memset)."""
+        self._s64_hw = max(self._s64_hw, self._s64_off)
+        if self._s64 is None or self._s64.numel() < self._s64_need:
+            self._s64 = torch.empty(self._s64_need, dtype=torch.float64, device=self.device)
+            self._s64_hw = self._s64.numel()
+        self._s64_off = 0
+        self._s64_overflow = []
+        memset0(self._s64[: min(self._s64_hw, self._s64.numel())])
+
+    def zeros64(self, *shape) -> torch.Tensor:
+        """Zeroed fp64 scratch valid until the next begin_scratch()."""
+        n = int(np.prod(shape))
+        start = round_up(self._s64_off, 32)  # 256-B aligned views
+        if self._s64 is not None and start + n <= self._s64.numel():
+            self._s64_off = start + n
+            return self._s64[start:start + n].view(shape)
+        # arena too small this step: plain zeroed tensor now, a larger arena from the next step
+        self._s64_need = max(self._s64_need, 2 * (start + n))
+        self._s64_off = start + n
+        t = torch.zeros(shape, dtype=torch.float64, device=self.device)
+        self._s64_overflow.append(t)
+        return t
 
     def zeros_f32(self, *shape) -> torch.Tensor:
         t = torch.empty(shape, dtype=torch.float32, device=self.device)
