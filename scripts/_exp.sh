@@ -1,0 +1,4 @@
+set -u
+mkdir -p gpurun_out
+timeout -k 10 300 python -m pytest -q -x -m gpu tests > gpurun_out/t_new.log 2>&1; echo "tests rc=$?"; tail -25 gpurun_out/t_new.log
+timeout -k 10 200 python scripts/kbench.py --out gpurun_out/kb_new.txt --top 400 > /dev/null 2>gpurun_out/kb_new.err || exit 1

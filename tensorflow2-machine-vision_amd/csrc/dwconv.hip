@@ -345,6 +345,274 @@ __global__ __launch_bounds__(256) void k_dw_wgrad(DwArgs g) {
   }
 }
 
+// ------------------------------------------------------------------ pipelined tile forms
+// Same work unit as k_dw_fwd / k_dw_wgrad (8x8 output tile x 32 channels, persistent over the
+// tiles of one channel block), with the per-tile latency chain cut:
+//   * the lazy BN affine is derived once per segment (it was re-derived from the fp64 sums for
+//     every tile, a dependent global round trip before the tile's own loads could start);
+//   * tile t+1's raw input vectors (and its SE gate values) are fetched into registers while
+//     tile t is computed, then transformed into the other half of a double-buffered LDS tile;
+//   * the stencil keeps one input row per kh in registers and reuses it for all K taps of that
+//     row (K x (8*S+K-1) LDS reads per 8 outputs instead of K*K*8).
+// wgrad stages dy through LDS the same way and needs one barrier per tile.
+template <typename T, int K, int S, bool WGRAD>
+__global__ __launch_bounds__(256) void k_dw3(DwArgs g) {
+  constexpr int IH = (DTS - 1) * S + K, IW = IH, NPIX = IH * IW;
+  constexpr int RW = (DTS - 1) * S + K;                 // input row window per output row
+  constexpr int NV = (NPIX * (DCB / 8) + 255) / 256;    // staged vectors per thread
+  constexpr int TILEF = NPIX * DCB;
+  __shared__ __attribute__((aligned(16))) float tile[2][TILEF];
+  __shared__ __attribute__((aligned(16))) float dyt[WGRAD ? 2 : 1][WGRAD ? DTS * DTS * DCB : 4];
+  __shared__ __attribute__((aligned(16))) T otile[WGRAD ? 8 : DTS * DTS * DCB];
+  __shared__ float2 xf[DCB];
+  __shared__ float red[2][8][DCB];
+  const int tid = threadIdx.x, c = tid & 31, r = tid >> 5;
+  const int w = blockIdx.x;
+  const int cb = w % g.ncb, G = gridDim.x / g.ncb;
+  const int c0 = cb * DCB;
+  const int C = g.C;
+  const bool cvalid = (c0 + c) < C;
+  const int t0 = w / g.ncb;
+  if (t0 >= g.tiles_total) return;
+  const int nt = (g.tiles_total - 1 - t0) / G + 1;
+
+  float wr[WGRAD ? 1 : K * K];
+  if constexpr (!WGRAD) {
+    const T* Wp = (const T*)g.w;
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(Wp[(size_t)i * C + c0 + c]) : 0.f;
+  }
+  const T* X = (const T*)g.x;
+  const T* DY = (const T*)g.dy;
+  const bool has_gate = g.lz.gate != nullptr;
+
+  // ---- prefetch registers
+  uint4 rx[NV][sizeof(T) == 2 ? 1 : 2];
+  float4 rg[NV][2];
+  uint4 rdy[sizeof(T) == 2 ? 1 : 2];
+  int rvalid = 0;  // bit u: staged vector u is inside the image
+  auto fetch = [&](int t) {
+    int seg, n, ty, tx;
+    locate_tile(g.pout, t, seg, n, ty, tx);
+    const int H = g.pin.H[seg], W = g.pin.W[seg];
+    const int iy0 = ty * DTS * S - same_pad(H, K, S), ix0 = tx * DTS * S - same_pad(W, K, S);
+    const size_t base = (size_t)g.pin.row_off[seg] + (size_t)n * H * W;
+    rvalid = 0;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int v = tid + u * 256;
+      const int pix = v >> 2, cv = (v & 3) * 8;
+      const int yy = pix / IW, xx = pix - yy * IW;
+      const int gy = iy0 + yy, gx = ix0 + xx;
+      if (v < NPIX * 4 && gy >= 0 && gy < H && gx >= 0 && gx < W && c0 + cv < C) {
+        const uint4* src = reinterpret_cast<const uint4*>(X + (base + (size_t)gy * W + gx) * g.lz.ld + c0 + cv);
+        rx[u][0] = src[0];
+        if constexpr (sizeof(T) == 4) rx[u][1] = src[1];
+        if (has_gate) {
+          const float4* gp = reinterpret_cast<const float4*>(g.lz.gate + (size_t)n * C + c0 + cv);
+          rg[u][0] = gp[0];
+          rg[u][1] = gp[1];
+        }
+        rvalid |= 1 << u;
+      }
+    }
+    if constexpr (WGRAD) {  // dy tile: pixel tid/4 of the 8x8 tile, channels (tid%4)*8
+      const int OH = g.pout.H[seg], OW = g.pout.W[seg];
+      const int px = tid >> 2, cv = (tid & 3) * 8;
+      const int oy = ty * DTS + (px >> 3), ox = tx * DTS + (px & 7);
+      rdy[0] = make_uint4(0, 0, 0, 0);
+      if constexpr (sizeof(T) == 4) rdy[1] = make_uint4(0, 0, 0, 0);
+      if (oy < OH && ox < OW && c0 + cv < C) {
+        const uint4* src = reinterpret_cast<const uint4*>(
+            DY + ((size_t)g.pout.row_off[seg] + (size_t)n * OH * OW + (size_t)oy * OW + ox) * C + c0 + cv);
+        rdy[0] = src[0];
+        if constexpr (sizeof(T) == 4) rdy[1] = src[1];
+      }
+    }
+  };
+  auto unpack8 = [&](const uint4* q, float* o) {
+    if constexpr (sizeof(T) == 2) {
+      const uint32_t wv[4] = {q[0].x, q[0].y, q[0].z, q[0].w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        o[2 * i] = __uint_as_float(wv[i] << 16);
+        o[2 * i + 1] = __uint_as_float(wv[i] & 0xffff0000u);
+      }
+    } else {
+      const uint32_t wv[8] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = __uint_as_float(wv[i]);
+    }
+  };
+  auto commit = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int v = tid + u * 256;
+      if (v >= NPIX * 4) break;
+      const int pix = v >> 2, cv = (v & 3) * 8;
+      float vals[8];
+      if (rvalid & (1 << u)) {
+        unpack8(rx[u], vals);
+        const float gv[8] = {rg[u][0].x, rg[u][0].y, rg[u][0].z, rg[u][0].w, rg[u][1].x, rg[u][1].y, rg[u][1].z, rg[u][1].w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          vals[j] = lazy_apply(vals[j], xf[cv + j], g.lz.act);
+          if (has_gate) vals[j] *= gv[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vals[j] = 0.f;
+      }
+      float* d = &tile[buf][pix * DCB + cv];
+      reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
+      reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+    }
+    if constexpr (WGRAD) {
+      float vals[8];
+      unpack8(rdy, vals);
+      float* d = &dyt[buf][tid * 8];  // [pixel][32] with pixel = tid/4, channels (tid%4)*8
+      reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
+      reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+    }
+  };
+  int xf_seg = -1;
+  auto ensure_affine = [&](int seg) {  // block-uniform; rare (segment changes)
+    if (seg == xf_seg) return;
+    __syncthreads();
+    if (tid < DCB) {
+      const int cc = c0 + tid;
+      xf[tid] = cc < C ? bn_affine(g.lz.bn, seg, cc, 1.f / (float)seg_rows(g.pin, seg)) : make_float2(1.f, 0.f);
+    }
+    __syncthreads();
+    xf_seg = seg;
+  };
+  auto tile_seg = [&](int t) {
+    int seg, n, ty, tx;
+    locate_tile(g.pout, t, seg, n, ty, tx);
+    return seg;
+  };
+
+  float s = 0.f, q = 0.f;  // fwd BN statistics of channel c
+  float acc[WGRAD ? K * K : 1];
+#pragma unroll
+  for (int i = 0; i < (WGRAD ? K * K : 1); ++i) acc[i] = 0.f;
+  int cur_seg = -1;
+  auto flush_stats = [&](int seg) {  // block-uniform
+    __syncthreads();
+    red[0][r][c] = s;
+    red[1][r][c] = q;
+    __syncthreads();
+    if (tid < DCB && c0 + tid < C) {
+      float ss = 0.f, qq = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
+      atomicAdd(g.stats.sum[seg] + c0 + tid, (double)ss);
+      atomicAdd(g.stats.sq[seg] + c0 + tid, (double)qq);
+    }
+    s = 0.f;
+    q = 0.f;
+  };
+
+  fetch(t0);
+  ensure_affine(tile_seg(t0));
+  commit(0);
+  __syncthreads();
+  for (int i = 0; i < nt; ++i) {
+    const int t = t0 + i * G, buf = i & 1;
+    const bool more = i + 1 < nt;
+    int seg, n, ty, tx;
+    locate_tile(g.pout, t, seg, n, ty, tx);
+    if (!WGRAD && g.has_stats && seg != cur_seg) {
+      if (cur_seg >= 0) flush_stats(cur_seg);
+      cur_seg = seg;
+    }
+    if (more) fetch(t + G);
+    const float* tb = tile[buf];
+    if constexpr (!WGRAD) {
+      float o[DTS];
+#pragma unroll
+      for (int j = 0; j < DTS; ++j) o[j] = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < K; ++kh) {
+        float rowv[RW];
+        const float* trow = tb + ((r * S + kh) * IW) * DCB + c;
+#pragma unroll
+        for (int x = 0; x < RW; ++x) rowv[x] = trow[x * DCB];
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+          for (int j = 0; j < DTS; ++j) o[j] += rowv[j * S + kw] * wr[kh * K + kw];
+      }
+      const int OH = g.pout.H[seg], OW = g.pout.W[seg];
+      const int oy = ty * DTS + r;
+#pragma unroll
+      for (int j = 0; j < DTS; ++j) {
+        otile[(r * DTS + j) * DCB + c] = from_f<T>(o[j]);
+        if (oy < OH && tx * DTS + j < OW && cvalid) { s += o[j]; q += o[j] * o[j]; }
+      }
+      __syncthreads();
+      {
+        const int px = tid >> 2, cv = (tid & 3) * 8;
+        const int py = ty * DTS + (px >> 3), pxx = tx * DTS + (px & 7);
+        if (py < OH && pxx < OW && c0 + cv < C) {
+          T* Y = (T*)g.y;
+          const size_t o_ = ((size_t)g.pout.row_off[seg] + (size_t)n * OH * OW + (size_t)py * OW + pxx) * C + c0 + cv;
+          if constexpr (sizeof(T) == 2) {
+            *reinterpret_cast<uint4*>(Y + o_) = *reinterpret_cast<const uint4*>(otile + px * DCB + cv);
+          } else {
+            *reinterpret_cast<float4*>(Y + o_) = *reinterpret_cast<const float4*>(otile + px * DCB + cv);
+            *reinterpret_cast<float4*>(Y + o_ + 4) = *reinterpret_cast<const float4*>(otile + px * DCB + cv + 4);
+          }
+        }
+      }
+    } else {
+      float dyv[DTS];
+#pragma unroll
+      for (int j = 0; j < DTS; ++j) dyv[j] = cvalid ? dyt[buf][(r * DTS + j) * DCB + c] : 0.f;
+#pragma unroll
+      for (int kh = 0; kh < K; ++kh) {
+        float rowv[RW];
+        const float* trow = tb + ((r * S + kh) * IW) * DCB + c;
+#pragma unroll
+        for (int x = 0; x < RW; ++x) rowv[x] = trow[x * DCB];
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) {
+          float a = 0.f;
+#pragma unroll
+          for (int j = 0; j < DTS; ++j) a += dyv[j] * rowv[j * S + kw];
+          acc[kh * K + kw] += a;
+        }
+      }
+    }
+    if (more) {
+      ensure_affine(tile_seg(t + G));
+      commit(buf ^ 1);
+    }
+    __syncthreads();
+  }
+  if constexpr (!WGRAD) {
+    if (g.has_stats && cur_seg >= 0) flush_stats(cur_seg);
+  } else {
+    // block reduction of the K*K x 32 filter partials over the 8 row-threads (both tile
+    // buffers are free now and contiguous)
+    static_assert(K * K * 8 <= 2 * NPIX, "wgrad reduction scratch exceeds the tile buffers");
+    float* lds = &tile[0][0];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) lds[(i * 8 + r) * DCB + c] = acc[i];
+    __syncthreads();
+    for (int e = tid; e < K * K * DCB; e += 256) {
+      const int i = e / DCB, cc = e - i * DCB;
+      if (c0 + cc < C) {
+        float sum = 0.f;
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) sum += lds[(i * 8 + rr) * DCB + cc];
+        atomicAdd(g.dw + (size_t)i * C + c0 + cc, sum);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ direct (barrier-free) forms
 // One thread = one output pixel x one 8-channel vector; the K*K taps are 16-byte loads served
 // by L1/L2 (each input vector is reused by the neighbouring pixels' threads), transformed,
@@ -479,9 +747,27 @@ __global__ __launch_bounds__(256) void k_dw2_dgrad(DwArgs g, DwGeom geo) {
   }
 }
 
+template <typename T, int K, int S, bool WG>
+static int launch_dw3(DwArgs g, hipStream_t s) {
+  constexpr int IH = (DTS - 1) * S + K, NPIX = IH * IH;
+  constexpr size_t lds = 2 * NPIX * DCB * 4 + (WG ? 2 * DTS * DTS * DCB * 4 : DTS * DTS * DCB * sizeof(T)) + 2 * 8 * DCB * 4 + 256;
+  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / lds));
+  g.tiles_total = host_tiles(g.pout);
+  if (!g.tiles_total) return EDET_OK;
+  const int G = std::max(1, std::min(g.tiles_total, cdiv(256 * per_cu, g.ncb)));
+  hipLaunchKernelGGL((k_dw3<T, K, S, WG>), dim3(G * g.ncb), dim3(256), 0, s, g);
+  return check_launch("edet dwconv3");
+}
+
 template <typename T, int K, int S>
 static int launch_dw(int which, DwArgs g, hipStream_t s) {
   g.ncb = cdiv(g.C, DCB);
+  // pipelined tile form where it measured faster (scripts/kbench.py, D0 b32): it halves the
+  // blocks per CU (double-buffered LDS, more registers), which costs more than the prefetch
+  // gains on the large stride-2 and wide-channel layers
+  if (which == 0 && ((K == 3 && S == 2 && g.C >= 192) || (S == 1 && g.C >= 144 && g.C <= 240)))
+    return launch_dw3<T, K, S, false>(g, s);
+  if (which == 2 && S == 1 && (g.C <= 64 || (K == 5 && g.C == 240))) return launch_dw3<T, K, S, true>(g, s);
   // forward: the LDS tile kernel applies the producer's lazy BN/swish/gate once per input
   // element; the direct form re-evaluates it per tap (K*K times) and only wins at k3 s2.
   // dgrad has no transform: the direct gather form measured equal or up to 1.4x faster.

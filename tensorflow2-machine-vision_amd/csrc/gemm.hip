@@ -19,8 +19,6 @@
 
 namespace edet {
 
-constexpr int GBK = 32;
-constexpr int GLDK = GBK + 8;  // padded LDS row (elements): 80 B bf16 / 160 B fp32
 
 struct GemmArgs {
   const void* a;
@@ -69,16 +67,18 @@ __device__ __forceinline__ bf16x8_t lds_frag_bf16(const uint16_t* p) {
 // pipelined: chunk k+1 is fetched global -> registers while chunk k's MFMAs run, LDS is
 // double-buffered, one barrier per chunk (the unpipelined loop exposed the full load latency
 // 36 times per tile: 150 GB/s at M = 8192).  B is the [N][K] weight (k contiguous).
-template <typename T, int BM, int BN, bool LAZY>
+template <typename T, int BM, int BN, int KC, bool LAZY>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-  constexpr int AV = (BM * (GBK / 8) + 255) / 256, BV = (BN * (GBK / 8) + 255) / 256;
+  constexpr int KV = KC / 8, LDK = KC + 8;
+  constexpr int AV = (BM * KV + 255) / 256, BV = (BN * KV + 255) / 256;
   using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
   constexpr int VW = sizeof(T) == 2 ? 1 : 2;  // 16-byte words per 8 elements
-  __shared__ __attribute__((aligned(16))) T As[2][BM * GLDK];
-  __shared__ __attribute__((aligned(16))) T Bs[2][BN * GLDK];
+  __shared__ __attribute__((aligned(16))) T As[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) T Bs[2][BN * LDK];
   __shared__ float red[2][2][BN];  // [sum|sq][wm][col]: one writer each, summed in fixed order
-  extern __shared__ float2 xf[];   // [K] lazy affine per input channel (LAZY only)
+  extern __shared__ float2 xf[];   // [K] lazy affine per input channel, then [2][K] gate rows
+  float* gts = reinterpret_cast<float*>(xf + (LAZY ? g.K : 0));
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -92,24 +92,44 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   const int seg_end = seg_off + seg_rows(g.pyr, seg);
   const int hw = g.pyr.H[seg] * g.pyr.W[seg];
 
+  // SE gate rows of the (at most two, hw >= BM) images this tile spans, staged in LDS once:
+  // the per-element global gate loads sat on the chunk loop's critical path
+  const bool gate_lds = LAZY && g.lz.gate != nullptr && hw >= BM;
+  const int n_lo = (row0 - seg_off) / hw;
   if constexpr (LAZY) {
     const float inv = 1.f / (float)seg_rows(g.pyr, seg);
     for (int k = tid; k < g.K; k += 256) xf[k] = bn_affine(g.lz.bn, seg, k, inv);
+    if (gate_lds)
+      for (int k = tid; k < 2 * g.K; k += 256) {
+        const int n = n_lo + (k >= g.K);
+        gts[k] = (n < g.pyr.batch) ? g.lz.gate[(size_t)n * g.K + (k >= g.K ? k - g.K : k)] : 0.f;
+      }
   }
   __syncthreads();
 
   const T* A = (const T*)g.a;
   const T* B = (const T*)g.b;
   V ra[AV][VW], rb[BV][VW];
+  // per-thread A rows are fixed across chunks: resolve their gate rows once
+  const float* gpu_[AV];
+#pragma unroll
+  for (int u = 0; u < AV; ++u) {
+    const int grow = row0 + (tid + u * 256) / KV;
+    gpu_[u] = nullptr;
+    if (LAZY && g.lz.gate && grow < g.M) {
+      const int img = (grow - seg_off) / hw;
+      gpu_[u] = gate_lds ? gts + (img - n_lo) * g.K : g.lz.gate + (size_t)img * g.K;
+    }
+  }
   // global -> registers (raw); invalid lanes hold zeros
   auto fetch = [&](int k0) {
 #pragma unroll
     for (int u = 0; u < AV; ++u) {
       const int v = tid + u * 256;
-      const int r = v >> 2, kv = (v & 3) * 8, grow = row0 + r, gk = k0 + kv;
+      const int r = v / KV, kv = (v % KV) * 8, grow = row0 + r, gk = k0 + kv;
 #pragma unroll
       for (int w = 0; w < VW; ++w) ra[u][w] = V{};
-      if (v < BM * 4 && grow < g.M && gk < g.K) {
+      if (v < BM * KV && grow < g.M && gk < g.K) {
         const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + gk);
 #pragma unroll
         for (int w = 0; w < VW; ++w) ra[u][w] = src[w];
@@ -118,10 +138,10 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 #pragma unroll
     for (int u = 0; u < BV; ++u) {
       const int v = tid + u * 256;
-      const int n = v >> 2, kv = (v & 3) * 8, gn = col0 + n, gk = k0 + kv;
+      const int n = v / KV, kv = (v % KV) * 8, gn = col0 + n, gk = k0 + kv;
 #pragma unroll
       for (int w = 0; w < VW; ++w) rb[u][w] = V{};
-      if (v < BN * 4 && gn < g.N && gk < g.K) {
+      if (v < BN * KV && gn < g.N && gk < g.K) {
         const V* src = reinterpret_cast<const V*>(B + (size_t)gn * g.ldb + gk);
 #pragma unroll
         for (int w = 0; w < VW; ++w) rb[u][w] = src[w];
@@ -133,14 +153,14 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 #pragma unroll
     for (int u = 0; u < AV; ++u) {
       const int v = tid + u * 256;
-      if (v < BM * 4) {
-        const int r = v >> 2, kv = (v & 3) * 8;
-        T* dst = &As[buf][r * GLDK + kv];
+      if (v < BM * KV) {
+        const int r = v / KV, kv = (v % KV) * 8;
+        T* dst = &As[buf][r * LDK + kv];
         if constexpr (LAZY) {
           const int grow = row0 + r, gk = k0 + kv;
           const T* e = reinterpret_cast<const T*>(&ra[u][0]);
           float vals[8];
-          const float* gp = (g.lz.gate && grow < g.M) ? g.lz.gate + (size_t)((grow - seg_off) / hw) * g.K : nullptr;
+          const float* gp = gpu_[u];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             float x = 0.f;
@@ -160,10 +180,10 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 #pragma unroll
     for (int u = 0; u < BV; ++u) {
       const int v = tid + u * 256;
-      if (v < BN * 4) {
-        const int n = v >> 2, kv = (v & 3) * 8;
+      if (v < BN * KV) {
+        const int n = v / KV, kv = (v % KV) * 8;
 #pragma unroll
-        for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(&Bs[buf][n * GLDK + kv])[w] = rb[u][w];
+        for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(&Bs[buf][n * LDK + kv])[w] = rb[u][w];
       }
     }
   };
@@ -174,45 +194,48 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = cdiv(g.K, GBK);
+  const int nk = cdiv(g.K, KC);
   fetch(0);
   commit(0, 0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     const bool more = kt + 1 < nk;
-    if (more) fetch((kt + 1) * GBK);
+    if (more) fetch((kt + 1) * KC);
     const T* Ab = As[buf];
     const T* Bb = Bs[buf];
-    if constexpr (sizeof(T) == 2) {
-      bf16x8_t af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
-        af[i] = lds_frag_bf16(&Ab[(wm * WM + i * 16 + (lane & 15)) * GLDK + 8 * (lane >> 4)]);
+    for (int ks = 0; ks < KC; ks += 32) {
+      if constexpr (sizeof(T) == 2) {
+        bf16x8_t af[FM], bfr[FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
-        bfr[j] = lds_frag_bf16(&Bb[(wn * WN + j * 16 + (lane & 15)) * GLDK + 8 * (lane >> 4)]);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i)
+          af[i] = lds_frag_bf16(&Ab[(wm * WM + i * 16 + (lane & 15)) * LDK + ks + 8 * (lane >> 4)]);
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int s = 0; s < GBK / 4; ++s) {
-        float af[FM], bfr[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) af[i] = Ab[(wm * WM + i * 16 + (lane & 15)) * GLDK + 4 * s + (lane >> 4)];
-#pragma unroll
-        for (int j = 0; j < FN; ++j) bfr[j] = Bb[(wn * WN + j * 16 + (lane & 15)) * GLDK + 4 * s + (lane >> 4)];
+          bfr[j] = lds_frag_bf16(&Bb[(wn * WN + j * 16 + (lane & 15)) * LDK + ks + 8 * (lane >> 4)]);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          float af[FM], bfr[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i) af[i] = Ab[(wm * WM + i * 16 + (lane & 15)) * LDK + ks + 4 * s + (lane >> 4)];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bfr[j] = Bb[(wn * WN + j * 16 + (lane & 15)) * LDK + ks + 4 * s + (lane >> 4)];
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
       }
     }
-    if (more) commit(buf ^ 1, (kt + 1) * GBK);
+    if (more) commit(buf ^ 1, (kt + 1) * KC);
     __syncthreads();
   }
 
@@ -827,15 +850,397 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
   }
 }
 
+// ------------------------------------------------------------------ B-resident GEMM
+// Persistent kernel for the memory-bound 1x1 convs.  Each block loads its column group of the
+// weight B [NG][KP] into LDS ONCE, then streams A through the chip in chunks of R rows x KC
+// columns (~16 KB): chunk q+1 is fetched global -> registers (raw values, plus the SE gate
+// values it will need) while chunk q is multiplied, then transformed (lazy BN / swish / gate)
+// into the other LDS buffer; one barrier per chunk.  Without B traffic the per-CU request
+// stream is only A (the previous kernels re-read B from L2 for every 32-128 row tile, and the
+// counters showed them parked on memory for ~65 % of the wave cycles).
+//   case S (!KSTREAM): the chunk holds whole rows (KC = KP <= 256), R = 64..256 rows; every
+//     64-row tile is multiplied against the group's columns in 64-column sub-chunks.
+//   case L (KSTREAM): R = 64, K walked in KC = 128 slices with the accumulators kept; NG =
+//     32 * FN columns per group (B [NG][KP] still resident).
+// Output: each wave stages its 32 x 16*FN accumulator tile in a private LDS patch and writes
+// it back as 16-byte row vectors (no block barrier).  BN statistics: per-block fp32 partials
+// in LDS with one owner lane each, flushed as fp64 atomics once per segment.
+#ifndef EDET_PW_ABL
+#define EDET_PW_ABL 0
+#endif
+struct PwPlan {
+  int R, KC, KP, nkc, NG, ngroups, nrg, LDA, LDB, nsub, NGtot;
+};
+
+constexpr int PW_NV = 8;  // max 16-byte A vectors per thread per chunk
+
+template <typename T, int FN, bool KSTREAM, bool LAZY>
+__global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
+  using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
+  constexpr int VW = sizeof(T) == 2 ? 1 : 2;
+  constexpr int CWLD = 16 * FN + 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* Bs = reinterpret_cast<T*>(smem);                  // [NG][LDB]
+  T* As = Bs + (size_t)p.NG * p.LDB;                    // [2][R][LDA]
+  T* Cw = As + 2 * (size_t)p.R * p.LDA;                 // [4 waves][32][CWLD]
+  float* red = reinterpret_cast<float*>(Cw + 4 * 32 * CWLD);  // [sum|sq][wm][NGtot]
+  float2* xf = reinterpret_cast<float2*>(red + 4 * p.NGtot);  // [nseg][KP] (LAZY)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = w % p.ngroups, G = gridDim.x / p.ngroups;
+  const int rg0 = w / p.ngroups;
+  if (rg0 >= p.nrg) return;
+  const int col_base = grp * p.NG;
+  const int K = g.K, N = g.N, M = g.M;
+
+  // ---- resident B (this group's columns, zero past N and K), stats partials, BN affine
+  {
+    const T* B = (const T*)g.b;
+    const int kvb = p.KP / 8;
+    for (int v = tid; v < p.NG * kvb; v += 256) {
+      const int n = v / kvb, kv = (v - n * kvb) * 8, gn = col_base + n;
+      T* dst = Bs + (size_t)n * p.LDB + kv;
+      if (gn < N && kv < K) cp8(dst, B + (size_t)gn * g.ldb + kv, K - kv);
+      else zero8(dst);
+    }
+    for (int c = tid; c < 4 * p.NGtot; c += 256) red[c] = 0.f;
+    if constexpr (LAZY) {
+      for (int s = 0; s < g.pyr.nseg; ++s) {
+        const float inv = 1.f / (float)seg_rows(g.pyr, s);
+        for (int k = tid; k < p.KP; k += 256) xf[s * p.KP + k] = k < K ? bn_affine(g.lz.bn, s, k, inv) : make_float2(0.f, 0.f);
+      }
+    }
+  }
+
+  const int KV = p.KC / 8;
+  const int nvec = p.R * KV;
+  const int nq = ((p.nrg - 1 - rg0) / G + 1) * p.nkc;
+  const T* A = (const T*)g.a;
+  const bool has_gate = LAZY && g.lz.gate != nullptr;
+  V ra[PW_NV][VW];
+  float4 gr[LAZY ? PW_NV : 1][2];
+
+  auto fetch = [&](int q) {
+    const int rg = rg0 + (q / p.nkc) * G, kc = q % p.nkc;
+    const int rbase = rg * p.R;
+    int seg = 0, seg_off = 0, hw = 1;
+    if (has_gate) { seg = seg_of_row(g.pyr, rbase); seg_off = g.pyr.row_off[seg]; hw = g.pyr.H[seg] * g.pyr.W[seg]; }
+#pragma unroll
+    for (int u = 0; u < PW_NV; ++u) {
+      const int v = tid + u * 256;
+#pragma unroll
+      for (int ww = 0; ww < VW; ++ww) ra[u][ww] = V{};
+      const int r = v / KV, kv = (v - r * KV) * 8;
+      const int grow = rbase + r, gk = kc * p.KC + kv;
+      const bool live = v < nvec && grow < M && gk < K;
+#if EDET_PW_ABL == 3
+      if (false) {
+#else
+      if (live) {
+#endif
+        const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + gk);
+#pragma unroll
+        for (int ww = 0; ww < VW; ++ww) ra[u][ww] = src[ww];
+      }
+      if constexpr (LAZY) {
+        if (has_gate && live) {
+          const float4* gp = reinterpret_cast<const float4*>(g.lz.gate + (size_t)((grow - seg_off) / hw) * K + gk);
+          gr[u][0] = gp[0];
+          gr[u][1] = gp[1];
+        }
+      }
+    }
+  };
+  auto commit = [&](int q, int buf) {
+    const int rg = rg0 + (q / p.nkc) * G, kc = q % p.nkc;
+    const int rbase = rg * p.R;
+    const int seg = LAZY ? seg_of_row(g.pyr, rbase) : 0;
+    T* Ab = As + (size_t)buf * p.R * p.LDA;
+#pragma unroll
+    for (int u = 0; u < PW_NV; ++u) {
+      const int v = tid + u * 256;
+      if (v >= nvec) break;
+      const int r = v / KV, kv = (v - r * KV) * 8;
+      T* dst = Ab + (size_t)r * p.LDA + kv;
+      if constexpr (LAZY) {
+        const int grow = rbase + r, gk = kc * p.KC + kv;
+        const bool live = grow < M && gk < K;
+        const T* e = reinterpret_cast<const T*>(&ra[u][0]);
+        const float gv[8] = {gr[u][0].x, gr[u][0].y, gr[u][0].z, gr[u][0].w,
+                             gr[u][1].x, gr[u][1].y, gr[u][1].z, gr[u][1].w};
+        const float2* af = xf + seg * p.KP + (live ? gk : 0);
+        float vals[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float x = lazy_apply(to_f<T>(e[j]), af[j], g.lz.act);
+          if (has_gate) x *= gv[j];
+          vals[j] = live ? x : 0.f;
+        }
+        st8(dst, vals);
+      } else {
+#pragma unroll
+        for (int ww = 0; ww < VW; ++ww) reinterpret_cast<V*>(dst)[ww] = ra[u][ww];
+      }
+    }
+  };
+
+  // ---- MFMA over k in [0, kn) of A rows (a_row0 ..) x B rows (b_row0 ..) at B column kb0
+  auto mma = [&](floatx4 (&acc)[2][FN], const T* Ab, int a_row0, int b_row0, int kb0, int kn) {
+#if EDET_PW_ABL == 2
+    return;
+#endif
+    const T* ap = Ab + (size_t)(a_row0 + wm * 32 + (lane & 15)) * p.LDA;
+    const T* bp = Bs + (size_t)(b_row0 + wn * 16 * FN + (lane & 15)) * p.LDB + kb0;
+    for (int ks = 0; ks < kn; ks += 32) {
+      if constexpr (sizeof(T) == 2) {
+        bf16x8_t af[2], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = lds_frag_bf16(ap + (size_t)i * 16 * p.LDA + ks + 8 * (lane >> 4));
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = lds_frag_bf16(bp + (size_t)j * 16 * p.LDB + ks + 8 * (lane >> 4));
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int s4 = 0; s4 < 8; ++s4) {
+          float af[2], bfr[FN];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) af[i] = ap[(size_t)i * 16 * p.LDA + ks + 4 * s4 + (lane >> 4)];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bfr[j] = bp[(size_t)j * 16 * p.LDB + ks + 4 * s4 + (lane >> 4)];
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  // ---- epilogue of one wave tile: rows row0 + wm*32 .., group-local columns cl0 + wn*16*FN ..
+  T* cw = Cw + (size_t)wave * 32 * CWLD;
+  T* C = (T*)g.c;
+  auto epilogue = [&](floatx4 (&acc)[2][FN], int row0, int cl0, int seg_end) {
+    const int wrow0 = row0 + wm * 32;
+    const int wcl0 = cl0 + wn * 16 * FN;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int cl = wcl0 + j * 16 + (lane & 15);
+      const int col = col_base + cl;
+      const float bv = (g.bias && col < N) ? g.bias[col] : 0.f;
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rl = i * 16 + (lane >> 4) * 4 + r;
+          const float v = acc[i][j][r] + bv;
+          cw[rl * CWLD + j * 16 + (lane & 15)] = from_f<T>(v);
+          if (wrow0 + rl < seg_end) { s += v; q += v * v; }
+        }
+      if (g.has_stats) {
+        s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+        q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+        if (lane < 16) {  // sole owner of (wm, cl)
+          red[(0 * 2 + wm) * p.NGtot + cl] += s;
+          red[(1 * 2 + wm) * p.NGtot + cl] += q;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr int VPR = 2 * FN;  // 8-element vectors per tile row
+#pragma unroll
+    for (int e = lane; e < 32 * VPR; e += 64) {
+      const int rr = e / VPR, cv = (e - rr * VPR) * 8;
+      const int grow = wrow0 + rr, gcol = col_base + wcl0 + cv;
+#if EDET_PW_ABL == 1
+      if (grow < 0) {
+#else
+      if (grow < M && gcol < N) {
+#endif
+        float vals[8];
+        const T* src = cw + rr * CWLD + cv;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) vals[jj] = to_f<T>(src[jj]);
+        acc8m(C + (size_t)grow * g.ldc + gcol, N - gcol, vals, g.accumulate);
+      }
+    }
+  };
+  auto flush = [&](int seg) {
+    if (!g.has_stats || seg < 0 || lane >= 16) return;
+    for (int sub = 0; sub < p.nsub; ++sub)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int cl = sub * 64 + wn * 16 * FN + j * 16 + lane;
+        const int col = col_base + cl;
+        if (col < N && cl < p.NGtot) {
+          float& rs = red[(0 * 2 + wm) * p.NGtot + cl];
+          float& rq = red[(1 * 2 + wm) * p.NGtot + cl];
+          atomicAdd(g.stats.sum[seg] + col, (double)rs);
+          atomicAdd(g.stats.sq[seg] + col, (double)rq);
+          rs = 0.f;
+          rq = 0.f;
+        }
+      }
+  };
+
+  floatx4 acc[2][FN];
+  int cur_seg = -1;
+  fetch(0);
+  __syncthreads();  // B, affine tables and partials are in place
+  commit(0, 0);
+  __syncthreads();
+  for (int q = 0; q < nq; ++q) {
+    const int buf = q & 1;
+    const bool more = q + 1 < nq;
+    if (more) fetch(q + 1);
+    const int rg = rg0 + (q / p.nkc) * G, kc = q % p.nkc;
+    const int rbase = rg * p.R;
+    const int seg = seg_of_row(g.pyr, rbase);
+    const int seg_end = g.pyr.row_off[seg] + seg_rows(g.pyr, seg);
+    if (seg != cur_seg) {
+      flush(cur_seg);
+      cur_seg = seg;
+    }
+    const T* Ab = As + (size_t)buf * p.R * p.LDA;
+    if constexpr (!KSTREAM) {
+      for (int t = 0; t < p.R / 64; ++t) {
+        const int row0 = rbase + t * 64;
+        if (row0 >= M) break;
+        for (int sub = 0; sub < p.nsub; ++sub) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+          mma(acc, Ab, t * 64, sub * 64, 0, p.KP);
+          epilogue(acc, row0, sub * 64, seg_end);
+        }
+      }
+    } else {
+      if (kc == 0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+      mma(acc, Ab, 0, 0, kc * p.KC, p.KC);
+      if (kc == p.nkc - 1) epilogue(acc, rbase, 0, seg_end);
+    }
+    if (more) commit(q + 1, buf ^ 1);
+    __syncthreads();
+  }
+  flush(cur_seg);
+}
+
+static size_t pw_lds(const PwPlan& p, int FN, int nseg, bool lazy, int es) {
+  return (size_t)p.NG * p.LDB * es + 2 * (size_t)p.R * p.LDA * es + 4 * 32 * (16 * FN + 8) * (size_t)es +
+         4 * (size_t)p.NGtot * 4 + (lazy ? (size_t)nseg * p.KP * 8 : 0);
+}
+
+// Plan the B-resident launch; false when the shape does not fit (caller falls back).
+static bool pw_plan(const GemmArgs& g, bool lazy, int es, PwPlan& p, int& FN, bool& kstream) {
+  const bool gate = lazy && g.lz.gate != nullptr;
+  const int nseg = g.pyr.nseg;
+  p.KP = cdiv(g.K, 32) * 32;
+  kstream = p.KP > (gate ? 128 : 256);
+  constexpr size_t CAP = 150 * 1024, PAIR = 78 * 1024;  // one / two blocks per CU
+  if (!kstream) {
+    p.KC = p.KP;
+    p.nkc = 1;
+    int R = 64;
+    while (R < 256 && 2 * R * p.KP <= 8192) R *= 2;
+    if (nseg > 1 && R > 128) R = 128;  // chunks never straddle a (128-aligned) segment start
+    p.R = R;
+    p.LDA = p.LDB = p.KP + 8;
+    FN = 2;
+    const int nch = cdiv(g.N, 64);
+    // fewest column groups whose LDS image fits; two blocks per CU preferred up to 4 groups
+    int best = -1;
+    for (int ng = 1; ng <= nch; ++ng) {
+      const int cps = cdiv(nch, ng);
+      PwPlan t = p;
+      t.NG = t.NGtot = cps * 64;
+      t.nsub = cps;
+      const size_t l = pw_lds(t, FN, nseg, lazy, es);
+      if (l <= PAIR && ng <= 4) { best = ng; break; }
+      if (l <= CAP && best < 0) best = ng;
+      if (l <= CAP && ng > 4) break;
+    }
+    if (best < 0) return false;
+    const int cps = cdiv(nch, best);
+    p.NG = p.NGtot = cps * 64;
+    p.nsub = cps;
+    p.ngroups = cdiv(nch, cps);
+  } else {
+    p.KC = 128;
+    p.KP = cdiv(g.K, p.KC) * p.KC;
+    p.nkc = p.KP / p.KC;
+    p.R = 64;
+    p.LDA = p.KC + 8;
+    p.LDB = p.KP + 8;
+    p.nsub = 1;
+    FN = 2;
+    p.NG = p.NGtot = 64;
+    if (pw_lds(p, FN, nseg, lazy, es) > CAP || g.N <= 32) {
+      FN = 1;
+      p.NG = p.NGtot = 32;
+      if (pw_lds(p, FN, nseg, lazy, es) > CAP) return false;
+    }
+    p.ngroups = cdiv(g.N, p.NG);
+  }
+  p.nrg = cdiv(g.M, p.R);
+  return true;
+}
+
+template <typename T, int FN, bool KS, bool LAZY>
+static int launch_pwb(const GemmArgs& g, const PwPlan& p, hipStream_t s) {
+  const size_t lds = pw_lds(p, FN, g.pyr.nseg, LAZY, sizeof(T));
+  const int per_cu = lds <= 78 * 1024 ? 2 : 1;
+  const long want = (long)256 * per_cu;
+  long rows = std::min<long>(p.nrg, std::max<long>(1, want / p.ngroups));
+  const int grid = (int)(rows * p.ngroups);
+  hipLaunchKernelGGL((k_pwb<T, FN, KS, LAZY>), dim3(grid), dim3(256), lds, s, g, p);
+  return check_launch("edet pwb");
+}
+
+template <typename T, bool LAZY>
+static int dispatch_pwb(const GemmArgs& g, hipStream_t s, bool& done) {
+  PwPlan p;
+  int FN;
+  bool ks;
+  done = false;
+  if (g.ldc % 8 != 0 || g.lda % 8 != 0 || g.K % 8 != 0) return EDET_OK;  // 16-byte row vectors
+  if (g.M == 0 || !pw_plan(g, LAZY, sizeof(T), p, FN, ks)) return EDET_OK;
+  // measured per shape against the A-resident / K-loop kernels (scripts/kbench.py): the
+  // B-resident form wins for wide outputs over short rows, where those re-stage B per tile
+  // (class predict 224 -> 104 us); the K-streamed variant re-reads and re-transforms A per
+  // column group and loses
+  const int KP = cdiv(g.K, 32) * 32;
+  const bool lazy_in = LAZY;
+  if (ks || !(lazy_in ? (g.N >= 192 && KP <= 96) : (g.N >= 128 && KP <= 192))) return EDET_OK;
+  done = true;
+  if (!ks) return launch_pwb<T, 2, false, LAZY>(g, p, s);
+  if (FN == 2) return launch_pwb<T, 2, true, LAZY>(g, p, s);
+  return launch_pwb<T, 1, true, LAZY>(g, p, s);
+}
+
 // ------------------------------------------------------------------ launch helpers
-template <typename T, int BM, int BN, bool LAZY>
+template <typename T, int BM, int BN, bool LAZY, int KC = 32>
 static int launch_gemm(GemmArgs g, hipStream_t s) {
   g.ntm = cdiv(g.M, BM);
   g.ntn = cdiv(g.N, BN);
   const int nwg = g.ntm * g.ntn;
   if (nwg == 0) return EDET_OK;
-  const size_t dyn = LAZY ? (size_t)g.K * sizeof(float2) : 0;
-  hipLaunchKernelGGL((k_gemm<T, BM, BN, LAZY>), dim3(nwg), dim3(256), dyn, s, g);
+  const size_t dyn = LAZY ? (size_t)g.K * (sizeof(float2) + 2 * sizeof(float)) : 0;
+  hipLaunchKernelGGL((k_gemm<T, BM, BN, KC, LAZY>), dim3(nwg), dim3(256), dyn, s, g);
   return check_launch("edet gemm");
 }
 
@@ -892,6 +1297,13 @@ static int dispatch_gemm_kloop(GemmArgs g, hipStream_t s) {
 
 template <typename T, bool LAZY>
 static int dispatch_gemm(GemmArgs g, hipStream_t s) {
+#ifndef EDET_NO_PWB
+  {
+    bool done = false;
+    const int rc = dispatch_pwb<T, LAZY>(g, s, done);
+    if (done || rc) return rc;
+  }
+#endif
   // A-resident kernel whenever its LDS image fits (<= 96 KB: >= 1 block per CU with room);
   // BM = rows per block chosen as the largest that fits.  Otherwise stream K (N <= 320).
   const int KP = cdiv(g.K, 32) * 32;

@@ -8,6 +8,7 @@
 //            with R_i in {identity, nearest resize (tf.image.resize, half-pixel centres),
 //            max-pool}; weights unconstrained (no ReLU)
 #include <float.h>
+#include <algorithm>
 #include "common.hpp"
 
 namespace edet {
@@ -134,6 +135,191 @@ __global__ __launch_bounds__(256) void k_stem_wgrad(const T* x, int B, int H, in
       else atomicAdd(dw + j, acc[i]);
     }
   }
+}
+
+// ------------------------------------------------------------------ stem on MFMA (bf16)
+// The 3x3x3 patch is K = 27 (zero-padded to 32): exactly one v_mfma_f32_16x16x32_bf16 step.
+// One block owns R output rows of one image and stages the 2R+1 input rows they need in LDS
+// (16-byte loads when a row is 16-byte aligned).  Operands are swapped (A = the weights as
+// [Cout][k], B = the patches as [k][pixel]) so each lane ends up with 4 consecutive output
+// channels of one pixel: 8-byte stores, and BN statistics accumulate per lane over all the
+// block's pixels before one cross-lane reduction.
+__device__ __forceinline__ void stem_stage_rows(const uint16_t* x, int H, int W, int n, int iy0, int IR, int RLP,
+                                                uint16_t* xs) {
+  const int RL = W * 3;
+  if ((W & 7) == 0) {
+    const int vpr = RL / 8;
+    for (int v = threadIdx.x; v < IR * vpr; v += blockDim.x) {
+      const int i = v / vpr, j = v - i * vpr, iy = iy0 + i;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (iy >= 0 && iy < H) val = *reinterpret_cast<const uint4*>(x + ((size_t)n * H + iy) * RL + j * 8);
+      *reinterpret_cast<uint4*>(xs + i * RLP + j * 8) = val;
+    }
+  } else {
+    for (int e = threadIdx.x; e < IR * RL; e += blockDim.x) {
+      const int i = e / RL, j = e - i * RL, iy = iy0 + i;
+      xs[i * RLP + j] = (iy >= 0 && iy < H) ? x[((size_t)n * H + iy) * RL + j] : (uint16_t)0;
+    }
+  }
+}
+
+// tap k = (kh*3 + kw)*3 + ci of output pixel (ry, ox) inside the staged rows (0 outside)
+__device__ __forceinline__ uint16_t stem_tap(const uint16_t* xs, int RLP, int W, int pl, int ry, int ox, int k) {
+  if (k >= 27) return 0;
+  const int kh = k / 9, kw = (k / 3) % 3, ci = k % 3;
+  const int ix = 2 * ox - pl + kw;
+  if (ix < 0 || ix >= W) return 0;
+  return xs[(2 * ry + kh) * RLP + ix * 3 + ci];
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) void k_stem2_fwd(const uint16_t* x, int B, int H, int W, const uint16_t* w, int Cout,
+                                                   uint16_t* y, double* sum, double* sq, int R) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
+  __shared__ float red[2][4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g4 = lane >> 4;
+  const int OH = cdiv(H, 2), OW = cdiv(W, 2);
+  const int pt = same_pad(H, 3, 2), pl = same_pad(W, 3, 2);
+  const int strips = cdiv(OH, R);
+  const int n = blockIdx.x / strips, oy0 = (blockIdx.x - n * strips) * R;
+  const int RLP = cdiv(W * 3, 8) * 8;
+  stem_stage_rows(x, H, W, n, oy0 * 2 - pt, 2 * R + 1, RLP, xs);
+  // A fragments: weights W[k][co] (HWIO), lane: k = 8*g4 .. +7, co = t*16 + lane%16
+  bf16x8_t wa[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    uint16_t e8[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * g4 + e;
+      e8[e] = k < 27 ? w[k * Cout + t * 16 + (lane & 15)] : (uint16_t)0;
+    }
+    wa[t] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(e8));
+  }
+  __syncthreads();
+  const int rows = min(R, OH - oy0);
+  const int P = rows * OW;
+  float s[NT][4], q[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[t][r] = q[t][r] = 0.f;
+  const size_t pix0 = ((size_t)n * OH + oy0) * OW;
+  for (int tile = wave; tile * 16 < P; tile += 4) {
+    const int pix = tile * 16 + (lane & 15);
+    const bool valid = pix < P;
+    const int ry = valid ? pix / OW : 0, ox = valid ? pix - ry * OW : 0;
+    uint16_t b8[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b8[e] = valid ? stem_tap(xs, RLP, W, pl, ry, ox, 8 * g4 + e) : (uint16_t)0;
+    const bf16x8_t bf = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(b8));
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      floatx4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t], bf, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      if (valid) {
+        uint32_t lo = (uint32_t)f2bf(acc[0]) | ((uint32_t)f2bf(acc[1]) << 16);
+        uint32_t hi = (uint32_t)f2bf(acc[2]) | ((uint32_t)f2bf(acc[3]) << 16);
+        *reinterpret_cast<uint2*>(y + (pix0 + pix) * Cout + t * 16 + 4 * g4) = make_uint2(lo, hi);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { s[t][r] += acc[r]; q[t][r] += acc[r] * acc[r]; }
+      }
+    }
+  }
+  // reduce over the 16 pixel lanes that share a channel group, then over the 4 waves
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a = s[t][r], b = q[t][r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
+      if ((lane & 15) == 0) {
+        red[0][wave][t * 16 + 4 * g4 + r] = a;
+        red[1][wave][t * 16 + 4 * g4 + r] = b;
+      }
+    }
+  __syncthreads();
+  if (tid < Cout) {
+    atomicAdd(sum + tid, (double)((red[0][0][tid] + red[0][1][tid]) + (red[0][2][tid] + red[0][3][tid])));
+    atomicAdd(sq + tid, (double)((red[1][0][tid] + red[1][1][tid]) + (red[1][2][tid] + red[1][3][tid])));
+  }
+}
+
+// dW[k][co] = sum_pixels patch[pixel][k] * dy[pixel][co]: D = A (patches^T, [k][pixel]) x
+// B (dy, [pixel][co]) over 32-pixel steps.  Persistent over row strips; each block writes one
+// [27][Cout] partial (summed in a fixed order afterwards).
+template <int NT>
+__global__ __launch_bounds__(256) void k_stem2_wgrad(const uint16_t* x, int B, int H, int W, const uint16_t* dy,
+                                                     int Cout, float* part, int R) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t xs[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g4 = lane >> 4;
+  const int OH = cdiv(H, 2), OW = cdiv(W, 2);
+  const int pt = same_pad(H, 3, 2), pl = same_pad(W, 3, 2);
+  const int strips = cdiv(OH, R), total = B * strips;
+  const int RLP = cdiv(W * 3, 8) * 8;
+  const int DLD = Cout + 8;
+  uint16_t* ds = xs + (2 * R + 1) * RLP;  // [R*OW][DLD]
+  floatx4 acc[2][NT];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[i][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int st = blockIdx.x; st < total; st += gridDim.x) {
+    const int n = st / strips, oy0 = (st - n * strips) * R;
+    const int rows = min(R, OH - oy0), P = rows * OW;
+    __syncthreads();  // previous strip's readers are done
+    stem_stage_rows(x, H, W, n, oy0 * 2 - pt, 2 * R + 1, RLP, xs);
+    const uint16_t* dsrc = dy + ((size_t)n * OH + oy0) * OW * Cout;
+    const int vpp = Cout / 8;
+    for (int v = tid; v < R * OW * vpp; v += 256) {
+      const int p = v / vpp, j = (v - p * vpp) * 8;
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (p < P) val = *reinterpret_cast<const uint4*>(dsrc + (size_t)p * Cout + j);
+      *reinterpret_cast<uint4*>(ds + p * DLD + j) = val;
+    }
+    __syncthreads();
+    for (int c32 = wave; c32 * 32 < P; c32 += 4) {
+      bf16x8_t af[2], bf[NT];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {  // A: row k = i*16 + lane%16, pixels 8*g4 .. +7 of this step
+        uint16_t e8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int pix = c32 * 32 + 8 * g4 + e;
+          const int ry = pix / OW, ox = pix - ry * OW;
+          e8[e] = pix < P ? stem_tap(xs, RLP, W, pl, ry, ox, i * 16 + (lane & 15)) : (uint16_t)0;
+        }
+        af[i] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(e8));
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {  // B: pixels 8*g4 .. +7, column co = t*16 + lane%16
+        uint16_t e8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {  // rows past P are not staged (0 * garbage may be NaN)
+          const int pix = c32 * 32 + 8 * g4 + e;
+          e8[e] = pix < P ? ds[pix * DLD + t * 16 + (lane & 15)] : (uint16_t)0;
+        }
+        bf[t] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(e8));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[t], acc[i][t], 0, 0, 0);
+    }
+  }
+  // reduce the four waves' accumulators (fixed order) and write this block's partial
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(xs);  // [4][32][Cout]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        red[(wave * 32 + i * 16 + 4 * g4 + r) * Cout + t * 16 + (lane & 15)] = acc[i][t][r];
+  __syncthreads();
+  for (int e = tid; e < 27 * Cout; e += 256)
+    part[(size_t)blockIdx.x * 27 * Cout + e] = (red[e] + red[32 * Cout + e]) + (red[64 * Cout + e] + red[96 * Cout + e]);
 }
 
 // ------------------------------------------------------------------ resample helpers
@@ -430,6 +616,24 @@ int edet_stem_fwd(int dtype, const void* x, int B, int H, int W, const void* w, 
   EDET_REQUIRE(Cout % 8 == 0 && Cout <= 64, "stem_fwd: Cout must be a multiple of 8, <= 64");
   const long px = (long)B * cdiv(H, 2) * cdiv(W, 2);
   const int nb = (int)((px + 255) / 256);
+  if (dtype == EDET_BF16 && Cout % 16 == 0 && px > 0) {
+    const int OH = cdiv(H, 2), OW = cdiv(W, 2);
+    const int R = std::max(1, std::min(8, 1024 / OW));
+    const size_t lds = (size_t)(2 * R + 1) * cdiv(W * 3, 8) * 8 * 2;
+    EDET_REQUIRE(lds <= 64 * 1024, "stem_fwd: image rows too wide (W=%d)", W);
+    const int grid = B * cdiv(OH, R);
+    const uint16_t* xb = (const uint16_t*)x;
+    const uint16_t* wb = (const uint16_t*)w;
+    uint16_t* yb = (uint16_t*)y;
+    hipStream_t st = (hipStream_t)stream;
+    switch (Cout / 16) {
+      case 1: hipLaunchKernelGGL(k_stem2_fwd<1>, dim3(grid), dim3(256), lds, st, xb, B, H, W, wb, Cout, yb, sum, sq, R); break;
+      case 2: hipLaunchKernelGGL(k_stem2_fwd<2>, dim3(grid), dim3(256), lds, st, xb, B, H, W, wb, Cout, yb, sum, sq, R); break;
+      case 3: hipLaunchKernelGGL(k_stem2_fwd<3>, dim3(grid), dim3(256), lds, st, xb, B, H, W, wb, Cout, yb, sum, sq, R); break;
+      default: hipLaunchKernelGGL(k_stem2_fwd<4>, dim3(grid), dim3(256), lds, st, xb, B, H, W, wb, Cout, yb, sum, sq, R); break;
+    }
+    return check_launch("edet stem2_fwd");
+  }
   EDET_DTYPE_DISPATCH(dtype, T, {
     if (nb) hipLaunchKernelGGL(k_stem_fwd<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const T*)x, B, H, W,
                                (const T*)w, Cout, (T*)y, sum, sq);
@@ -442,6 +646,28 @@ int edet_stem_wgrad(int dtype, const void* x, int B, int H, int W, const void* d
   EDET_REQUIRE(x && dy && dw, "stem_wgrad: null argument");
   EDET_REQUIRE(Cout % 8 == 0 && Cout <= 64, "stem_wgrad: Cout must be a multiple of 8, <= 64");
   const long px = (long)B * cdiv(H, 2) * cdiv(W, 2);
+  if (dtype == EDET_BF16 && Cout % 16 == 0 && px > 0) {
+    const int OH = cdiv(H, 2), OW = cdiv(W, 2);
+    const int R = std::max(1, std::min(8, 512 / OW));
+    const size_t lds = std::max((size_t)(2 * R + 1) * cdiv(W * 3, 8) * 8 * 2 + (size_t)R * OW * (Cout + 8) * 2,
+                                (size_t)4 * 32 * Cout * 4);
+    const int grid = std::min(B * cdiv(OH, R), 512);
+    float* part = workspace_f32((size_t)grid * 27 * Cout);
+    if (part && lds <= 96 * 1024) {
+      const uint16_t* xb = (const uint16_t*)x;
+      const uint16_t* db = (const uint16_t*)dy;
+      hipStream_t st = (hipStream_t)stream;
+      switch (Cout / 16) {
+        case 1: hipLaunchKernelGGL(k_stem2_wgrad<1>, dim3(grid), dim3(256), lds, st, xb, B, H, W, db, Cout, part, R); break;
+        case 2: hipLaunchKernelGGL(k_stem2_wgrad<2>, dim3(grid), dim3(256), lds, st, xb, B, H, W, db, Cout, part, R); break;
+        case 3: hipLaunchKernelGGL(k_stem2_wgrad<3>, dim3(grid), dim3(256), lds, st, xb, B, H, W, db, Cout, part, R); break;
+        default: hipLaunchKernelGGL(k_stem2_wgrad<4>, dim3(grid), dim3(256), lds, st, xb, B, H, W, db, Cout, part, R); break;
+      }
+      int rc = check_launch("edet stem2_wgrad");
+      if (rc) return rc;
+      return sum_partials(part, grid, 27L * Cout, dw, st);
+    }
+  }
   long per = (px + 2047) / 2048;  // latency-bound: 512 blocks measured 1.4x slower
   per = ((per + 63) / 64) * 64;
   if (per < 64) per = 64;

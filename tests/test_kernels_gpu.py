@@ -350,9 +350,10 @@ def test_residual(dt):
 
 
 @pytest.mark.parametrize("dt", DTS)
-def test_stem(dt, workspace_mode):
+@pytest.mark.parametrize("shape", [(2, 21, 18, 32), (3, 34, 40, 48), (2, 64, 64, 32)])
+def test_stem(dt, shape, workspace_mode):
     rng = np.random.default_rng(9)
-    B, H, W, Co = 2, 21, 18, 32
+    B, H, W, Co = shape
     x = g(torch.rand(B, H, W, 3), dt)
     w = g(rnd(rng, 3, 3, 3, Co, scale=0.3), dt)
     OH, OW = (H + 1) // 2, (W + 1) // 2
