@@ -321,6 +321,7 @@ def main():
     ap.add_argument("--graph", type=int, default=1)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--kernel-timing", type=int, default=1)
+    ap.add_argument("--overlap", type=int, default=0, help="weight gradients on a side stream")
     args = ap.parse_args()
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -343,6 +344,7 @@ def main():
                                  world_size=world, grad_allreduce=ar, npos_allreduce=ar,
                                  lr_schedule={"warmup_steps": 100, "total_steps": 10000,
                                               "adjusted_lr": 0.08 * B * world / 64})
+    model.eng.overlap = bool(args.overlap)
     x, t = synthetic_batch(anchors, B, S, 1000 + rank, dev, model.eng.tdtype)
     data = (x, t)
     log(f"[bench] {args.model} B={B}/gpu world={world} dtype={args.dtype} params={model.P.n_trainable}")
@@ -398,8 +400,10 @@ def main():
         if ctx.distributed:
             model.grad_allreduce = None
             model.npos_allreduce = None
+        model.eng.overlap = False  # per-kernel attribution: one stream, no concurrency
         with KernelTimer(es) as kt:
             model.train_step(data)
+        model.eng.overlap = bool(args.overlap)
         agg = kt.summary()
         if os.environ.get("EDET_KERNEL_DETAIL"):
             kt.detail(os.environ["EDET_KERNEL_DETAIL"])

@@ -40,6 +40,7 @@ def main():
     anchors = Anchors(cfg.min_level, cfg.max_level, (S, S), cfg.num_scales, cfg.aspect_ratios, cfg.anchor_scale, device=dev)
     model = EfficientDetNetTrain(efficientnet_b0_blocks(), cfg, anchors, dtype="bf16", device=dev, seed=0,
                                  lr_schedule={"warmup_steps": 100, "total_steps": 10000})
+    model.eng.overlap = False  # isolated replays
     x, t = bench.synthetic_batch(anchors, B, S, 1000, dev, model.eng.tdtype)
     model.train_step((x, t))
     torch.cuda.synchronize()

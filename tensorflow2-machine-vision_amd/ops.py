@@ -88,7 +88,8 @@ def stem(eng: Engine, P: ParamStore, x: torch.Tensor, wname: str, bn: BNParam) -
             return
         d, ld = value_grad_to_raw(eng, out, rec)
         assert ld == Cout
-        L.call("edet_stem_wgrad", eng.dt, vp(x), B, H, W, vp(d), Cout, vp(P.grad(wname)), stream())
+        with eng.side(x, d):
+            L.call("edet_stem_wgrad", eng.dt, vp(x), B, H, W, vp(d), Cout, vp(P.grad(wname)), stream())
 
     eng.record(bwd)
     return out
@@ -112,9 +113,10 @@ def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optio
         if rec is None:
             return
         d, ld = value_grad_to_raw(eng, out, rec)
+        with eng.side(x.raw, x.gate, d):
+            L.call("edet_conv1x1_wgrad", eng.dt, x.lazy(), x.pyr.c, K, vp(d), ld, N, vp(P.grad(wname)),
+                   vp(P.grad(bname) if bname else None), stream())
         s = stream()
-        L.call("edet_conv1x1_wgrad", eng.dt, x.lazy(), x.pyr.c, K, vp(d), ld, N, vp(P.grad(wname)),
-               vp(P.grad(bname) if bname else None), s)
         dx, acc = eng.tape.dst(x)
         L.call("edet_conv1x1_dgrad", eng.dt, vp(d), ld, x.pyr.c, N, vp(P.wtv(wname)), K, vp(dx), K, acc, s)
 
@@ -138,8 +140,10 @@ def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
             return
         d, ld = value_grad_to_raw(eng, out, rec)
         assert ld == C
+        with eng.side(x.raw, x.gate, d):
+            L.call("edet_dwconv_wgrad", eng.dt, x.lazy(), x.pyr.c, C, k, stride, vp(d), pout.c, vp(P.grad(wname)),
+                   stream())
         s = stream()
-        L.call("edet_dwconv_wgrad", eng.dt, x.lazy(), x.pyr.c, C, k, stride, vp(d), pout.c, vp(P.grad(wname)), s)
         dx, acc = eng.tape.dst(x)
         L.call("edet_dwconv_dgrad", eng.dt, vp(d), pout.c, C, k, stride, vp(P.wcv(wname)), vp(dx), x.pyr.c, acc, s)
 

@@ -425,6 +425,7 @@ class Tape:
         for fn in reversed(entries):
             fn()
         self.g.clear()
+        self.eng.join_side()
 
 
 # --------------------------------------------------------------------------- engine
@@ -470,6 +471,16 @@ class Engine:
         self._s64_need = 1 << 20
         self._s64_hw = 0  # high-water mark over all steps: the extent the memset must cover
         self._s64_overflow = []
+        # Optional: weight gradients on a side stream (off the backward critical path: nothing
+        # in the step reads them before the optimizer).  Tensors they read stay referenced
+        # until join_side() orders the main stream after them, so the caching allocator cannot
+        # hand their memory to a main-stream op while a side kernel may still read it.  Off by
+        # default: measured 1351 vs 1388 img/s (D0 b32) -- the wide side kernels take the CUs
+        # the main chain needs instead of filling idle ones.
+        self.overlap = False
+        self._side = None
+        self._side_used = False
+        self._side_keep: list = []
 
     def empty(self, rows: int, C: int, dtype=None) -> torch.Tensor:
         return torch.empty((rows, C), dtype=dtype or self.tdtype, device=self.device)
@@ -506,6 +517,26 @@ class Engine:
     def record(self, fn):
         if self.training and self.tape is not None:
             self.tape.record(fn)
+
+    def side(self, *keep):
+        """Context for a weight-gradient launch: the side stream after the main stream's work
+        so far (or the main stream itself when overlap is off)."""
+        import contextlib
+        if not self.overlap:
+            return contextlib.nullcontext()
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        self._side_keep.extend(keep)
+        self._side_used = True
+        return torch.cuda.stream(self._side)
+
+    def join_side(self):
+        """Order the main stream after every side-stream launch; release their operands."""
+        if self._side_used:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            self._side_used = False
+        self._side_keep.clear()
 
 
 def memset0(t: torch.Tensor):
