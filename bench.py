@@ -80,6 +80,8 @@ def algorithmic_bytes(name, args, es):
     if name == "edet_dwconv_dgrad":
         pout, C, pin, acc = args[2], args[3], args[8], args[9]
         return (rows(pout) + rows(pin) * (1 + acc)) * C * es
+    if name == "edet_lazy_materialize":
+        return 2 * rows(args[2]) * args[3] * es
     if name == "edet_lazy_bwd_reduce":
         return 2 * rows(args[2]) * args[3] * es
     if name == "edet_lazy_bwd_apply":
@@ -117,7 +119,7 @@ def shape_tag(name, args):
             return f"in={rows(args[2])} C={args[3]} k={args[4]} s={args[5]}"
         if name == "edet_dwconv_dgrad":
             return f"out={rows(args[2])} C={args[3]} k={args[4]} s={args[5]}"
-        if name in ("edet_lazy_bwd_reduce", "edet_lazy_bwd_apply"):
+        if name in ("edet_lazy_bwd_reduce", "edet_lazy_bwd_apply", "edet_lazy_materialize"):
             return f"M={rows(args[2])} C={args[3]} {lazy(args[1])}"
     except Exception:  # noqa: BLE001
         pass

@@ -202,6 +202,12 @@ int edet_se_bwd(int B, int C, int R, int HW, const double* s, const float* z1,
                 float* dw1, float* db1, float* dw2, float* db2, float* dsq, float* dz1,
                 edet_stream_t stream); /* dz1: [B][R] scratch; weight grads accumulate (+=) */
 
+/* ---- out[rows][C] = v(x) = act(bn(x)) * gate: the SE-gated depthwise output written once for
+ * the MBConv project conv (mb_conv_block.py:150-154), whose forward GEMM and weight gradient
+ * both read it ---- */
+int edet_lazy_materialize(int dtype, const edet_lazy* x, const edet_pyramid* p, int C, void* out,
+                          edet_stream_t stream);
+
 /* ---- heads: out = v(x) * scale[seg][n] + v(res) (drop-connect + residual) ---- */
 int edet_residual_fwd(int dtype, const edet_lazy* x, const edet_lazy* res,
                       const edet_pyramid* p, int C, const float* scale, void* out,

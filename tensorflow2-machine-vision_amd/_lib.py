@@ -94,6 +94,7 @@ SIGNATURES = {
     "edet_gate_grad": [c_int, PLazy, c_int, c_int, c_int, P, P, P],
     "edet_se_bwd": [c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "edet_residual_fwd": [c_int, PLazy, PLazy, PPyr, c_int, P, P, P],
+    "edet_lazy_materialize": [c_int, PLazy, PPyr, c_int, P, P],
     "edet_maxpool_fwd": [c_int, PLazy, c_int, c_int, c_int, c_int, P, P],
     "edet_maxpool_bwd": [c_int, PLazy, c_int, c_int, c_int, c_int, P, P, c_int, P],
     "edet_bifpn_fuse_fwd": [c_int, c_int, PFuse, P, c_int, c_int, c_int, c_int, P, P],

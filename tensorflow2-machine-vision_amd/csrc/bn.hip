@@ -412,6 +412,48 @@ __global__ __launch_bounds__(256) void k_residual(LArgs g) {
   }
 }
 
+// out = v(x) = act(bn(x)) * gate, written once.  Used for the SE-gated depthwise output that
+// both the project conv's forward GEMM and its weight gradient read: applying the transform in
+// their A-operand loads cost more than this extra pass (it was recomputed per column tile).
+template <typename T>
+__global__ __launch_bounds__(256) void k_materialize(LArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int C = g.C;
+  float2* ax = reinterpret_cast<float2*>(smem);
+  const RowGeom geo = g.geo;
+  const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
+  int seg, chunk;
+  chunk_lookup(g.p, geo.CH, blockIdx.x, seg, chunk);
+  const int rows = seg_rows(g.p, seg);
+  load_tables(g.lz, seg, 1.f / (float)rows, C, ax, nullptr, nullptr, nullptr);
+  __syncthreads();
+  if (rr >= geo.R) return;
+  const int off = g.p.row_off[seg];
+  const int m_begin = off + chunk * geo.CH, m_end = min(off + rows, m_begin + geo.CH);
+  const int hw = g.p.H[seg] * g.p.W[seg];
+  const int NV = C / 8;
+  T* OUT = (T*)g.dx;
+  for (int m = m_begin + rr; m < m_end; m += geo.R) {
+    const int n = (m - off) / hw;
+#pragma unroll
+    for (int v = 0; v < RVPT; ++v) {
+      const int cv = tv + v * geo.TPR;
+      if (v < geo.VPT && cv < NV) {
+        const int c = cv * 8;
+        float x[8], gt[8];
+        ld8((const T*)g.lz.x + (size_t)m * g.lz.ld + c, x);
+        if (g.lz.gate) ld8(g.lz.gate + (size_t)n * C + c, gt);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          x[j] = lazy_apply(x[j], ax[c + j], g.lz.act);
+          if (g.lz.gate) x[j] *= gt[j];
+        }
+        st8(OUT + (size_t)m * C + c, x);
+      }
+    }
+  }
+}
+
 // Keras BatchNormalization moving statistics: m -= (m - batch) * (1 - momentum), with the
 // Bessel-corrected batch variance that FusedBatchNormV3 returns in training mode.
 __global__ void k_bn_update(int64_t n, const double* sum, const double* sq, const float* count,
@@ -562,6 +604,22 @@ int edet_residual_fwd(int dtype, const edet_lazy* x, const edet_lazy* res,
   EDET_DTYPE_DISPATCH(dtype, T, {
     if (nb) hipLaunchKernelGGL(k_residual<T>, dim3(nb), row_block(g.geo), lds, (hipStream_t)stream, g);
     return check_launch("edet residual");
+  });
+}
+
+int edet_lazy_materialize(int dtype, const edet_lazy* x, const edet_pyramid* p, int C, void* out,
+                          edet_stream_t stream) {
+  int rc = lazy_checks(x, p, C);
+  if (rc) return rc;
+  EDET_REQUIRE(out, "lazy_materialize: null out");
+  LArgs g{};
+  g.lz = *x; g.p = *p; g.dx = out; g.C = C;
+  g.geo = row_geom(C);
+  const int nb = total_chunks(*p, g.geo.CH);
+  const size_t lds = C * sizeof(float2);
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    if (nb) hipLaunchKernelGGL(k_materialize<T>, dim3(nb), row_block(g.geo), lds, (hipStream_t)stream, g);
+    return check_launch("edet lazy_materialize");
   });
 }
 

@@ -56,6 +56,8 @@ class EfficientDetNet:
         self.P.finalize(self.eng.device, self.eng.tdtype, seed)
         self._count_batch = None
         self.last_outputs = None
+        # SE-gated depthwise outputs written once before the project conv (ops.materialize)
+        self.materialize_se = True
 
     # ------------------------------------------------------------------ parameters
     def _register(self):
@@ -261,6 +263,8 @@ class EfficientDetNet:
         d = ops.dwconv(eng, P, x, f"{pre}/depthwise_conv2d/depthwise_kernel", sp.kernel_size, sp.stride,
                        bns=[b["bn1"]], act=L.ACT_SWISH, name=f"{pre}/dw")
         ops.squeeze_excite(eng, P, d, f"{pre}/se", sp.se_filters)
+        if self.materialize_se:
+            d = ops.materialize(eng, d, name=f"{pre}/se_out")
         return ops.conv1x1(eng, P, d, b["project_w"], sp.output_filters, bns=[b["bn2"]], name=f"{pre}/project")
 
     def backbone(self, x: torch.Tensor, training: bool) -> List[Act]:

@@ -171,6 +171,24 @@ def squeeze_excite(eng: Engine, P: ParamStore, x: Act, prefix: str, R: int):
     return x
 
 
+def materialize(eng: Engine, x: Act, name: str = "") -> Act:
+    """Write v(x) once as a plain tensor (same bf16 rounding the GEMM A-operand staging
+    applies, so the consumer's inputs are unchanged).  Backward: the gradient of the plain copy
+    IS the gradient of x's value, handed to x's own backward as is."""
+    y = eng.empty(x.pyr.rows, x.C)
+    L.call("edet_lazy_materialize", eng.dt, x.lazy(), x.pyr.c, x.C, vp(y), stream())
+    out = Act(y, x.pyr, x.C, training=eng.training, name=name)
+
+    def bwd():
+        rec = eng.tape.take(out)
+        if rec is None:
+            return
+        eng.tape.alias(x, rec.t, rec.ld, rec.scale)
+
+    eng.record(bwd)
+    return out
+
+
 # --------------------------------------------------------------------------- resampling
 def maxpool(eng: Engine, x: Act, name: str = "") -> Act:
     assert x.pyr.nseg == 1

@@ -331,6 +331,23 @@ def test_bifpn_fuse(dt):
 
 
 @pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("kind", ["gate", "pyramid"])
+def test_lazy_materialize(dt, kind):
+    rng = np.random.default_rng(31)
+    C = 48
+    pyr = Pyr(3, [(5, 7)]) if kind == "gate" else Pyr(2, [(4, 4), (2, 2)])
+    x = g(rnd(rng, pyr.rows, C), dt)
+    gate = g(torch.rand(pyr.batch, C), "f32") if kind == "gate" else None
+    lz = LazyDesc(x, pyr, C, bn=make_bn(x, pyr, C, rng), act=1, gate=gate)
+    out = torch.full((pyr.rows, C), float("nan"), dtype=TDT[dt], device=DEV)
+    L.call("edet_lazy_materialize", DT[dt], lz.c, pyr.c, C, vp(out), stream())
+    ref = lz.cpu_value()
+    for s in range(pyr.nseg):
+        sl = pyr.seg_slice(s)
+        close(out[sl], ref[sl], dt)
+
+
+@pytest.mark.parametrize("dt", DTS)
 def test_residual(dt):
     rng = np.random.default_rng(3)
     pyr = Pyr(2, [(8, 8), (4, 4)])
