@@ -173,10 +173,21 @@ __global__ __launch_bounds__(256) void k_loss(LossArgs g) {
   }
 }
 
+// 16 mask bytes per thread and step, few blocks: the count ends in one same-address atomic
+// per block (exact: integer-valued floats far below 2^24)
 __global__ void k_count_pos(const uint8_t* mask, int64_t n, float* out) {
   __shared__ float red[4];
   float s = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+  const int64_t nv = n / 16;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (int64_t)gridDim.x * 256) {
+    const uint4 v = reinterpret_cast<const uint4*>(mask)[i];
+    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) s += ((w4[k] >> (8 * b)) & 0xffu) ? 1.f : 0.f;
+  }
+  for (int64_t i = nv * 16 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     s += mask[i] ? 1.f : 0.f;
   s = block_sum(s, red);
   if (threadIdx.x == 0) atomicAdd(out, s);
@@ -223,8 +234,10 @@ int edet_detection_loss(int dtype, const void* cls, int ldc, const void* box, in
 int edet_count_positives(const uint8_t* mask, int64_t n, float* out, edet_stream_t stream) {
   EDET_REQUIRE(mask && out, "count_positives: null argument");
   if (n <= 0) return EDET_OK;
-  int nb = (int)((n + 255) / 256);
-  if (nb > 1024) nb = 1024;
+  EDET_REQUIRE(((uintptr_t)mask & 15) == 0, "count_positives: mask must be 16-byte aligned");
+  int nb = (int)((n / 16 + 255) / 256);
+  if (nb > 64) nb = 64;
+  if (nb < 1) nb = 1;
   hipLaunchKernelGGL(k_count_pos, dim3(nb), dim3(256), 0, (hipStream_t)stream, mask, n, out);
   return check_launch("edet count_positives");
 }

@@ -5,6 +5,8 @@
 //   ema -= (1 - d)(ema - w)                           (tfa MovingAverage, train.py:117-119)
 //   lr  = CosineLrSchedule(step)                      (train.py:35-63)
 // plus the fp32 -> compute-dtype weight cast, drop-connect masks and device step counter.
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace edet {
@@ -136,7 +138,10 @@ int edet_opt_norm(const float* w, const float* g, int64_t n, int64_t n_l2,
                   const edet_sched* sched, float* scalars, int32_t* step,
                   edet_stream_t stream) {
   EDET_REQUIRE(w && g && sched && scalars && step && n_l2 <= n, "opt_norm: bad argument");
-  hipLaunchKernelGGL(k_opt_norm, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, w, g, n, n_l2, *sched,
+  // 256 blocks: every block ends in two same-address float atomics, and 2048 of them
+  // serialised in L2 for ~40 us
+  const int nb = std::min(grid_for(n), 256);
+  hipLaunchKernelGGL(k_opt_norm, dim3(nb), dim3(256), 0, (hipStream_t)stream, w, g, n, n_l2, *sched,
                      scalars, step);
   return check_launch("edet opt_norm");
 }
