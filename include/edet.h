@@ -252,6 +252,19 @@ int edet_generate_targets(const float* anchors, const edet_pyramid* p, int A,
 int edet_decode_boxes(int dtype, const float* anchors, const edet_pyramid* p, int A,
                       const void* rel, int ld, float* out, edet_stream_t stream);
 
+/* Detection post-processing of a batch (the test_step / inference path): per image, the
+ * anchors whose first-argmax class over the NC logits is not class 0 and whose max logit is
+ * >= score_thr, greedy DIoU-NMS in descending logit order (ties: lower flat index) with
+ * suppression at DIoU >= iou_thr, at most max_out kept; scores returned as sigmoid(logit).
+ * boxes: decoded [rows][A][4] fp32 (edet_decode_boxes); cls: logits [rows][ldc] in dtype,
+ * channel a*NC + c; scratch: batch * N * 8 bytes with N = sum_l H_l*W_l*A.
+ * Outputs [batch][max_out][4], [batch][max_out], [batch][max_out], [batch].
+ * Replaces Anchors.convert_outputs_one (anchors.py:161-202) + get_nms (nms.py:5-61). */
+int edet_detect_nms(int dtype, const float* boxes, const void* cls, int ldc, const edet_pyramid* p, int A,
+                    int NC, int max_out, float iou_thr, float score_thr, void* scratch,
+                    float* out_boxes, int32_t* out_cls, float* out_scores, int32_t* out_count,
+                    edet_stream_t stream);
+
 /* ---- optimizer: L2 + clip_by_global_norm + SGD momentum + EMA, fused ----
  * scalars: [0] loss  [1] sum g^2  [2] sum w^2 (L2 params)  [3] gnorm  [4] lr  [5] npos
  * step: device int32 step counter (incremented by edet_opt_apply). */

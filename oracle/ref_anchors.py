@@ -8,6 +8,8 @@ without FMA contraction, like TF's CPU kernels):
   generate_targets anchors.py:91-138   (argmax first-max, >= threshold, encode, one-hot)
   encode           anchors.py:219-243
   decode           anchors.py:245-274
+  get_nms          nms.py:5-61         (sort + boolean_mask greedy loop, DIoU)
+  convert_outputs_one anchors.py:161-202
 """
 from __future__ import annotations
 
@@ -91,9 +93,14 @@ def diou(b1, b2):
     ey2 = np.maximum(b1[..., 2], b2[..., 2]); ex2 = np.maximum(b1[..., 3], b2[..., 3])
     c1 = np.stack([(b1[..., 0] + b1[..., 2]) / f32(2), (b1[..., 1] + b1[..., 3]) / f32(2)], -1)
     c2 = np.stack([(b2[..., 0] + b2[..., 2]) / f32(2), (b2[..., 1] + b2[..., 3]) / f32(2)], -1)
-    e2 = np.sum((c2 - c1) ** 2, -1)
-    d2 = (ey2 - ey1) ** 2 + (ex2 - ex1) ** 2
-    return (v - np.where(d2 == 0, f32(0), e2 / np.where(d2 == 0, f32(1), d2))).astype(f32)
+    # iou.py:91-96: tf.linalg.norm = sqrt(sum of squares), then **2
+    e = np.sqrt(np.sum((c2 - c1) * (c2 - c1), -1, dtype=f32))
+    diag = np.stack([ey2 - ey1, ex2 - ex1], -1)
+    d = np.sqrt(np.sum(diag * diag, -1, dtype=f32))
+    e2, d2 = e * e, d * d
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = np.where(d2 == 0, f32(0), e2 / np.where(d2 == 0, f32(1), d2))
+    return (v - r).astype(f32)
 
 
 def _center_size(b):
@@ -153,3 +160,47 @@ def generate_targets(anchor_levels, boxes, classes, classes_num, iou_threshold=0
         om.append(mask[..., None])
         oi.append(cls.astype(np.int32))
     return ob, oc, om, oi
+
+
+def get_nms(boxes, scores, max_output_size, iou_threshold=0.5, score_threshold=float("-inf")):
+    """nms.py:5-61, literally: indices sorted by descending score (tf.argsort DESCENDING: ties
+    keep the lower index first), then repeatedly keep the head and drop the rest whose DIoU
+    with it is >= iou_threshold; stop at max_output_size, an empty list or a head score below
+    score_threshold."""
+    boxes = np.asarray(boxes, f32)
+    scores = np.asarray(scores, f32)
+    order = np.argsort(-scores, kind="stable")
+    boxes_sort, idxs = boxes[order], order
+    result = []
+    while True:
+        if len(result) >= max_output_size or len(idxs) == 0:
+            break
+        top = idxs[0]
+        if scores[top] < f32(score_threshold):
+            break
+        result.append(int(top))
+        if len(idxs) == 1:
+            break
+        keep = diou(boxes_sort[0:1], boxes_sort[1:]) < f32(iou_threshold)
+        boxes_sort, idxs = boxes_sort[1:][keep], idxs[1:][keep]
+    return np.asarray(result, np.int64)
+
+
+def convert_outputs_one(level_boxes, level_logits, max_output_size=200, iou_threshold=0.5,
+                        score_threshold=0.0001):
+    """anchors.py:161-202 for one image: per level argmax class / max logit over [H,W,A],
+    drop class 0, concatenate levels, DIoU-NMS on the logits, sigmoid of the kept scores.
+    level_boxes: decoded [H,W,A,4]; level_logits: [H,W,A,NC]."""
+    nb, nc, ns = [], [], []
+    for b, lg in zip(level_boxes, level_logits):
+        lg = np.asarray(lg, f32).reshape(-1, np.shape(lg)[-1])
+        cid = np.argmax(lg, -1)
+        sc = np.max(lg, -1)
+        m = cid != 0
+        nb.append(np.asarray(b, f32).reshape(-1, 4)[m])
+        nc.append(cid[m])
+        ns.append(sc[m])
+    nb, nc, ns = np.concatenate(nb), np.concatenate(nc), np.concatenate(ns)
+    idx = get_nms(nb, ns, max_output_size, iou_threshold, score_threshold)
+    s = ns[idx]
+    return nb[idx], nc[idx], (f32(1) / (f32(1) + np.exp(-s))).astype(f32)

@@ -106,6 +106,7 @@ SIGNATURES = {
     "edet_anchor_boxes": [c_int, c_int, c_float, c_float, c_float, c_float, c_int, P, P, P],
     "edet_generate_targets": [P, PPyr, c_int, P, P, P, c_int, c_float, P, P, P, P],
     "edet_decode_boxes": [c_int, P, PPyr, c_int, P, c_int, P, P],
+    "edet_detect_nms": [c_int, P, P, c_int, PPyr, c_int, c_int, c_int, c_float, c_float, P, P, P, P, P, P],
     "edet_opt_norm": [P, P, c_int64, c_int64, PSched, P, P, P],
     "edet_opt_apply": [P, P, P, P, c_int64, c_int64, PSched, P, c_int, P, P],
     "edet_cast_f32": [c_int, P, P, c_int64, P],

@@ -35,6 +35,22 @@ def anchor_half_sizes(image_size, feat_sizes, level, num_scales, aspect_ratios, 
     return stride, np.asarray(halves, np.float32)
 
 
+def _pyramid_base(levels, pyr: Pyr):
+    """(base pointer, row stride in elements, dtype code) of per-level [B,H,W,A,k] views that
+    share one pyramid buffer [rows][ld] (what EfficientDetNet.call and convert_outputs_boxes
+    return)."""
+    lv = levels[0]
+    # row stride from the first dimension of size > 1 (torch reports nominal strides for
+    # size-1 dimensions, e.g. the 1x1 top level)
+    ld = lv.stride(2) if lv.shape[2] > 1 else lv.stride(1) if lv.shape[1] > 1 else lv.stride(0)
+    for s, v in enumerate(levels):  # the views must really be segments of one buffer
+        assert v.untyped_storage().data_ptr() == lv.untyped_storage().data_ptr()
+        assert v.storage_offset() - lv.storage_offset() == (pyr.row_off[s] - pyr.row_off[0]) * ld
+    base = lv.untyped_storage().data_ptr()
+    ptr = base + (lv.storage_offset() - pyr.row_off[0] * ld) * lv.element_size()
+    return ptr, ld, (L.BF16 if lv.dtype == torch.bfloat16 else L.F32)
+
+
 class Targets:
     """Compact training targets in pyramid row layout (rows = the heads' pyramid rows)."""
 
@@ -152,13 +168,8 @@ class Anchors:
         pyramid buffer (as returned by EfficientDetNet.call) or a raw [rows, ld] buffer."""
         A = self.get_anchors_per_location()
         if isinstance(outputs_boxes, (tuple, list)):
-            lv = outputs_boxes[0]
-            B = lv.shape[0]
-            pyr = pyr or self.pyramid(B)
-            base = lv.untyped_storage().data_ptr()
-            raw_ptr = base + (lv.storage_offset() - pyr.row_off[0] * lv.stride(2)) * lv.element_size()
-            ld = lv.stride(2)
-            dt = L.BF16 if lv.dtype == torch.bfloat16 else L.F32
+            pyr = pyr or self.pyramid(outputs_boxes[0].shape[0])
+            raw_ptr, ld, dt = _pyramid_base(outputs_boxes, pyr)
         else:
             raw_ptr = outputs_boxes.data_ptr()
             dt = L.BF16 if outputs_boxes.dtype == torch.bfloat16 else L.F32
@@ -168,3 +179,36 @@ class Anchors:
         for s, (fh, fw) in enumerate(self.level_sizes):
             res.append(out[pyr.seg_slice(s)].view(pyr.batch, fh, fw, A, 4))
         return tuple(res)
+
+    def detect(self, outputs_boxes, outputs_classes, max_output_size: int = 200, iou_threshold: float = 0.5,
+               score_threshold: float = 0.0001):
+        """convert_outputs_one (anchors.py:161-202 + nms.py:5-61) for every image of the batch,
+        one GPU launch: first-argmax class != 0, DIoU-NMS on the logits, sigmoid scores.
+
+        outputs_boxes: decoded per-level boxes (convert_outputs_boxes); outputs_classes:
+        per-level logits [B,H,W,A,NC] as returned by EfficientDetNet.call.  Returns
+        (boxes [B,max,4], class ids [B,max], scores [B,max], counts [B]); rows past counts[b]
+        are unspecified."""
+        B = outputs_classes[0].shape[0]
+        NC = outputs_classes[0].shape[-1]
+        A = self.get_anchors_per_location()
+        pyr = self.pyramid(B)
+        bptr, bld, bdt = _pyramid_base(outputs_boxes, pyr)
+        assert bdt == L.F32 and bld == 4 * A, "outputs_boxes must be decoded fp32 boxes"
+        cptr, cld, cdt = _pyramid_base(outputs_classes, pyr)
+        N = sum(h * w for h, w in self.level_sizes) * A
+        dev = self.device
+        scratch = torch.empty(2 * B * N, dtype=torch.float32, device=dev)
+        ob = torch.empty((B, max_output_size, 4), dtype=torch.float32, device=dev)
+        oc = torch.empty((B, max_output_size), dtype=torch.int32, device=dev)
+        os_ = torch.empty((B, max_output_size), dtype=torch.float32, device=dev)
+        cnt = torch.empty(B, dtype=torch.int32, device=dev)
+        L.call("edet_detect_nms", cdt, bptr, cptr, cld, pyr.c, A, NC, max_output_size, float(iou_threshold),
+               float(score_threshold), vp(scratch), vp(ob), vp(oc), vp(os_), vp(cnt), stream())
+        return ob, oc, os_, cnt
+
+    def convert_outputs_one(self, batch_index: int, outputs_boxes, outputs_classes):
+        """anchors.py:161-202 signature: (boxes [k,4], class ids [k], scores [k]) of one image."""
+        ob, oc, os_, cnt = self.detect(outputs_boxes, outputs_classes)
+        k = int(cnt[batch_index])
+        return ob[batch_index, :k], oc[batch_index, :k].long(), os_[batch_index, :k]

@@ -528,6 +528,43 @@ class EfficientDetNetTrain(EfficientDetNet):
         L.call("edet_bn_update_moving", P.n_bn, vp(P.bn_tstats[0]), vp(P.bn_tstats[1]), vp(P.bn_count),
                float(cfg.batch_norm_momentum), vp(P.bn_mm), vp(P.bn_mv), s)
 
+    def test_step(self, data):
+        """test_step (efficientdet_net_train.py:135-169): inference-mode forward, the same loss
+        (forward only), decode + DIoU-NMS per image on the GPU, and the reference's per-image
+        mAP (host numpy, metrics.py) averaged over the batch.
+
+        data = (x, gt_boxes [B,G,4], gt_classes [B,G], y_true_boxes[5], y_true_classes[5],
+        y_true_masks[5]); each image's G ground-truth rows are scored as given, like the
+        reference's numpy_function call."""
+        from . import metrics
+        x, real_boxes, real_classes, yb, yc, ym = data
+        boxes_out, classes_out = self.call(x, training=False)
+        cls, box, pyr = self.last_outputs
+        t = Targets.from_reference(yb, yc, ym, pyr, self.A, self.eng.device)
+        s = stream()
+        sc = torch.zeros(8, dtype=torch.float32, device=self.eng.device)
+        parts = torch.zeros(2 * L.MAX_SEG, dtype=torch.float32, device=self.eng.device)
+        for seg in range(pyr.nseg):
+            sl = pyr.seg_slice(seg)
+            L.call("edet_count_positives", vp(t.mask[sl]), pyr.seg_rows(seg) * self.A, vp(sc[5:6]), s)
+        L.call("edet_detection_loss", self.eng.dt, vp(cls.raw), cls.ld, vp(box.raw), box.ld, pyr.c, self.A, self.NC,
+               vp(t.cls), vp(t.box), vp(sc[5:6]), float(self.cfg.alpha), float(self.cfg.gamma), 0.1, 50.0, 1.0,
+               None, None, vp(sc[0:1]), vp(parts), s)
+        P = self.P  # _reg_l2_loss (efficientdet_net_train.py:21-28): the L2 prefix of the flat weights
+        l2 = 4e-5 * 0.5 * float((P.w[: P.n_l2].double() ** 2).sum())
+        loss = float(sc[0]) + l2
+        ob, oc, os_, cnt = self.anchors.detect(self.anchors.convert_outputs_boxes(boxes_out), classes_out)
+        ob, oc, os_, cnt = ob.cpu().numpy(), oc.cpu().numpy(), os_.cpu().numpy(), cnt.cpu().numpy()
+        rb = np.asarray(real_boxes.cpu() if isinstance(real_boxes, torch.Tensor) else real_boxes, np.float64)
+        rc = np.asarray(real_classes.cpu() if isinstance(real_classes, torch.Tensor) else real_classes, np.float64)
+        m = 0.0
+        for b in range(x.shape[0]):
+            k = int(cnt[b])
+            pred = np.concatenate([ob[b, :k], oc[b, :k, None], os_[b, :k, None]], -1)
+            gt = np.concatenate([rb[b], rc[b][:, None]], -1)
+            m += metrics.get_map_one(gt, pred, self.NC, 0.5)
+        return {"loss": loss, "mAP": m / x.shape[0]}
+
     def train_step(self, data):
         """train_step_normal (efficientdet_net_train.py:112-132)."""
         self.forward_backward(data)

@@ -74,3 +74,46 @@ def test_reference_format_roundtrip():
                                     torch.tensor([1, 2]), 3)
     assert bool(om[0][4, 4, 0, 0]) and oc[0][4, 4, 0].tolist() == [0, 1, 0]
     assert ob[0][4, 4, 0].abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize("dt,size,NC", [("f32", 128, 5), ("bf16", 128, 5), ("f32", 256, 81)])
+def test_detect_nms_matches_oracle(dt, size, NC):
+    """§8(f) row 2: convert_outputs_one + DIoU-NMS (anchors.py:161-202, nms.py:5-61) on the GPU.
+    Kept boxes, their order and class ids bit-exact with the oracle's literal sort/boolean_mask
+    loop on the same decoded boxes and logits; scores (sigmoid) within 2 ulp."""
+    from tf2mv_amd.runtime import Pyr
+    rng = np.random.default_rng(size + NC)
+    a = Anchors(3, 7, (size, size), 3, ASPECTS, 4.0, device="cuda")
+    A, B = 9, 3
+    pyr = a.pyramid(B)
+    tdt = torch.float32 if dt == "f32" else torch.bfloat16
+    ld_b, ld_c = A * 4, A * NC + 7  # an unaligned logits stride, like inference's A*NC
+    rel = torch.zeros(pyr.rows, ld_b)
+    logits = torch.zeros(pyr.rows, ld_c)
+    for s in range(pyr.nseg):
+        sl = pyr.seg_slice(s)
+        n = pyr.seg_rows(s)
+        rel[sl] = torch.tensor(rng.normal(0, 0.3, (n, ld_b)), dtype=torch.float32)
+        # logits with exact ties and many background winners
+        lg = np.round(rng.normal(0, 2, (n, ld_c)) * 4) / 4
+        logits[sl] = torch.tensor(lg, dtype=torch.float32)
+    rel_g, log_g = rel.to("cuda", tdt), logits.to("cuda", tdt)
+    box_levels, cls_levels = [], []
+    for s, (fh, fw) in enumerate(a.level_sizes):
+        sl = pyr.seg_slice(s)
+        box_levels.append(rel_g[sl].view(B, fh, fw, A, 4))
+        cls_levels.append(log_g[sl, : A * NC].view(B, fh, fw, A, NC))
+    dec = a.convert_outputs_boxes(tuple(box_levels))
+    ob, oc, os_, cnt = a.detect(dec, tuple(cls_levels))
+    torch.cuda.synchronize()
+    for b in range(B):
+        rb, rc, rs = RA.convert_outputs_one([d[b].cpu().numpy() for d in dec],
+                                            [c[b].float().cpu().numpy() for c in cls_levels])
+        k = int(cnt[b])
+        assert k == len(rb) and k > 0
+        np.testing.assert_array_equal(ob[b, :k].cpu().numpy(), rb)
+        np.testing.assert_array_equal(oc[b, :k].cpu().numpy(), rc)
+        np.testing.assert_allclose(os_[b, :k].cpu().numpy(), rs, rtol=3e-7, atol=0)
+    # the single-image API of the reference
+    bb, cc, ss = a.convert_outputs_one(1, dec, tuple(cls_levels))
+    assert bb.shape[0] == int(cnt[1])

@@ -271,3 +271,33 @@ def test_forward_is_reproducible(dtype):
         assert float(((st - outs[0][0]).abs() / (outs[0][0].abs() + 1e-30)).max()) < 1e-12
         assert torch.allclose(parts[:5], outs[0][1][:5], rtol=1e-6, atol=0)
         assert float((g - outs[0][2]).norm()) <= 1e-4 * float(outs[0][2].norm())
+
+
+def test_test_step_loss_and_map():
+    """test_step (efficientdet_net_train.py:135-169): inference-mode loss (with the L2 term)
+    within 1e-4 of the oracle; the per-image mAP is the reference's metric on the GPU
+    detections, recomputed here from the oracle NMS over the GPU's own outputs."""
+    from oracle import ref_anchors as RA
+    from tf2mv_amd import metrics
+    m, anchors = _train_model("f32")
+    x, boxes, cls, n = synth(4)
+    t, yb, yc, ym = make_targets(m, anchors, boxes, cls, n)
+    data = (torch.tensor(x).cuda(), torch.tensor(boxes), torch.tensor(cls),
+            [torch.tensor(v) for v in yb], [torch.tensor(v) for v in yc], [torch.tensor(v) for v in ym])
+    out = m.test_step(data)
+    ref = RefEfficientDet(m, m.state_dict())
+    with torch.no_grad():
+        rb, rc = ref.forward(x, False)
+        rloss, _ = ref.detection_loss(rb, rc, yb, yc, ym)
+    assert abs(out["loss"] - float(rloss)) / float(rloss) < 1e-4, (out["loss"], float(rloss))
+    # the detections behind the mAP: oracle NMS on the GPU's decoded boxes and logits
+    bo, co = m.call(torch.tensor(x).cuda(), training=False)
+    dec = anchors.convert_outputs_boxes(bo)
+    want = 0.0
+    for b in range(B):
+        pb, pc, ps = RA.convert_outputs_one([d[b].cpu().numpy() for d in dec], [c[b].float().cpu().numpy() for c in co])
+        pred = np.concatenate([pb, pc[:, None], ps[:, None]], -1)
+        gt = np.concatenate([boxes[b], cls[b][:, None]], -1)
+        want += metrics.get_map_one(gt, pred, NC, 0.5)
+    assert 0.0 <= out["mAP"] <= 1.0
+    assert out["mAP"] == pytest.approx(want / B, abs=1e-12)

@@ -43,3 +43,26 @@ def test_encode_decode_roundtrip():
     g = a + rng.uniform(-2, 2, a.shape).astype(f32)
     g[:, 2:] = np.maximum(g[:, 2:], g[:, :2] + 1)
     np.testing.assert_allclose(RA.decode(a, RA.encode(a, g)), g, rtol=0, atol=1e-3)
+
+
+def test_nms_oracle_greedy_diou():
+    # three overlapping boxes around (10,10), one far away; scores are logits
+    boxes = np.array([[0, 0, 10, 10], [1, 1, 11, 11], [30, 30, 40, 40], [0, 0, 10, 10.5]], f32)
+    scores = np.array([0.5, 0.9, 0.7, 0.9], f32)
+    # order by score desc, ties by index: 1, 3, 2, 0.  Box 1 suppresses 3 (DIoU >= 0.5) and 0.
+    assert RA.diou(boxes[1:2], boxes[3:4])[0] >= 0.5 and RA.diou(boxes[1:2], boxes[0:1])[0] >= 0.5
+    np.testing.assert_array_equal(RA.get_nms(boxes, scores, 200, 0.5, 1e-4), [1, 2])
+    np.testing.assert_array_equal(RA.get_nms(boxes, scores, 1, 0.5, 1e-4), [1])
+    # score threshold on the logits: nothing at or above 1.0
+    assert RA.get_nms(boxes, scores, 200, 0.5, 1.0).size == 0
+
+
+def test_convert_outputs_one_drops_background():
+    boxes = [np.arange(2 * 2 * 1 * 4, dtype=f32).reshape(2, 2, 1, 4) * f32(10)]
+    lg = np.full((2, 2, 1, 3), -5, f32)
+    lg[0, 0, 0] = [3, 1, 0]     # background wins: dropped
+    lg[0, 1, 0] = [0, 2, 1]     # class 1, logit 2
+    lg[1, 1, 0] = [0, 1, 1]     # tie between classes 1 and 2: first max (1)
+    b, c, s = RA.convert_outputs_one(boxes, [lg])
+    np.testing.assert_array_equal(c, [1, 1])
+    np.testing.assert_allclose(s, 1 / (1 + np.exp(-np.array([2.0, 1.0]))), rtol=1e-6)
