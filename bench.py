@@ -312,6 +312,50 @@ def cpu_baseline(model, seconds=12.0):
                       f"(torch-CPU restatement of the reference TF2 semantics), {el:.1f} s"}
 
 
+def bench_backbone(args):
+    """BASELINE config 2: EfficientNet-B0 backbone forward (inference BN), 224x224, one GPU,
+    B = --batch (64 for the config).  Same timing contract as the train step."""
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    from tf2mv_amd import dist as dp
+    from tf2mv_amd.config import efficientnet_b0_blocks, get_efficientdet_config
+    from tf2mv_amd.model import EfficientDetNet
+
+    ctx = dp.init_from_env("nccl", dev)
+    world, rank = ctx.world, ctx.rank
+    cfg = get_efficientdet_config("efficientdet-d0", {"image_size": 224})
+    B = args.batch
+    model = EfficientDetNet(efficientnet_b0_blocks(), cfg, dtype=args.dtype, device=dev, seed=0)
+    rng = np.random.default_rng(1000 + rank)
+    x = torch.tensor(rng.random((B, 224, 224, 3), dtype=np.float32), device=dev).to(model.eng.tdtype)
+    for _ in range(2):
+        model.backbone(x, training=False)
+    torch.cuda.synchronize()
+    step = lambda: model.backbone(x, training=False)  # noqa: E731
+    if args.graph:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            model.backbone(x, training=False)
+        step = g.replay
+    for _ in range(args.warmup):
+        step()
+    el = dp.timed(ctx, step, args.steps, torch.cuda.synchronize)
+    el = dp.max_over_ranks(ctx, el, dev)
+    value = world * B * args.steps / el
+    log(f"[bench] backbone B0@224 B={B}/gpu: {args.steps} steps in {el:.3f}s -> {value:.1f} img/s")
+    if rank == 0:
+        print(json.dumps({
+            "metric": "EfficientNet-B0 backbone forward images/sec", "value": round(value, 2), "unit": "images/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic",
+            "config": {"workload": f"efficientnet-b0 backbone forward 224x224, B={B}/GPU, inference BN",
+                       "model": "efficientnet-b0", "global_batch": B * world, "image_size": 224,
+                       "parallelism": f"dp{world}", "graph": bool(args.graph)}}), flush=True)
+    dp.shutdown(ctx)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -324,7 +368,11 @@ def main():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--kernel-timing", type=int, default=1)
     ap.add_argument("--overlap", type=int, default=0, help="weight gradients on a side stream")
+    ap.add_argument("--workload", default="train", choices=["train", "backbone"],
+                    help="train: the headline D0 train step; backbone: BASELINE config 2 (B0 @224 forward)")
     args = ap.parse_args()
+    if args.workload == "backbone":
+        return bench_backbone(args)
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)

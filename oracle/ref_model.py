@@ -197,6 +197,17 @@ class RefEfficientDet:
             out.append(c.permute(0, 2, 3, 1).reshape(B, H, W, self.m.A, last))
         return out
 
+    def backbone(self, x_nhwc, training, st: Optional[BNState] = None):
+        """BackboneModel.call (backbone_model.py:96-148): [features, reduction_1..5], NHWC."""
+        x = torch.as_tensor(np.asarray(x_nhwc), dtype=self.dtype).permute(0, 3, 1, 2)
+        x = self.stem(x, training, st)
+        reds = []
+        for i in range(len(self.m.specs)):
+            x = self.mbconv(x, i, training, st)
+            if i in self.m.red_idx:
+                reds.append(x)
+        return [t.permute(0, 2, 3, 1) for t in [x] + reds]
+
     def forward(self, x_nhwc, training, masks=None, st: Optional[BNState] = None):
         """EfficientDetNet.call: returns (boxes list, classes list) NHWC [B,H,W,A,*]."""
         x = torch.as_tensor(np.asarray(x_nhwc), dtype=self.dtype).permute(0, 3, 1, 2)

@@ -767,6 +767,14 @@ static int launch_dw(int which, DwArgs g, hipStream_t s) {
   // gains on the large stride-2 and wide-channel layers
   if (which == 0 && ((K == 3 && S == 2 && g.C >= 192) || (S == 1 && g.C >= 144 && g.C <= 240)))
     return launch_dw3<T, K, S, false>(g, s);
+  // the direct forms keep one row of C/8 threads per block (C <= 2048); wider channel counts
+  // (EfficientDet-D4+ last stages, C = 2688) take the channel-blocked tile kernels
+  if (g.C > 2048 && which == 0) return launch_dw3<T, K, S, false>(g, s);
+  if (g.C > 2048 && which == 1) {
+    g.tiles_total = host_tiles(g.pin);
+    if (g.tiles_total) hipLaunchKernelGGL((k_dw_dgrad<T, K, S>), dim3(g.tiles_total * g.ncb), dim3(256), 0, s, g);
+    return check_launch("edet dwconv");
+  }
   if (which == 2 && S == 1 && (g.C <= 64 || (K == 5 && g.C == 240))) return launch_dw3<T, K, S, true>(g, s);
   // forward: the LDS tile kernel applies the producer's lazy BN/swish/gate once per input
   // element; the direct form re-evaluates it per tap (K*K times) and only wins at k3 s2.
@@ -836,7 +844,7 @@ int edet_dwconv_fwd(int dtype, const edet_lazy* x, const edet_pyramid* pin, int 
                     int stride, const void* w, void* y, const edet_pyramid* pout,
                     const edet_statout* stats, edet_stream_t stream) {
   EDET_REQUIRE(x && w && y, "dwconv_fwd: null argument");
-  EDET_REQUIRE(C % 8 == 0 && C <= 2048 && x->ld % 8 == 0, "dwconv_fwd: need C%%8==0, C<=2048, ld%%8==0");
+  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0, "dwconv_fwd: need C%%8==0, ld%%8==0");
   int rc = check_pyrs(pin, pout, k, stride);
   if (rc) return rc;
   DwArgs g{};
@@ -850,7 +858,7 @@ int edet_dwconv_dgrad(int dtype, const void* dy, const edet_pyramid* pout, int C
                       int stride, const void* w, void* dx, const edet_pyramid* pin,
                       int accumulate, edet_stream_t stream) {
   EDET_REQUIRE(dy && w && dx, "dwconv_dgrad: null argument");
-  EDET_REQUIRE(C % 8 == 0 && C <= 2048, "dwconv_dgrad: need C%%8==0 and C<=2048");
+  EDET_REQUIRE(C % 8 == 0, "dwconv_dgrad: need C%%8==0");
   int rc = check_pyrs(pin, pout, k, stride);
   if (rc) return rc;
   DwArgs g{};

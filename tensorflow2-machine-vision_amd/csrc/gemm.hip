@@ -1291,8 +1291,9 @@ static int dispatch_gemm_kloop(GemmArgs g, hipStream_t s) {
     if (NP <= 192) return launch_gemm<T, 64, 192, LAZY>(g, s);
     if (NP <= 320) return launch_gemm<T, 64, 320, LAZY>(g, s);
   }
-  set_error("gemm: K=%d > 512 needs N <= 320 (N=%d)", g.K, g.N);
-  return EDET_EUNSUPPORTED;
+  // wider outputs (EfficientDet-D4+ project convs: K = 1632 -> N = 448): 128-column tiles
+  if (cdiv(g.M, 64) < 512) return launch_gemm<T, 32, 128, LAZY>(g, s);
+  return launch_gemm<T, 64, 128, LAZY>(g, s);
 }
 
 template <typename T, bool LAZY>

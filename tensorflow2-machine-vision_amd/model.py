@@ -267,8 +267,30 @@ class EfficientDetNet:
             d = ops.materialize(eng, d, name=f"{pre}/se_out")
         return ops.conv1x1(eng, P, d, b["project_w"], sp.output_filters, bns=[b["bn2"]], name=f"{pre}/project")
 
-    def backbone(self, x: torch.Tensor, training: bool) -> List[Act]:
-        """BackboneModel.call: returns [features, reduction_1, ..., reduction_5]."""
+    def backbone(self, inputs, training: bool = False) -> List[torch.Tensor]:
+        """BackboneModel.call (backbone_model.py:96-148): [features, reduction_1..5] as
+        [B, H, W, C] tensors in the compute dtype (the normalised, activated block outputs)."""
+        if training:
+            memset0(self.P.bn_tstats)
+        self.eng.tape = None
+        x = self._prepare_input(inputs)
+        B = x.shape[0]
+        self._set_counts(B)
+        self.eng.begin_scratch()
+        self.eng.training = training
+        if not training:
+            L.call("edet_bn_inference_stats", self.P.n_bn, vp(self.P.bn_mm), vp(self.P.bn_mv), vp(self.P.bn_count),
+                   vp(self.P.bn_istats[0]), vp(self.P.bn_istats[1]), stream())
+        acts = self._backbone_acts(x, training)
+        outs = []
+        for a in acts:
+            y = ops.materialize(self.eng, a).raw
+            outs.append(y[: a.pyr.rows].view(B, a.pyr.H, a.pyr.W, a.C))
+        self.eng.training = False
+        return outs
+
+    def _backbone_acts(self, x: torch.Tensor, training: bool) -> List[Act]:
+        """Backbone as lazy activations: [features, reduction_1, ..., reduction_5]."""
         eng = self.eng
         out = ops.stem(eng, self.P, x, f"{self.bb}/stem/conv2d/kernel", self.stem_bn)
         reds = []
@@ -348,7 +370,7 @@ class EfficientDetNet:
         if not training:
             L.call("edet_bn_inference_stats", P.n_bn, vp(P.bn_mm), vp(P.bn_mv), vp(P.bn_count),
                    vp(P.bn_istats[0]), vp(P.bn_istats[1]), stream())
-        all_feats = self.backbone(x, training)
+        all_feats = self._backbone_acts(x, training)
         feats = [all_feats[l] for l in self.levels if l < len(all_feats)]
         for l in self.levels:
             if l < len(all_feats):

@@ -301,3 +301,32 @@ def test_test_step_loss_and_map():
         want += metrics.get_map_one(gt, pred, NC, 0.5)
     assert 0.0 <= out["mAP"] <= 1.0
     assert out["mAP"] == pytest.approx(want / B, abs=1e-12)
+
+
+@pytest.mark.parametrize("training", [False, True])
+def test_backbone_b0_224_parity_fp32(training):
+    """BASELINE config 2's path (EfficientNet-B0 backbone at 224x224): BackboneModel.call's
+    [features, reduction_1..5] within 1e-3 relative of the oracle."""
+    c = get_efficientdet_config("efficientdet-d0", {"image_size": 224, "num_classes": NC})
+    m = EfficientDetNet(efficientnet_b0_blocks(), c, dtype="f32", seed=5)
+    x = np.random.default_rng(5).random((2, 224, 224, 3), dtype=np.float32)
+    outs = m.backbone(torch.tensor(x).cuda(), training=training)
+    ref = RefEfficientDet(m, m.state_dict()).backbone(x, training)
+    assert [tuple(o.shape) for o in outs] == [(2, 7, 7, 320), (2, 112, 112, 16), (2, 56, 56, 24), (2, 28, 28, 40),
+                                               (2, 14, 14, 112), (2, 7, 7, 320)]
+    for o, r in zip(outs, ref):
+        assert rel_err(o.cpu(), r) < 1e-3
+
+
+def test_d4_topology_forward_parity_fp32():
+    """BASELINE config 5's model (EfficientDet-D4: width 1.4, depth 1.8, 224-channel BiFPN x 7
+    cells, 4 head repeats) at a reduced 256x256 input, inference mode, vs the oracle."""
+    c = get_efficientdet_config("efficientdet-d4", {"image_size": 256, "num_classes": NC, "survival_prob": None})
+    m = EfficientDetNet(efficientnet_b0_blocks(), c, dtype="f32", seed=6)
+    assert len(m.specs) == 32 and m.F == 224 and len(m.cells) == 7
+    x = np.random.default_rng(6).random((1, 256, 256, 3), dtype=np.float32)
+    boxes, classes = m.call(torch.tensor(x).cuda(), training=False)
+    rb, rc = RefEfficientDet(m, m.state_dict()).forward(x, False)
+    for l in range(5):
+        assert rel_err(boxes[l].cpu(), rb[l].detach()) < 1e-3, l
+        assert rel_err(classes[l].cpu(), rc[l].detach()) < 1e-3, l
