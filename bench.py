@@ -491,7 +491,7 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "EfficientDet-D0 bf16 train-step images/sec",
+            "metric": f"EfficientDet-{args.model.split('-')[-1].upper()} bf16 train-step images/sec",
             "value": round(value, 2),
             "unit": "images/s",
             "n_gpus": world,
@@ -503,7 +503,7 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic",
-            "config": {"workload": f"{args.model} full train step 512x512, B={B}/GPU, focal+Huber loss, SGD+EMA",
+            "config": {"workload": f"{args.model} full train step {S}x{S}, B={B}/GPU, focal+Huber loss, SGD+EMA",
                        "model": args.model, "global_batch": B * world, "image_size": S,
                        "parallelism": f"dp{world}", "graph": bool(args.graph)},
             "loss": round(loss, 5),
