@@ -197,6 +197,16 @@ int edet_se_fwd(int B, int C, int R, const double* s, const float* w1, const flo
 /* dgate += sum_hw dv * v(x) into a zeroed fp64 [B][C] (feeds dx through se_bwd -> dsq) */
 int edet_gate_grad(int dtype, const edet_lazy* x, int B, int HW, int C, const void* dv,
                    double* dgate, edet_stream_t stream);
+/* SE-gated BN value v = swish(bn(x)) * gate: one pass over (x, dv) giving, per image and
+ * channel, sums5[q][n][c] (fp64, accumulated) for q = 0: dv*swish(u) (the gate gradient),
+ * 1: dv*swish'(u), 2: swish'(u), 3: dv*swish'(u)*xhat, 4: swish'(u)*xhat; then
+ * edet_se_bn_combine folds gate and dsq in: dbeta += sum_n gate*[1] + dsq*[2], dgamma +=
+ * sum_n gate*[3] + dsq*[4] -- the edet_lazy_bwd_reduce result, without its pass over x, dv.
+ * (layers/se.py:35-39 + mb_conv_block.py:147-150 backward; C <= 2048.) */
+int edet_gate_bn_reduce(int dtype, const edet_lazy* x, int B, int HW, int C, const void* dv,
+                        double* sums5, edet_stream_t stream);
+int edet_se_bn_combine(int B, int C, const float* gate, const float* dsq, const double* sums5,
+                       const edet_bngrad64* acc, edet_stream_t stream);
 int edet_se_bwd(int B, int C, int R, int HW, const double* s, const float* z1,
                 const float* gate, const double* dgate, const float* w1, const float* w2,
                 float* dw1, float* db1, float* dw2, float* db2, float* dsq, float* dz1,

@@ -92,6 +92,8 @@ SIGNATURES = {
     "edet_se_squeeze": [c_int, PLazy, c_int, c_int, c_int, P, P],
     "edet_se_fwd": [c_int, c_int, c_int, P, P, P, P, P, P, P, P],
     "edet_gate_grad": [c_int, PLazy, c_int, c_int, c_int, P, P, P],
+    "edet_gate_bn_reduce": [c_int, PLazy, c_int, c_int, c_int, P, P, P],
+    "edet_se_bn_combine": [c_int, c_int, P, P, P, PBnG, P],
     "edet_se_bwd": [c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "edet_residual_fwd": [c_int, PLazy, PLazy, PPyr, c_int, P, P, P],
     "edet_lazy_materialize": [c_int, PLazy, PPyr, c_int, P, P],

@@ -274,6 +274,83 @@ __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
   }
 }
 
+// SE-gated value v = swish(u) * gate, u = bn(x): one pass over (x, dv) yields, per image and
+// channel, everything the SE backward and the BN backward reduction need:
+//   [0] sum dv*swish(u)             -> d gate (the gate gradient, as k_img_reduce<T, true>)
+//   [1] sum dv*swish'(u)  [2] sum swish'(u)  [3] sum dv*swish'(u)*xhat  [4] sum swish'(u)*xhat
+// Since du = (dv*gate + dsq) * swish'(u) with gate and dsq constant per (image, channel),
+//   dbeta = sum_n gate*[1] + dsq*[2],  dgamma = sum_n gate*[3] + dsq*[4]   (k_se_bn_combine)
+// which replaces the separate k_lazy_bwd_reduce pass over x and dv for these tensors.
+template <typename T>
+__global__ __launch_bounds__(256) void k_gate_bn_reduce(LArgs g) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int C = g.C;
+  float2* af = reinterpret_cast<float2*>(smem);
+  float2* mr = af + C;
+  float* red = reinterpret_cast<float*>(mr + C);  // [R][C] per quantity, reused 5 times
+  const RowGeom geo = g.geo;
+  const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
+  const int n = blockIdx.x / g.chunks_per_img, chunk = blockIdx.x - n * g.chunks_per_img;
+  load_tables(g.lz, 0, 1.f / (float)seg_rows(g.p, 0), C, af, mr, nullptr, nullptr);
+  __syncthreads();
+  const int m_begin = n * g.hw + chunk * geo.CH, m_end = min((n + 1) * g.hw, m_begin + geo.CH);
+  const int c = tv * 8;
+  const bool live = rr < geo.R && tv < C / 8;
+  float a[5][8];
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[q][j] = 0.f;
+  if (live) {
+    for (int m = m_begin + rr; m < m_end; m += geo.R) {
+      float x[8], d[8];
+      ld8((const T*)g.lz.x + (size_t)m * g.lz.ld + c, x);
+      ld8((const T*)g.dv + (size_t)m * C + c, d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float2 t = af[c + j], b = mr[c + j];
+        const float u = x[j] * t.x + t.y;
+        const float sg = sigmoidf_(u);
+        const float sw = u * sg, dsw = sg * (1.f + u * (1.f - sg));
+        const float xh = (x[j] - b.x) * b.y;
+        a[0][j] += d[j] * sw;
+        a[1][j] += d[j] * dsw;
+        a[2][j] += dsw;
+        a[3][j] += d[j] * dsw * xh;
+        a[4][j] += dsw * xh;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    __syncthreads();
+    if (live)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[rr * C + c + j] = a[q][j];
+    __syncthreads();
+    for (int cc = tid; cc < C; cc += blockDim.x) {
+      float ss = 0.f;
+      for (int i = 0; i < geo.R; ++i) ss += red[i * C + cc];
+      atomicAdd(g.out64 + ((size_t)q * g.p.batch + n) * C + cc, (double)ss);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_se_bn_combine(int B, int C, const float* gate, const float* dsq,
+                                                       const double* s5, double* dgamma, double* dbeta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double gb = 0.0, gg = 0.0;
+  for (int n = 0; n < B; ++n) {
+    const double gt = gate[(size_t)n * C + c], ds = dsq[(size_t)n * C + c];
+    const size_t i = (size_t)n * C + c, BC = (size_t)B * C;
+    gb += gt * s5[1 * BC + i] + ds * s5[2 * BC + i];
+    gg += gt * s5[3 * BC + i] + ds * s5[4 * BC + i];
+  }
+  dbeta[c] += gb;
+  dgamma[c] += gg;
+}
+
 // SE excite: z1 = W1 s + b1 ; gate = sigmoid(W2 swish(z1) + b2)   (layers/se.py:36-39).
 // The excite is tiny (B x C x R MACs) but was one block per image; it is now spread over the
 // chip: one wave per (n, r) dot product over C, then one thread per (n, c) over R.  Every
@@ -562,6 +639,33 @@ int edet_se_squeeze(int dtype, const edet_lazy* x, int B, int HW, int C, double*
 int edet_gate_grad(int dtype, const edet_lazy* x, int B, int HW, int C, const void* dv,
                    double* dgate, edet_stream_t stream) {
   return img_reduce(dtype, true, x, B, HW, C, dv, dgate, (hipStream_t)stream);
+}
+
+int edet_gate_bn_reduce(int dtype, const edet_lazy* x, int B, int HW, int C, const void* dv,
+                        double* sums5, edet_stream_t stream) {
+  EDET_REQUIRE(x && x->x && dv && sums5, "gate_bn_reduce: null argument");
+  EDET_REQUIRE(x->bn.enabled && x->act == EDET_ACT_SWISH, "gate_bn_reduce: needs bn + swish");
+  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0 && C <= 2048, "gate_bn_reduce: need C%%8==0, C<=2048");
+  LArgs g{};
+  g.lz = *x; g.lz.gate = nullptr;
+  g.p.nseg = 1; g.p.batch = B; g.p.row_off[0] = 0; g.p.H[0] = HW; g.p.W[0] = 1;
+  g.dv = dv; g.out64 = sums5; g.C = C; g.hw = HW;
+  g.geo = row_geom(C);
+  g.chunks_per_img = cdiv(HW, g.geo.CH);
+  const int nb = B * g.chunks_per_img;
+  const size_t lds = 2 * C * sizeof(float2) + (size_t)g.geo.R * C * sizeof(float);
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    hipLaunchKernelGGL(k_gate_bn_reduce<T>, dim3(nb), row_block(g.geo), lds, (hipStream_t)stream, g);
+    return check_launch("edet gate_bn_reduce");
+  });
+}
+
+int edet_se_bn_combine(int B, int C, const float* gate, const float* dsq, const double* sums5,
+                       const edet_bngrad64* acc, edet_stream_t stream) {
+  EDET_REQUIRE(gate && dsq && sums5 && acc && acc->dgamma[0] && acc->dbeta[0], "se_bn_combine: null argument");
+  hipLaunchKernelGGL(k_se_bn_combine, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, B, C, gate, dsq, sums5,
+                     acc->dgamma[0], acc->dbeta[0]);
+  return check_launch("edet se_bn_combine");
 }
 
 int edet_se_fwd(int B, int C, int R, const double* s, const float* w1, const float* b1,

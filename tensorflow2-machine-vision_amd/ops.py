@@ -42,12 +42,22 @@ def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor
     s = stream()
     lz = out.lazy()
     dsq = None
+    # SE-gated swish(BN) value: the gate gradient and the BN-backward sums come out of one
+    # pass over (x, dv) (edet_gate_bn_reduce); no separate reduce pass
+    fused_se = (out.se is not None and out.bns is not None and len(out.bns) == 1 and out.act == L.ACT_SWISH
+                and rec.scale is None and out.C <= 2048)
+    sums5 = None
     if out.se is not None:
         se = out.se
         B = out.pyr.batch
         HW = out.pyr.H * out.pyr.W
-        dgate = eng.zeros64(B, out.C)
-        L.call("edet_gate_grad", eng.dt, lz, B, HW, out.C, vp(rec.t), vp(dgate), s)
+        if fused_se:
+            sums5 = eng.zeros64(5, B, out.C)
+            L.call("edet_gate_bn_reduce", eng.dt, lz, B, HW, out.C, vp(rec.t), vp(sums5), s)
+            dgate = sums5[0]
+        else:
+            dgate = eng.zeros64(B, out.C)
+            L.call("edet_gate_grad", eng.dt, lz, B, HW, out.C, vp(rec.t), vp(dgate), s)
         dsq = torch.empty((B, out.C), dtype=torch.float32, device=eng.device)
         dz1 = torch.empty((B, se.R), dtype=torch.float32, device=eng.device)
         L.call("edet_se_bwd", B, out.C, se.R, HW, vp(se.s), vp(se.z1), vp(se.gate), vp(dgate),
@@ -60,7 +70,10 @@ def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor
         acc = L.BnGrad64()
         for i in range(len(out.bns)):
             acc.dgamma[i], acc.dbeta[i] = acc_t[0, i].data_ptr(), acc_t[1, i].data_ptr()
-        L.call("edet_lazy_bwd_reduce", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, s)
+        if fused_se:
+            L.call("edet_se_bn_combine", out.pyr.batch, out.C, vp(out.gate), vp(dsq), vp(sums5), acc, s)
+        else:
+            L.call("edet_lazy_bwd_reduce", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, s)
     dx = eng.empty(out.pyr.rows, out.C)
     L.call("edet_lazy_bwd_apply", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, grads,
            vp(dx), 0, s)

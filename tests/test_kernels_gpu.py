@@ -539,3 +539,33 @@ def test_transpose_cast(dt):
         got = dst[o: o + k * ldn].view(k, ldn).float().cpu()
         close(got[:, :n], w.t(), dt)
         assert float(got[:, n:].abs().max() if ldn > n else 0) == 0.0
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("C,HW", [(48, 9 * 10), (144, 23 * 17)])
+def test_gate_bn_reduce_equals_separate_passes(dt, C, HW):
+    """edet_gate_bn_reduce + edet_se_bn_combine (one pass) == edet_gate_grad + se_bwd's dsq +
+    edet_lazy_bwd_reduce (two passes) on an SE-gated swish(BN) value."""
+    rng = np.random.default_rng(C + HW)
+    B = 3
+    pyr = Pyr(B, [(HW, 1)])
+    x = pyr_data(rng, pyr, C, dt, scale=2.0)
+    bn = make_bn(x, pyr, C, rng)
+    gt = g(torch.rand(B, C) + 0.5, "f32")
+    lz = LazyDesc(x, pyr, C, bn=bn, act=1, gate=gt)
+    dv = pyr_data(rng, pyr, C, dt)
+    dsq = g(rnd(rng, B, C) * 0.1, "f32")
+    # two-pass reference path
+    dg = zeros64(B, C)
+    L.call("edet_gate_grad", DT[dt], lz.c, B, HW, C, vp(dv), vp(dg), stream())
+    acc_t, acc = bngrad64(1, C)
+    L.call("edet_lazy_bwd_reduce", DT[dt], lz.c, pyr.c, C, vp(dv), None, vp(dsq), acc, stream())
+    # fused
+    s5 = zeros64(5, B, C)
+    L.call("edet_gate_bn_reduce", DT[dt], lz.c, B, HW, C, vp(dv), vp(s5), stream())
+    acc2_t, acc2 = bngrad64(1, C)
+    L.call("edet_se_bn_combine", B, C, vp(gt), vp(dsq), vp(s5), acc2, stream())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(s5[0], dg, rtol=1e-5, atol=1e-6)
+    scale = float(acc_t.abs().max())
+    torch.testing.assert_close(acc2_t, acc_t, rtol=1e-4, atol=1e-5 * scale)
