@@ -51,31 +51,63 @@ static int host_tiles(const edet_pyramid& p) {
   return t;
 }
 
-// Stage the transformed input halo of one tile into LDS (fp32, [IH][IW][DCB]).
+// Stage the transformed input halo of one tile into LDS (fp32, [IH][IW][DCB]) in two halves so
+// the loads are all in flight together: fetch issues every raw vector of the tile into
+// registers with select-predicated addresses (a load wrapped in a divergent `if` is waited on
+// inside it, one latency per vector), commit transforms them into LDS once the tile's affine
+// and gate are in LDS.
 template <typename T, int IH, int IW>
-__device__ __forceinline__ void stage_input(const DwArgs& g, float* tile, const float2* xf, const float* gt,
-                                            int seg, int n, int iy0, int ix0, int c0) {
-  const int H = g.pin.H[seg], W = g.pin.W[seg], C = g.C;
-  const T* X = (const T*)g.x;
-  const size_t base = (size_t)g.pin.row_off[seg] + (size_t)n * H * W;
-  for (int v = threadIdx.x; v < IH * IW * (DCB / 8); v += 256) {
-    const int pix = v >> 2, cv = (v & 3) * 8;
-    const int yy = pix / IW, xx = pix - yy * IW;
-    const int gy = iy0 + yy, gx = ix0 + xx, nc = C - (c0 + cv);
-    float vals[8];
-    if (gy >= 0 && gy < H && gx >= 0 && gx < W && nc > 0) {
-      ld8m(X + (base + (size_t)gy * W + gx) * g.lz.ld + c0 + cv, nc, vals);
+struct Stage {
+  static constexpr int NV = (IH * IW * (DCB / 8) + 255) / 256;
+  static constexpr int WORDS = sizeof(T) == 2 ? 1 : 2;
+  uint4 raw[NV][WORDS];
+  uint32_t ok;
+  __device__ __forceinline__ void fetch(const DwArgs& g, int seg, int n, int iy0, int ix0, int c0) {
+    const int H = g.pin.H[seg], W = g.pin.W[seg];
+    const T* X = (const T*)g.x + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * g.lz.ld + c0;
+    ok = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) vals[j] = (j < nc) ? lazy_apply(vals[j], xf[cv + j], g.lz.act) * gt[cv + j] : 0.f;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) vals[j] = 0.f;
+    for (int u = 0; u < NV; ++u) {
+      const int v = threadIdx.x + u * 256;
+      const int pix = v >> 2, cv = (v & 3) * 8;
+      const int yy = pix / IW, xx = pix - yy * IW;
+      const int gy = iy0 + yy, gx = ix0 + xx;
+      const bool in = v < IH * IW * 4 && gy >= 0 && gy < H && gx >= 0 && gx < W && c0 + cv < g.C;
+      const uint4* src = reinterpret_cast<const uint4*>(X + (in ? (uint32_t)(gy * W + gx) * g.lz.ld + cv : 0u));
+      raw[u][0] = src[0];
+      if constexpr (WORDS == 2) raw[u][1] = src[1];
+      ok |= (uint32_t)in << u;
     }
-    float* d = tile + pix * DCB + cv;
-    reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
-    reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
   }
-}
+  __device__ __forceinline__ void commit(const DwArgs& g, float* tile, const float2* xf, const float* gt) const {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int v = threadIdx.x + u * 256;
+      if (v >= IH * IW * 4) break;
+      const int pix = v >> 2, cv = (v & 3) * 8;
+      float vals[8];
+      if constexpr (WORDS == 1) {
+        const uint32_t w4[4] = {raw[u][0].x, raw[u][0].y, raw[u][0].z, raw[u][0].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          vals[2 * i] = __uint_as_float(w4[i] << 16);
+          vals[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+        }
+      } else {
+        const uint32_t w8[8] = {raw[u][0].x, raw[u][0].y, raw[u][0].z, raw[u][0].w,
+                                raw[u][1].x, raw[u][1].y, raw[u][1].z, raw[u][1].w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vals[i] = __uint_as_float(w8[i]);
+      }
+      const bool in = (ok >> u) & 1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vals[j] = in ? lazy_apply(vals[j], xf[cv + j], g.lz.act) * gt[cv + j] : 0.f;
+      float* d = tile + pix * DCB + cv;
+      reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
+      reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+    }
+  }
+};
 
 __device__ __forceinline__ void prep_xf(const DwArgs& g, float2* xf, float* gt, int seg, int n, int c0) {
   const int tid = threadIdx.x;
@@ -139,9 +171,11 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
       q = 0.f;
       cur_seg = seg;
     }
+    Stage<T, IH, IW> st;
+    st.fetch(g, seg, n, oy0 * S - pt, ox0 * S - pl, c0);
     prep_xf(g, xf, gt, seg, n, c0);
     __syncthreads();
-    stage_input<T, IH, IW>(g, tile, xf, gt, seg, n, oy0 * S - pt, ox0 * S - pl, c0);
+    st.commit(g, tile, xf, gt);
     __syncthreads();
 
     float acc[DTS];
@@ -306,9 +340,11 @@ __global__ __launch_bounds__(256) void k_dw_wgrad(DwArgs g) {
     const int pt = same_pad(H, K, S), pl = same_pad(W, K, S);
     const int oy0 = ty * DTS, ox0 = tx * DTS;
     __syncthreads();
+    Stage<T, IH, IW> st;
+    st.fetch(g, seg, n, oy0 * S - pt, ox0 * S - pl, c0);
     prep_xf(g, xf, gt, seg, n, c0);
     __syncthreads();
-    stage_input<T, IH, IW>(g, lds, xf, gt, seg, n, oy0 * S - pt, ox0 * S - pl, c0);
+    st.commit(g, lds, xf, gt);
     const int oy = oy0 + r;
     const size_t obase = (size_t)g.pout.row_off[seg] + (size_t)n * OH * OW;
     float dyv[DTS];
@@ -747,6 +783,132 @@ __global__ __launch_bounds__(256) void k_dw2_dgrad(DwArgs g, DwGeom geo) {
   }
 }
 
+// ------------------------------------------------------------------ register-blocked dgrad
+// One thread = one PH x PW patch of dx pixels x CPT channels; the K*K weights of its channels
+// live in registers as fp32 for the whole launch.  Patches start on u = iy + pt multiples of S,
+// so which dy pixel pairs with which (dx pixel, tap) is known at compile time:
+//   dy row = A + (e - kh) / S  for (e - kh) % S == 0   (A = patch row / S, e = row in patch)
+// Every dy vector the patch needs is loaded and unpacked once and feeds all its taps (k3 s2:
+// 4 loads for 4 dx pixels, against 9 tap loads + 9 weight loads per pixel in k_dw2_dgrad).
+template <int CPT, typename T> __device__ __forceinline__ void ldv(const T* p, float* o) {
+  if constexpr (CPT == 8) {
+    ld8(p, o);
+  } else if constexpr (sizeof(T) == 2) {
+    uint2 v = *reinterpret_cast<const uint2*>(p);
+    o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
+    o[2] = __uint_as_float(v.y << 16); o[3] = __uint_as_float(v.y & 0xffff0000u);
+  } else {
+    float4 a = *reinterpret_cast<const float4*>(p);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  }
+}
+template <int CPT, typename T> __device__ __forceinline__ void stv(T* p, const float* v) {
+  if constexpr (CPT == 8) {
+    st8(p, v);
+  } else if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                                              (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+template <typename T, int K, int S, int CPT, int PH, int PW>
+__global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo) {
+  static_assert(PH % S == 0 && PW % S == 0, "patch must cover whole strides");
+  constexpr int DLO = -((K - 1) / S), DHR = (PH - 1) / S, DHC = (PW - 1) / S;
+  const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
+  if (rr >= geo.R) return;
+  const int c = tv * CPT, C = g.C;
+  const T* DY = (const T*)g.dy;
+  T* DX = (T*)g.dx;
+  float w[K * K][CPT];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) ldv<CPT>((const T*)g.w + (size_t)i * C + c, w[i]);
+  for (int seg = 0; seg < g.pin.nseg; ++seg) {
+    const int OH = g.pout.H[seg], OW = g.pout.W[seg], H = g.pin.H[seg], W = g.pin.W[seg];
+    const int pt = same_pad(H, K, S), pl = same_pad(W, K, S);
+    const int PR = cdiv(H + pt, PH), PC = cdiv(W + pl, PW), per_img = PR * PC;
+    const int npatch = g.pin.batch * per_img;
+    for (int q = blockIdx.x * geo.R + rr; q < npatch; q += gridDim.x * geo.R) {
+      const int n = q / per_img, rem = q - n * per_img;
+      const int pr = rem / PC, pc = rem - pr * PC;
+      const int A = pr * (PH / S), Bc = pc * (PW / S);
+      const T* dyb = DY + ((size_t)g.pout.row_off[seg] + (size_t)n * OH * OW) * C + c;
+      float acc[PH][PW][CPT];
+#pragma unroll
+      for (int e = 0; e < PH; ++e)
+#pragma unroll
+        for (int f = 0; f < PW; ++f)
+#pragma unroll
+          for (int j = 0; j < CPT; ++j) acc[e][f][j] = 0.f;
+      // loads are predicated by select, not branched around: a load inside a divergent `if`
+      // is waited on before the join, which serialises the K*K-ish loads of a k5 patch
+#pragma unroll
+      for (int dr = DLO; dr <= DHR; ++dr) {
+        const int oy = A + dr;
+        const bool rok = oy >= 0 && oy < OH;
+#pragma unroll
+        for (int dc = DLO; dc <= DHC; ++dc) {
+          const int ox = Bc + dc;
+          const bool ok = rok && ox >= 0 && ox < OW;
+          float v[CPT];
+          ldv<CPT>(dyb + (ok ? (uint32_t)((oy * OW + ox) * C) : 0u), v);
+#pragma unroll
+          for (int j = 0; j < CPT; ++j) v[j] = ok ? v[j] : 0.f;
+#pragma unroll
+          for (int e = 0; e < PH; ++e) {
+            const int kh = e - S * dr;
+            if (kh < 0 || kh >= K) continue;
+#pragma unroll
+            for (int f = 0; f < PW; ++f) {
+              const int kw = f - S * dc;
+              if (kw < 0 || kw >= K) continue;
+#pragma unroll
+              for (int j = 0; j < CPT; ++j) acc[e][f][j] += v[j] * w[kh * K + kw][j];
+            }
+          }
+        }
+      }
+      T* dxb = DX + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * C + c;
+#pragma unroll
+      for (int e = 0; e < PH; ++e) {
+        const int iy = pr * PH + e - pt;
+        if (iy < 0 || iy >= H) continue;
+#pragma unroll
+        for (int f = 0; f < PW; ++f) {
+          const int ix = pc * PW + f - pl;
+          if (ix < 0 || ix >= W) continue;
+          T* p = dxb + (uint32_t)((iy * W + ix) * C);
+          if (g.accumulate) {
+            float o[CPT];
+            ldv<CPT>(p, o);
+#pragma unroll
+            for (int j = 0; j < CPT; ++j) acc[e][f][j] += o[j];
+          }
+          stv<CPT>(p, acc[e][f]);
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int K, int S>
+static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s) {
+  constexpr int CPT = K == 3 ? 8 : 4;
+  DwGeom geo;
+  geo.TPR = g.C / CPT;
+  geo.R = std::max(1, 256 / geo.TPR);
+  long patches = 0;
+  for (int i = 0; i < g.pin.nseg; ++i) {
+    const int pt = same_pad(g.pin.H[i], K, S), pl = same_pad(g.pin.W[i], K, S);
+    patches += (long)g.pin.batch * cdiv(g.pin.H[i] + pt, 2) * cdiv(g.pin.W[i] + pl, 2);
+  }
+  const int grid = (int)std::max<long>(1, std::min<long>(4096, (patches + geo.R - 1) / geo.R));
+  if (patches) hipLaunchKernelGGL((k_dw4_dgrad<T, K, S, CPT, 2, 2>), dim3(grid), dim3(geo.TPR * geo.R), 0, s, g, geo);
+  return check_launch("edet dwconv dgrad");
+}
+
 template <typename T, int K, int S, bool WG>
 static int launch_dw3(DwArgs g, hipStream_t s) {
   constexpr int IH = (DTS - 1) * S + K, NPIX = IH * IH;
@@ -759,43 +921,61 @@ static int launch_dw3(DwArgs g, hipStream_t s) {
   return check_launch("edet dwconv3");
 }
 
+// Kernel forms: TILE = k_dw_fwd / k_dw_wgrad / k_dw_dgrad (8x8 LDS tiles), DW3 = k_dw3
+// (pipelined tiles), DIRECT = k_dw2_fwd / k_dw2_dgrad (one pixel per thread), DW4 =
+// k_dw4_dgrad (register-blocked patches).  EDET_DW_FWD / EDET_DW_WGRAD / EDET_DW_DGRAD
+// (0..3) force one form where it applies, for A/B timing (scripts/dw_probe.py).
+enum DwForm { DW_TILE = 0, DW_DW3 = 1, DW_DIRECT = 2, DW_DW4 = 3 };
+
+static int dw_env(const char* name) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : -1;
+}
+
+static DwForm dw_form(int which, int K, int S, int C) {
+  static const int force[3] = {dw_env("EDET_DW_FWD"), dw_env("EDET_DW_DGRAD"), dw_env("EDET_DW_WGRAD")};
+  const bool direct_ok = C <= 2048;
+  const bool dw4_ok = C / (K == 3 ? 8 : 4) <= 256;
+  int f = force[which];
+  if (which == 0) {
+    if (f == DW_TILE || f == DW_DW3 || (f == DW_DIRECT && direct_ok)) return (DwForm)f;
+    // per-shape winners of scripts/dw_probe.py over the D0 b32 layers: the tile form with its
+    // loads all in flight beats the direct form (which re-evaluates the lazy transform per
+    // tap) everywhere; the pipelined tiles win where the double-buffered LDS still leaves
+    // enough blocks per CU, and take C > 2048 (channel-blocked)
+    if ((K == 3 && S == 2 && C >= 192) || (S == 1 && C == 240) || C > 2048) return DW_DW3;
+    return DW_TILE;
+  }
+  if (which == 1) {
+    if (f == DW_TILE || (f == DW_DIRECT && direct_ok) || (f == DW_DW4 && dw4_ok)) return (DwForm)f;
+    if (dw4_ok) return DW_DW4;
+    return direct_ok ? DW_DIRECT : DW_TILE;
+  }
+  if (f == DW_TILE || f == DW_DW3) return (DwForm)f;
+  return (S == 1 && (C <= 64 || (K == 5 && C == 240))) ? DW_DW3 : DW_TILE;
+}
+
 template <typename T, int K, int S>
 static int launch_dw(int which, DwArgs g, hipStream_t s) {
   g.ncb = cdiv(g.C, DCB);
-  // pipelined tile form where it measured faster (scripts/kbench.py, D0 b32): it halves the
-  // blocks per CU (double-buffered LDS, more registers), which costs more than the prefetch
-  // gains on the large stride-2 and wide-channel layers
-  if (which == 0 && ((K == 3 && S == 2 && g.C >= 192) || (S == 1 && g.C >= 144 && g.C <= 240)))
-    return launch_dw3<T, K, S, false>(g, s);
-  // the direct forms keep one row of C/8 threads per block (C <= 2048); wider channel counts
-  // (EfficientDet-D4+ last stages, C = 2688) take the channel-blocked tile kernels
-  if (g.C > 2048 && which == 0) return launch_dw3<T, K, S, false>(g, s);
-  if (g.C > 2048 && which == 1) {
-    g.tiles_total = host_tiles(g.pin);
-    if (g.tiles_total) hipLaunchKernelGGL((k_dw_dgrad<T, K, S>), dim3(g.tiles_total * g.ncb), dim3(256), 0, s, g);
-    return check_launch("edet dwconv");
-  }
-  if (which == 2 && S == 1 && (g.C <= 64 || (K == 5 && g.C == 240))) return launch_dw3<T, K, S, true>(g, s);
-  // forward: the LDS tile kernel applies the producer's lazy BN/swish/gate once per input
-  // element; the direct form re-evaluates it per tap (K*K times) and only wins at k3 s2.
-  // dgrad has no transform: the direct gather form measured equal or up to 1.4x faster.
-  if (which == 0 && !(K == 3 && S == 2)) {
-    g.tiles_total = host_tiles(g.pout);
-    const int G = std::max(1, std::min(g.tiles_total, cdiv(2048, g.ncb)));
-    if (g.tiles_total) hipLaunchKernelGGL((k_dw_fwd<T, K, S>), dim3(G * g.ncb), dim3(256), 0, s, g);
-  } else if (which == 0 || which == 1) {
-    const DwGeom geo = dw_geom(g.C);
-    const edet_pyramid& pp = which == 0 ? g.pout : g.pin;
-    long px = 0;
-    for (int i = 0; i < pp.nseg; ++i) px += (long)pp.batch * pp.H[i] * pp.W[i];
-    const int grid = (int)std::max<long>(1, std::min<long>(4096, (px + geo.R - 1) / geo.R));
-    if (which == 0) {
-      const size_t lds = g.has_stats ? 2 * (size_t)geo.R * g.C * sizeof(float) : 0;
-      if (px) hipLaunchKernelGGL((k_dw2_fwd<T, K, S>), dim3(grid), dim3(geo.TPR * geo.R), lds, s, g, geo);
-    } else {
-      if (px) hipLaunchKernelGGL((k_dw2_dgrad<T, K, S>), dim3(grid), dim3(geo.TPR * geo.R), 0, s, g, geo);
+  const DwForm form = dw_form(which, K, S, g.C);
+  if (which == 0) {
+    if (form == DW_DW3) return launch_dw3<T, K, S, false>(g, s);
+    if (form == DW_TILE) {
+      g.tiles_total = host_tiles(g.pout);
+      const int G = std::max(1, std::min(g.tiles_total, cdiv(2048, g.ncb)));
+      if (g.tiles_total) hipLaunchKernelGGL((k_dw_fwd<T, K, S>), dim3(G * g.ncb), dim3(256), 0, s, g);
+      return check_launch("edet dwconv fwd");
+    }
+  } else if (which == 1) {
+    if (form == DW_DW4) return launch_dw4_dgrad<T, K, S>(g, s);
+    if (form == DW_TILE) {
+      g.tiles_total = host_tiles(g.pin);
+      if (g.tiles_total) hipLaunchKernelGGL((k_dw_dgrad<T, K, S>), dim3(g.tiles_total * g.ncb), dim3(256), 0, s, g);
+      return check_launch("edet dwconv dgrad");
     }
   } else {
+    if (form == DW_DW3) return launch_dw3<T, K, S, true>(g, s);
     g.tiles_total = host_tiles(g.pout);
     // ~2048 blocks: these loops are latency-bound (768 blocks measured 1.3-1.9x slower)
     int chunks = cdiv(2048, g.ncb);
@@ -805,9 +985,19 @@ static int launch_dw(int which, DwArgs g, hipStream_t s) {
     chunks = cdiv(g.tiles_total, g.tiles_per_wg);
     g.part = nullptr;  // K*K*C is small: atomics measured faster than a 2048-way partial sum
     if (g.tiles_total) hipLaunchKernelGGL((k_dw_wgrad<T, K, S>), dim3(chunks * g.ncb), dim3(256), 0, s, g);
-    int rc = check_launch("edet dwconv");
-    if (rc || !g.part || !g.tiles_total) return rc;
-    return sum_partials(g.part, chunks, (long)K * K * g.C, g.dw, s);
+    return check_launch("edet dwconv wgrad");
+  }
+  // DW_DIRECT (fwd / dgrad)
+  const DwGeom geo = dw_geom(g.C);
+  const edet_pyramid& pp = which == 0 ? g.pout : g.pin;
+  long px = 0;
+  for (int i = 0; i < pp.nseg; ++i) px += (long)pp.batch * pp.H[i] * pp.W[i];
+  const int grid = (int)std::max<long>(1, std::min<long>(4096, (px + geo.R - 1) / geo.R));
+  if (which == 0) {
+    const size_t lds = g.has_stats ? 2 * (size_t)geo.R * g.C * sizeof(float) : 0;
+    if (px) hipLaunchKernelGGL((k_dw2_fwd<T, K, S>), dim3(grid), dim3(geo.TPR * geo.R), lds, s, g, geo);
+  } else {
+    if (px) hipLaunchKernelGGL((k_dw2_dgrad<T, K, S>), dim3(grid), dim3(geo.TPR * geo.R), 0, s, g, geo);
   }
   return check_launch("edet dwconv");
 }
