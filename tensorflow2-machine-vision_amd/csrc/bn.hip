@@ -23,13 +23,14 @@ struct RowGeom {
   int TPR, R, VPT, CH;  // threads per row, rows per pass, vectors per thread, rows per chunk
 };
 
-static RowGeom row_geom(int C) {
+// passes: rows per chunk = R * passes; 0 = about 16K elements per chunk (at most 16 passes)
+static RowGeom row_geom(int C, int passes = 0) {
   RowGeom r;
   const int NV = C / 8;
   r.TPR = NV <= 256 ? NV : 256;
   r.VPT = cdiv(NV, r.TPR);
   r.R = 256 / r.TPR;
-  int passes = 16384 / (r.R * C);
+  if (passes <= 0) passes = 16384 / (r.R * C);
   if (passes < 1) passes = 1;
   if (passes > 16) passes = 16;
   r.CH = r.R * passes;
@@ -579,11 +580,14 @@ int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, i
   EDET_REQUIRE(dsq == nullptr || p->nseg == 1, "lazy_bwd_reduce: dsq needs one segment");
   LArgs g{};
   g.lz = *x; g.p = *p; g.acc = *acc; g.dv = dv; g.dv_scale = dv_scale; g.dsq = dsq; g.C = C;
-  g.geo = row_geom(C);
+  // Every block flushes 2C fp64 atomics to the same addresses, which serialise (~20 ns per
+  // block and address): long chunks and at most 1024 persistent blocks measured best
+  // (scripts/row_probe.py: -20..-30 % on the C >= 240 and C = 16 layers, equal elsewhere).
+  g.geo = row_geom(C, 16);
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 2 * C * sizeof(float2) + 2 * (size_t)g.geo.R * C * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    const int grid = nb < 2048 ? nb : 2048;
+    const int grid = nb < 1024 ? nb : 1024;
     if (nb) hipLaunchKernelGGL(k_lazy_bwd_reduce<T>, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
     return check_launch("edet lazy_bwd_reduce");
   });
