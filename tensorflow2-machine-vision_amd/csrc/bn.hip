@@ -121,8 +121,8 @@ __device__ __forceinline__ void flush_reduce(const LArgs& g, const RowGeom& geo,
   for (int c = tid; c < C; c += blockDim.x) {
     float ss = 0.f, qq = 0.f;
     for (int i = 0; i < geo.R; ++i) { ss += red[i * C + c]; qq += red[(geo.R + i) * C + c]; }
-    atomicAdd(g.acc.dbeta[seg] + c, (double)ss);
-    atomicAdd(g.acc.dgamma[seg] + c, (double)qq);
+    stat_add(g.acc.dbeta[seg] + c, (double)ss);
+    stat_add(g.acc.dgamma[seg] + c, (double)qq);
   }
   __syncthreads();
 }

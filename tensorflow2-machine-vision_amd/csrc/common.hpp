@@ -109,6 +109,15 @@ __device__ __forceinline__ float dswishf_(float x) {
   return s * (1.f + x * (1.f - s));
 }
 
+// fp64 statistics accumulation.  EDET_EXP_NOATOM drops it: a timing experiment only (the
+// statistics are then wrong), used to price same-address atomic serialisation.
+__device__ __forceinline__ void stat_add(double* p, double v) {
+#ifdef EDET_EXP_NOATOM
+  if (v == 1234.5)
+#endif
+    atomicAdd(p, v);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

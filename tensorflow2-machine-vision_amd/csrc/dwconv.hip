@@ -163,8 +163,8 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
           float ss = 0.f, qq = 0.f;
 #pragma unroll
           for (int i = 0; i < 8; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
-          atomicAdd(g.stats.sum[cur_seg] + c0 + tid, (double)(ss));
-          atomicAdd(g.stats.sq[cur_seg] + c0 + tid, (double)(qq));
+          stat_add(g.stats.sum[cur_seg] + c0 + tid, (double)(ss));
+          stat_add(g.stats.sq[cur_seg] + c0 + tid, (double)(qq));
         }
       }
       s = 0.f;
@@ -227,8 +227,8 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
       float ss = 0.f, qq = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
-      atomicAdd(g.stats.sum[cur_seg] + c0 + tid, (double)(ss));
-      atomicAdd(g.stats.sq[cur_seg] + c0 + tid, (double)(qq));
+      stat_add(g.stats.sum[cur_seg] + c0 + tid, (double)(ss));
+      stat_add(g.stats.sq[cur_seg] + c0 + tid, (double)(qq));
     }
   }
 }
@@ -542,8 +542,8 @@ __global__ __launch_bounds__(256) void k_dw3(DwArgs g) {
       float ss = 0.f, qq = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
-      atomicAdd(g.stats.sum[seg] + c0 + tid, (double)ss);
-      atomicAdd(g.stats.sq[seg] + c0 + tid, (double)qq);
+      stat_add(g.stats.sum[seg] + c0 + tid, (double)ss);
+      stat_add(g.stats.sq[seg] + c0 + tid, (double)qq);
     }
     s = 0.f;
     q = 0.f;
@@ -731,8 +731,8 @@ __global__ __launch_bounds__(256) void k_dw2_fwd(DwArgs g, DwGeom geo) {
       for (int ch = tid; ch < C; ch += blockDim.x) {
         float ss = 0.f, qq = 0.f;
         for (int i = 0; i < geo.R; ++i) { ss += red2[i * C + ch]; qq += red2[(geo.R + i) * C + ch]; }
-        atomicAdd(g.stats.sum[seg] + ch, (double)ss);
-        atomicAdd(g.stats.sq[seg] + ch, (double)qq);
+        stat_add(g.stats.sum[seg] + ch, (double)ss);
+        stat_add(g.stats.sq[seg] + ch, (double)qq);
       }
       __syncthreads();
     }

@@ -277,8 +277,8 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     for (int i = tid; i < BN; i += 256) {
       const int col = col0 + i;
       if (col < g.N) {
-        atomicAdd(g.stats.sum[seg] + col, (double)(red[0][0][i] + red[0][1][i]));
-        atomicAdd(g.stats.sq[seg] + col, (double)(red[1][0][i] + red[1][1][i]));
+        stat_add(g.stats.sum[seg] + col, (double)(red[0][0][i] + red[0][1][i]));
+        stat_add(g.stats.sq[seg] + col, (double)(red[1][0][i] + red[1][1][i]));
       }
     }
   }
@@ -336,8 +336,8 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
     __syncthreads();
     if (cur_seg >= 0 && g.has_stats)
       for (int c = tid; c < ncols; c += 256) {
-        atomicAdd(g.stats.sum[cur_seg] + cbase + c, (double)(red[c] + red[LDC + c]));
-        atomicAdd(g.stats.sq[cur_seg] + cbase + c, (double)(red[2 * LDC + c] + red[3 * LDC + c]));
+        stat_add(g.stats.sum[cur_seg] + cbase + c, (double)(red[c] + red[LDC + c]));
+        stat_add(g.stats.sq[cur_seg] + cbase + c, (double)(red[2 * LDC + c] + red[3 * LDC + c]));
         red[c] = red[LDC + c] = red[2 * LDC + c] = red[3 * LDC + c] = 0.f;
       }
     if constexpr (LAZY) {
@@ -521,8 +521,8 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   __syncthreads();
   if (cur_seg >= 0 && g.has_stats)
     for (int c = tid; c < ncols; c += 256) {
-      atomicAdd(g.stats.sum[cur_seg] + cbase + c, (double)(red[c] + red[LDC + c]));
-      atomicAdd(g.stats.sq[cur_seg] + cbase + c, (double)(red[2 * LDC + c] + red[3 * LDC + c]));
+      stat_add(g.stats.sum[cur_seg] + cbase + c, (double)(red[c] + red[LDC + c]));
+      stat_add(g.stats.sq[cur_seg] + cbase + c, (double)(red[2 * LDC + c] + red[3 * LDC + c]));
     }
 }
 
@@ -1084,8 +1084,8 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
         if (col < N && cl < p.NGtot) {
           float& rs = red[(0 * 2 + wm) * p.NGtot + cl];
           float& rq = red[(1 * 2 + wm) * p.NGtot + cl];
-          atomicAdd(g.stats.sum[seg] + col, (double)rs);
-          atomicAdd(g.stats.sq[seg] + col, (double)rq);
+          stat_add(g.stats.sum[seg] + col, (double)rs);
+          stat_add(g.stats.sq[seg] + col, (double)rq);
           rs = 0.f;
           rq = 0.f;
         }
@@ -1310,6 +1310,13 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
   const int KP = cdiv(g.K, 32) * 32;
   const int LDCf = cdiv(g.N, 8) * 8;
   constexpr size_t BUDGET = 96 * 1024;
+  // EDET_GEMM_FORM=1 forces the K-streaming form (A/B timing, scripts/gemm_probe.py)
+  static const int force = getenv("EDET_GEMM_FORM") ? atoi(getenv("EDET_GEMM_FORM")) : 0;
+  if (force == 1) return dispatch_gemm_kloop<T, LAZY>(g, s);
+  // lazy A with K >= 112 into N > 320 (the stage 5-7 expand convs): the A-resident form walks
+  // its column chunks one dependent B load at a time with 2 blocks per CU; the pipelined
+  // K loop over 128-column tiles measured 1.3-1.4x faster (8192x192x1152, 32768x112x672)
+  if (LAZY && g.K >= 112 && g.N > 320) return dispatch_gemm_kloop<T, LAZY>(g, s);
   if (g.K <= 512) {
     if (gemm_r_lds<T, 128, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 128, LAZY>(g, s);
     if (gemm_r_lds<T, 64, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 64, LAZY>(g, s);
