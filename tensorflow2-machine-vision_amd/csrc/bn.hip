@@ -342,6 +342,7 @@ __global__ __launch_bounds__(256) void k_se_bn_combine(int B, int C, const float
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= C) return;
   double gb = 0.0, gg = 0.0;
+#pragma unroll 8
   for (int n = 0; n < B; ++n) {
     const double gt = gate[(size_t)n * C + c], ds = dsq[(size_t)n * C + c];
     const size_t i = (size_t)n * C + c, BC = (size_t)B * C;
@@ -365,6 +366,7 @@ __global__ __launch_bounds__(256) void k_se_reduce_c(int B, int C, int R, const 
   if (item >= B * R) return;
   const int n = item / R, r = item - n * R;
   float a = 0.f;
+#pragma unroll 4
   for (int c = lane; c < C; c += 64) a += w1[(size_t)r * C + c] * (float)s[(size_t)n * C + c];
   a = wave_sum(a);
   if (lane == 0) z1[item] = a + b1[r];
@@ -377,6 +379,7 @@ __global__ __launch_bounds__(256) void k_se_excite(int B, int C, int R, const fl
   if (idx >= B * C) return;
   const int n = idx / C, c = idx - n * C;
   float a = b2[c];
+#pragma unroll 8
   for (int r = 0; r < R; ++r) {
     const float z = z1[(size_t)n * R + r];
     a += w2[(size_t)c * R + r] * (z * sigmoidf_(z));
@@ -393,6 +396,7 @@ __global__ __launch_bounds__(256) void k_se_dz1(int B, int C, int R, const float
   if (item >= B * R) return;
   const int n = item / R, r = item - n * R;
   float a = 0.f;
+#pragma unroll 4
   for (int c = lane; c < C; c += 64) {
     const float gv = gate[(size_t)n * C + c];
     a += (float)dgate[(size_t)n * C + c] * gv * (1.f - gv) * w2[(size_t)c * R + r];
@@ -417,6 +421,7 @@ __global__ __launch_bounds__(256) void k_se_wgrad(int B, int C, int R, int HW, c
   if (idx < C * R) {
     const int c = idx / R, r = idx - c * R;
     float a2 = 0.f, a1 = 0.f;
+#pragma unroll 8
     for (int n = 0; n < B; ++n) {
       const float gv = gate[(size_t)n * C + c];
       const float d2 = (float)dgate[(size_t)n * C + c] * gv * (1.f - gv);
@@ -430,11 +435,13 @@ __global__ __launch_bounds__(256) void k_se_wgrad(int B, int C, int R, int HW, c
   if (idx < B * C) {
     const int n = idx / C, c = idx - n * C;
     float a = 0.f;
+#pragma unroll 8
     for (int r = 0; r < R; ++r) a += dz1[(size_t)n * R + r] * w1[(size_t)r * C + c];
     dsq[idx] = a / (float)HW;
   }
   if (idx < C) {
     float a = 0.f;
+#pragma unroll 8
     for (int n = 0; n < B; ++n) {
       const float gv = gate[(size_t)n * C + idx];
       a += (float)dgate[(size_t)n * C + idx] * gv * (1.f - gv);
@@ -443,6 +450,7 @@ __global__ __launch_bounds__(256) void k_se_wgrad(int B, int C, int R, int HW, c
   }
   if (idx < R) {
     float a = 0.f;
+#pragma unroll 8
     for (int n = 0; n < B; ++n) a += dz1[(size_t)n * R + idx];
     db1[idx] += a;
   }
