@@ -175,6 +175,10 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
   if (cur_seg >= 0) flush_reduce<T>(g, geo, cur_seg, rr, tv, red, s, q);
 }
 
+#ifndef EDET_APPLY_EU
+#define EDET_APPLY_EU 2
+#endif
+constexpr int EU = EDET_APPLY_EU;
 template <typename T>
 __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -201,21 +205,30 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g) {
   const int NV = C / 8;
   T* DX = (T*)g.dx;
   const bool bn = g.lz.bn.enabled;
-  for (int m = m_begin + rr; m < m_end; m += geo.R) {
-    const int n = (m - off) / hw;
 #pragma unroll
-    for (int v = 0; v < RVPT; ++v) {
-      const int cv = tv + v * geo.TPR;
-      if (v < geo.VPT && cv < NV) {
-        const int c = cv * 8;
-        float du[8], xh[8], o[8];
-        lazy_du<T>(g, seg, m, n, c, af, mr, du, xh);
+  for (int v = 0; v < RVPT; ++v) {
+    const int cv = tv + v * geo.TPR;
+    if (!(v < geo.VPT && cv < NV)) continue;
+    const int c = cv * 8;
+    // EU rows per trip, all loads before any store (vmcnt orders loads behind earlier stores)
+    for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
+      float du[EU][8], xh[EU][8];
+#pragma unroll
+      for (int u = 0; u < EU; ++u) {
+        const int mu = min(m + u * geo.R, m_end - 1);
+        lazy_du<T>(g, seg, mu, (mu - off) / hw, c, af, mr, du[u], xh[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < EU; ++u) {
+        const int mu = m + u * geo.R;
+        if (mu >= m_end) break;
+        float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float2 d = gb[c + j];
-          o[j] = bn ? af[c + j].x * (du[j] - d.y - xh[j] * d.x) : du[j];
+          o[j] = bn ? af[c + j].x * (du[u][j] - d.y - xh[u][j] * d.x) : du[u][j];
         }
-        acc8m(DX + (size_t)m * C + c, 8, o, g.accumulate);
+        acc8m(DX + (size_t)mu * C + c, 8, o, g.accumulate);
       }
     }
   }
