@@ -18,6 +18,12 @@ namespace edet {
 // R contiguous rows of the NHWC tensor (fully coalesced, no idle lanes for C = 96/144/240...)
 // and each thread keeps a fixed channel vector -> per-thread partial sums need no atomics.
 constexpr int RVPT = 2;  // vectors per thread (C <= 4096)
+// rows per trip in the streaming row loops: both rows' loads are issued before either is
+// consumed (in apply, before either store: vmcnt orders loads behind earlier stores)
+#ifndef EDET_APPLY_EU
+#define EDET_APPLY_EU 2
+#endif
+constexpr int EU = EDET_APPLY_EU;
 
 struct RowGeom {
   int TPR, R, VPT, CH;  // threads per row, rows per pass, vectors per thread, rows per chunk
@@ -157,16 +163,26 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
     const int m_begin = off + chunk * geo.CH, m_end = min(off + rows, m_begin + geo.CH);
     const int hw = g.p.H[seg] * g.p.W[seg];
     if (rr < geo.R) {
-      for (int m = m_begin + rr; m < m_end; m += geo.R) {
-        const int n = (m - off) / hw;
 #pragma unroll
-        for (int v = 0; v < RVPT; ++v) {
-          const int cv = tv + v * geo.TPR;
-          if (v < geo.VPT && cv < NV) {
-            float du[8], xh[8];
-            lazy_du<T>(g, seg, m, n, cv * 8, af, mr, du, xh);
+      for (int v = 0; v < RVPT; ++v) {
+        const int cv = tv + v * geo.TPR;
+        if (!(v < geo.VPT && cv < NV)) continue;
+        for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
+          float du[EU][8], xh[EU][8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) { s[v][j] += du[j]; q[v][j] += du[j] * xh[j]; }
+          for (int u = 0; u < EU; ++u) {
+            const int mu = min(m + u * geo.R, m_end - 1);
+            lazy_du<T>(g, seg, mu, (mu - off) / hw, cv * 8, af, mr, du[u], xh[u]);
+          }
+#pragma unroll
+          for (int u = 0; u < EU; ++u) {
+            const float k = m + u * geo.R < m_end ? 1.f : 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float d = du[u][j] * k;
+              s[v][j] += d;
+              q[v][j] += d * xh[u][j];
+            }
           }
         }
       }
@@ -175,10 +191,6 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
   if (cur_seg >= 0) flush_reduce<T>(g, geo, cur_seg, rr, tv, red, s, q);
 }
 
-#ifndef EDET_APPLY_EU
-#define EDET_APPLY_EU 2
-#endif
-constexpr int EU = EDET_APPLY_EU;
 template <typename T>
 __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -254,19 +266,26 @@ __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[v][j] = 0.f;
   if (rr < geo.R) {
-    for (int m = m_begin + rr; m < m_end; m += geo.R) {
 #pragma unroll
-      for (int v = 0; v < RVPT; ++v) {
-        const int cv = tv + v * geo.TPR;
-        if (v < geo.VPT && cv < NV) {
-          const int c = cv * 8;
-          float x[8], d[8];
-          ld8((const T*)g.lz.x + (size_t)m * g.lz.ld + c, x);
-          if (GATEGRAD) ld8((const T*)g.dv + (size_t)m * C + c, d);
+    for (int v = 0; v < RVPT; ++v) {
+      const int cv = tv + v * geo.TPR;
+      if (!(v < geo.VPT && cv < NV)) continue;
+      const int c = cv * 8;
+      for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
+        float x[EU][8], d[EU][8];
+#pragma unroll
+        for (int u = 0; u < EU; ++u) {
+          const int mu = min(m + u * geo.R, m_end - 1);
+          ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
+          if (GATEGRAD) ld8((const T*)g.dv + (size_t)mu * C + c, d[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < EU; ++u) {
+          const float k = m + u * geo.R < m_end ? 1.f : 0.f;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float val = lazy_apply(x[j], af[c + j], g.lz.act);
-            s[v][j] += GATEGRAD ? d[j] * val : val;
+            const float val = lazy_apply(x[u][j], af[c + j], g.lz.act) * k;
+            s[v][j] += GATEGRAD ? d[u][j] * val : val;
           }
         }
       }
@@ -316,22 +335,31 @@ __global__ __launch_bounds__(256) void k_gate_bn_reduce(LArgs g) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[q][j] = 0.f;
   if (live) {
-    for (int m = m_begin + rr; m < m_end; m += geo.R) {
-      float x[8], d[8];
-      ld8((const T*)g.lz.x + (size_t)m * g.lz.ld + c, x);
-      ld8((const T*)g.dv + (size_t)m * C + c, d);
+    for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
+      float x[EU][8], d[EU][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float2 t = af[c + j], b = mr[c + j];
-        const float u = x[j] * t.x + t.y;
-        const float sg = sigmoidf_(u);
-        const float sw = u * sg, dsw = sg * (1.f + u * (1.f - sg));
-        const float xh = (x[j] - b.x) * b.y;
-        a[0][j] += d[j] * sw;
-        a[1][j] += d[j] * dsw;
-        a[2][j] += dsw;
-        a[3][j] += d[j] * dsw * xh;
-        a[4][j] += dsw * xh;
+      for (int u = 0; u < EU; ++u) {
+        const int mu = min(m + u * geo.R, m_end - 1);
+        ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
+        ld8((const T*)g.dv + (size_t)mu * C + c, d[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < EU; ++u) {
+        const float k = m + u * geo.R < m_end ? 1.f : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float2 t = af[c + j], b = mr[c + j];
+          const float uu = x[u][j] * t.x + t.y;
+          const float sg = sigmoidf_(uu);
+          const float sw = uu * sg, dsw = sg * (1.f + uu * (1.f - sg)) * k;
+          const float xh = (x[u][j] - b.x) * b.y;
+          const float dd = d[u][j] * k;
+          a[0][j] += dd * sw;
+          a[1][j] += dd * dsw;
+          a[2][j] += dsw;
+          a[3][j] += dd * dsw * xh;
+          a[4][j] += dsw * xh;
+        }
       }
     }
   }
@@ -532,22 +560,29 @@ __global__ __launch_bounds__(256) void k_materialize(LArgs g) {
   const int hw = g.p.H[seg] * g.p.W[seg];
   const int NV = C / 8;
   T* OUT = (T*)g.dx;
-  for (int m = m_begin + rr; m < m_end; m += geo.R) {
-    const int n = (m - off) / hw;
 #pragma unroll
-    for (int v = 0; v < RVPT; ++v) {
-      const int cv = tv + v * geo.TPR;
-      if (v < geo.VPT && cv < NV) {
-        const int c = cv * 8;
-        float x[8], gt[8];
-        ld8((const T*)g.lz.x + (size_t)m * g.lz.ld + c, x);
-        if (g.lz.gate) ld8(g.lz.gate + (size_t)n * C + c, gt);
+  for (int v = 0; v < RVPT; ++v) {
+    const int cv = tv + v * geo.TPR;
+    if (!(v < geo.VPT && cv < NV)) continue;
+    const int c = cv * 8;
+    for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
+      float x[EU][8], gt[EU][8];
+#pragma unroll
+      for (int u = 0; u < EU; ++u) {
+        const int mu = min(m + u * geo.R, m_end - 1);
+        ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
+        if (g.lz.gate) ld8(g.lz.gate + (size_t)((mu - off) / hw) * C + c, gt[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < EU; ++u) {
+        const int mu = m + u * geo.R;
+        if (mu >= m_end) break;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          x[j] = lazy_apply(x[j], ax[c + j], g.lz.act);
-          if (g.lz.gate) x[j] *= gt[j];
+          x[u][j] = lazy_apply(x[u][j], ax[c + j], g.lz.act);
+          if (g.lz.gate) x[u][j] *= gt[u][j];
         }
-        st8(OUT + (size_t)m * C + c, x);
+        st8(OUT + (size_t)mu * C + c, x[u]);
       }
     }
   }
