@@ -36,7 +36,13 @@ static RowGeom row_geom(int C, int passes = 0) {
   r.TPR = NV <= 256 ? NV : 256;
   r.VPT = cdiv(NV, r.TPR);
   r.R = 256 / r.TPR;
-  if (passes <= 0) passes = 16384 / (r.R * C);
+  static const int force = getenv("EDET_ROW_PASSES") ? atoi(getenv("EDET_ROW_PASSES")) : 0;  // A/B only
+  if (passes <= 0) {
+    passes = force > 0 ? force : 16384 / (r.R * C);
+    // C >= 1024 runs one row per block pass: shorter chunks give more blocks in flight
+    // (M = 8192, C = 1152 apply: 38 -> 31 us, scripts/row_probe.py)
+    if (force <= 0 && C >= 1024 && passes > 8) passes = 8;
+  }
   if (passes < 1) passes = 1;
   if (passes > 16) passes = 16;
   r.CH = r.R * passes;
