@@ -1320,10 +1320,10 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
   if (g.K <= 512) {
     if (gemm_r_lds<T, 128, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 128, LAZY>(g, s);
     if (gemm_r_lds<T, 64, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 64, LAZY>(g, s);
-    // wide N (> 320, beyond the k-loop kernel) splits the columns until the C tile fits
-    if (gemm_r_lds<T, 32, LAZY>(g.K, KP, LDCf) <= BUDGET ||
-        (g.N > 320 && gemm_r_lds<T, 32, LAZY>(g.K, KP, RNB) <= 150 * 1024))
-      return launch_gemm_r<T, 32, LAZY>(g, s);
+    if (gemm_r_lds<T, 32, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 32, LAZY>(g, s);
+    // wider C tiles than fit: the column-split A-resident form walked its chunks one
+    // dependent B load at a time with one block per CU (dgrad 8192 x 320 -> 1152: 88 us);
+    // the pipelined K loop over 128-column tiles takes 31 us
   }
   return dispatch_gemm_kloop<T, LAZY>(g, s);
 }
