@@ -16,7 +16,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from tf2mv_amd import _lib as L  # noqa: E402
-from tf2mv_amd.runtime import Pyr, stream, vp  # noqa: E402
+from tf2mv_amd.runtime import Pyr, ensure_workspace, stream, vp  # noqa: E402
 from gpu_util import LazyDesc, make_bn, stat_out, zeros64  # noqa: E402
 
 
@@ -37,6 +37,8 @@ def main():
     only = os.environ.get("ONLY", "")  # run just one variant (for rocprofv3 --pmc passes)
     shapes = [tuple(int(v) for v in a.split("x")) for a in sys.argv[1:]] or [(8192, 1152, 320)]
     rng = np.random.default_rng(0)
+    if os.environ.get("NO_WS", "0") != "1":
+        ensure_workspace(torch.device("cuda"))  # as the model runs: split partials, not atomics
     for (M, K, N) in shapes:
         # images of hw = 256 rows (16x16) as in the MBConv stage 5/6 tensors
         hw = 256 if M % 256 == 0 else M

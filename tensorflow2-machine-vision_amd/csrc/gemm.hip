@@ -1393,10 +1393,11 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
     int split = cdiv(1024, tiles);
     const int max_split = std::max(1, cdiv(g.M, WT_BM * 4));
     if (split > max_split) split = max_split;
-    // large weights (N*K >= 16K, the MBConv expand/project and head convs at small M): at
-    // most 128 splits write plain partials that one fixed-order pass sums (split x N x K
-    // atomics were millions per launch); small weights keep the atomics and full split
-    const bool use_part = (long)N * K >= 16384 && workspace_f32(0) != nullptr;
+    // fp32 atomics into dW (distinct addresses, split-way contention) measured faster than
+    // per-split partials + a fixed-order sum pass for every D0 shape (-95 us/step, class head
+    // 152 -> 118 us); EDET_WG_PART=1 restores the partials for N*K >= 16K (A/B)
+    static const int part_env = getenv("EDET_WG_PART") ? atoi(getenv("EDET_WG_PART")) : 0;  // A/B only
+    const bool use_part = part_env == 1 && (long)N * K >= 16384 && workspace_f32(0) != nullptr;
     if (use_part && split > 128) split = 128;
     g.rows_per = cdiv(cdiv(g.M, split), WT_BM) * WT_BM;
     split = std::max(1, cdiv(g.M, g.rows_per));
