@@ -1388,10 +1388,13 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
   hipStream_t s = (hipStream_t)stream;
   const bool plain = lazy_is_plain(a);
   if (dtype == EDET_BF16) {
-    // ~1024 blocks, each at least 4 stages of 64 rows (stages never straddle a segment:
-    // segments start on 128-row boundaries)
-    int split = cdiv(1024, tiles);
-    const int max_split = std::max(1, cdiv(g.M, WT_BM * 4));
+    // stages never straddle a segment: segments start on 128-row boundaries
+    static const int blk_env = getenv("EDET_WG_BLOCKS") ? atoi(getenv("EDET_WG_BLOCKS")) : 0;  // A/B only
+    static const int stg_env = getenv("EDET_WG_STAGES") ? atoi(getenv("EDET_WG_STAGES")) : 0;  // A/B only
+    // ~2048 blocks of at least 8 stages each (scripts/kbench.py sweep over the D0 step:
+    // 2.37 -> 2.23 ms against 1024 blocks x 4 stages)
+    int split = cdiv(blk_env > 0 ? blk_env : 2048, tiles);
+    const int max_split = std::max(1, cdiv(g.M, WT_BM * (stg_env > 0 ? stg_env : 8)));
     if (split > max_split) split = max_split;
     // fp32 atomics into dW (distinct addresses, split-way contention) measured faster than
     // per-split partials + a fixed-order sum pass for every D0 shape (-95 us/step, class head
