@@ -118,6 +118,17 @@ __device__ __forceinline__ void stat_add(double* p, double v) {
     atomicAdd(p, v);
 }
 
+// Sum over the four 16-lane rows of a wave (lane bits 4 and 5), result in every lane: the
+// MFMA epilogues reduce a column's 4 row groups this way.  gfx950's v_permlane16/32_swap are
+// plain VALU ops; the __shfl_xor form was two dependent ds_bpermute round trips per value
+// (the BN-statistics epilogue cost 25 us of a 90 us GEMM).  Same additions, same order.
+__device__ __forceinline__ float row4_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -266,8 +266,8 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       float s = ssum[j], q = ssq[j];
-      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+      s = row4_sum(s);
+      q = row4_sum(q);
       if (lane < 16) {
         red[0][wm][wn * WN + j * 16 + lane] = s;
         red[1][wm][wn * WN + j * 16 + lane] = q;
@@ -473,8 +473,8 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
           if (row0 + rl < seg_end && col < N) { s += v; q += v * v; }
         }
       if (g.has_stats) {
-        s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-        q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+        s = row4_sum(s);
+        q = row4_sum(q);
         if (lane < 16 && col < N) {
           red[wm * LDC + col - cbase] += s;
           red[(2 + wm) * LDC + col - cbase] += q;
@@ -1045,8 +1045,8 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
           if (wrow0 + rl < seg_end) { s += v; q += v * v; }
         }
       if (g.has_stats) {
-        s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-        q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+        s = row4_sum(s);
+        q = row4_sum(q);
         if (lane < 16) {  // sole owner of (wm, cl)
           red[(0 * 2 + wm) * p.NGtot + cl] += s;
           red[(1 * 2 + wm) * p.NGtot + cl] += q;
