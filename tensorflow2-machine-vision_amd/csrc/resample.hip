@@ -346,17 +346,41 @@ __device__ __forceinline__ void pool_window(const edet_lazy& lz, const float2* a
                                             int pt, int pl, int oy, int ox, int c, int nc, float* best, int* arg) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) { best[j] = -FLT_MAX; arg[j] = -1; }
-  for (int kh = 0; kh < 3; ++kh) {
-    const int iy = oy * 2 - pt + kh;
-    if (iy < 0 || iy >= H) continue;
-    for (int kw = 0; kw < 3; ++kw) {
-      const int ix = ox * 2 - pl + kw;
-      if (ix < 0 || ix >= W) continue;
-      float v[8];
-      lazy_load8<T>(lz, af, img_row0 + (size_t)iy * W + ix, c, nc, v);
+  if (nc < 8) {  // channel tail (not reached with C % 8 == 0)
+    for (int kh = 0; kh < 3; ++kh) {
+      const int iy = oy * 2 - pt + kh;
+      if (iy < 0 || iy >= H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int ix = ox * 2 - pl + kw;
+        if (ix < 0 || ix >= W) continue;
+        float v[8];
+        lazy_load8<T>(lz, af, img_row0 + (size_t)iy * W + ix, c, nc, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (arg[j] < 0 || v[j] > best[j]) { best[j] = v[j]; arg[j] = iy * W + ix; }
+        for (int j = 0; j < 8; ++j)
+          if (arg[j] < 0 || v[j] > best[j]) { best[j] = v[j]; arg[j] = iy * W + ix; }
+      }
+    }
+    return;
+  }
+  // all nine taps are loaded first (select-predicated addresses: a load inside a divergent
+  // `if` is waited on inside it), then scanned in the same row-major order
+  float v[9][8];
+  bool in[9];
+  const T* X = (const T*)lz.x + img_row0 * lz.ld + c;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int iy = oy * 2 - pt + k / 3, ix = ox * 2 - pl + k % 3;
+    in[k] = iy >= 0 && iy < H && ix >= 0 && ix < W;
+    ld8(X + (in[k] ? (size_t)(iy * W + ix) * lz.ld : 0), v[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    if (!in[k]) continue;
+    const int pos = (oy * 2 - pt + k / 3) * W + (ox * 2 - pl + k % 3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float t = lazy_apply(v[k][j], af[j], lz.act);
+      if (arg[j] < 0 || t > best[j]) { best[j] = t; arg[j] = pos; }
     }
   }
 }
