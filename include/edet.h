@@ -109,6 +109,9 @@ typedef struct edet_fuse_input {
   int32_t H, W;         /* input spatial size */
   int32_t mode;         /* EDET_MODE_* : same / nearest upsample / maxpool 3x3 s2 SAME */
   int32_t accumulate;   /* backward: accumulate into dx */
+  uint8_t* pool_arg;    /* MAXPOOL, optional: [B*H_out*W_out][C] window tap (0..8, row-major) of
+                           each output's max.  fwd writes it, bwd reads it instead of
+                           re-evaluating the windows (null: recompute) */
 } edet_fuse_input;
 
 typedef struct edet_sched {

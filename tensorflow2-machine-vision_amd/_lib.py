@@ -56,7 +56,7 @@ class BnGrad64(ctypes.Structure):
 
 class FuseInput(ctypes.Structure):
     _fields_ = [("v", Lazy), ("dx", c_void_p), ("H", c_int32), ("W", c_int32),
-                ("mode", c_int32), ("accumulate", c_int32)]
+                ("mode", c_int32), ("accumulate", c_int32), ("pool_arg", c_void_p)]
 
 
 class Sched(ctypes.Structure):

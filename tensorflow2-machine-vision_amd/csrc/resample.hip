@@ -343,9 +343,11 @@ __device__ __forceinline__ void lazy_load8(const edet_lazy& lz, const float2* af
 // max over the 3x3 s2 SAME window of output (oy, ox); optionally the argmax (row-major first)
 template <typename T>
 __device__ __forceinline__ void pool_window(const edet_lazy& lz, const float2* af, size_t img_row0, int H, int W,
-                                            int pt, int pl, int oy, int ox, int c, int nc, float* best, int* arg) {
+                                            int pt, int pl, int oy, int ox, int c, int nc, float* best, int* arg,
+                                            int* tap = nullptr) {
+  int tk[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { best[j] = -FLT_MAX; arg[j] = -1; }
+  for (int j = 0; j < 8; ++j) { best[j] = -FLT_MAX; arg[j] = -1; tk[j] = 0; }
   if (nc < 8) {  // channel tail (not reached with C % 8 == 0)
     for (int kh = 0; kh < 3; ++kh) {
       const int iy = oy * 2 - pt + kh;
@@ -357,9 +359,12 @@ __device__ __forceinline__ void pool_window(const edet_lazy& lz, const float2* a
         lazy_load8<T>(lz, af, img_row0 + (size_t)iy * W + ix, c, nc, v);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (arg[j] < 0 || v[j] > best[j]) { best[j] = v[j]; arg[j] = iy * W + ix; }
+          if (arg[j] < 0 || v[j] > best[j]) { best[j] = v[j]; arg[j] = iy * W + ix; tk[j] = kh * 3 + kw; }
       }
     }
+    if (tap)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tap[j] = tk[j];
     return;
   }
   // all nine taps are loaded first (select-predicated addresses: a load inside a divergent
@@ -380,9 +385,31 @@ __device__ __forceinline__ void pool_window(const edet_lazy& lz, const float2* a
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float t = lazy_apply(v[k][j], af[j], lz.act);
-      if (arg[j] < 0 || t > best[j]) { best[j] = t; arg[j] = pos; }
+      if (arg[j] < 0 || t > best[j]) { best[j] = t; arg[j] = pos; tk[j] = k; }
     }
   }
+  if (tap)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tap[j] = tk[j];
+}
+
+// the 8 window taps of a stored argmax vector (one byte per channel)
+__device__ __forceinline__ void load_taps(const uint8_t* p, int* tap) {
+  const uint2 w = *reinterpret_cast<const uint2*>(p);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    tap[j] = (w.x >> (8 * j)) & 0xff;
+    tap[4 + j] = (w.y >> (8 * j)) & 0xff;
+  }
+}
+__device__ __forceinline__ void store_taps(uint8_t* p, const int* tap) {
+  uint2 w = make_uint2(0u, 0u);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    w.x |= (uint32_t)tap[j] << (8 * j);
+    w.y |= (uint32_t)tap[4 + j] << (8 * j);
+  }
+  *reinterpret_cast<uint2*>(p) = w;
 }
 
 // per-channel lazy-BN affine of each input, once per block into LDS (was recomputed per
@@ -423,14 +450,30 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(edet_lazy lz, int B, int H,
 
 // gather form of the max-pool backward: input pixel collects dy of every window whose
 // (recomputed) argmax is this pixel
+// (or, given the forward's stored taps `parg`, reads them instead of re-evaluating windows)
 template <typename T>
 __device__ __forceinline__ void pool_bwd_gather(const edet_lazy& lz, const float2* af, const T* dy, size_t img_row0,
                                                 size_t out_row0, int H, int W, int OH, int OW, int C, int iy, int ix,
-                                                int c, float scale, float* d) {
+                                                int c, float scale, float* d, const uint8_t* parg = nullptr) {
   const int pt = same_pad(H, 3, 2), pl = same_pad(W, 3, 2);
   const int oy_lo = max(0, fdiv(iy + pt - 2 + 1, 2)), oy_hi = min(OH - 1, fdiv(iy + pt, 2));
   const int ox_lo = max(0, fdiv(ix + pl - 2 + 1, 2)), ox_hi = min(OW - 1, fdiv(ix + pl, 2));
   const int me = iy * W + ix;
+  if (parg) {
+    for (int oy = oy_lo; oy <= oy_hi; ++oy)
+      for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+        const size_t o = out_row0 + (size_t)oy * OW + ox;
+        int tap[8];
+        load_taps(parg + o * C + c, tap);
+        float g[8];
+        ld8(dy + o * C + c, g);
+        const int kme = (iy - (oy * 2 - pt)) * 3 + (ix - (ox * 2 - pl));
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (tap[j] == kme) d[j] += g[j] * scale;
+      }
+    return;
+  }
   for (int oy = oy_lo; oy <= oy_hi; ++oy)
     for (int ox = ox_lo; ox <= ox_hi; ++ox) {
       float best[8];
@@ -480,9 +523,12 @@ struct FuseArgs {
 };
 
 // resampled value of input i at output pixel (n, h, w), 8 channels from c
+// MAXPOOL with fi.pool_arg: `store` (forward) writes the window taps of output pixel `pix`;
+// otherwise (backward) they are read and only the 8 winning taps are loaded and transformed
 template <typename T>
 __device__ __forceinline__ void fuse_input_value(const edet_fuse_input& fi, const float2* af, int n, int h, int w,
-                                                 int OH, int OW, int c, float* v) {
+                                                 int OH, int OW, int c, float* v, size_t pix = 0, int C = 0,
+                                                 bool store = false) {
   const int Hi = fi.H, Wi = fi.W;
   const size_t r0 = (size_t)n * Hi * Wi;
   if (fi.mode == EDET_MODE_SAME) {
@@ -490,9 +536,20 @@ __device__ __forceinline__ void fuse_input_value(const edet_fuse_input& fi, cons
   } else if (fi.mode == EDET_MODE_UPSAMPLE) {
     const int iy = nearest_src(h, Hi, OH), ix = nearest_src(w, Wi, OW);
     lazy_load8<T>(fi.v, af, r0 + (size_t)iy * Wi + ix, c, 8, v);
+  } else if (fi.pool_arg && !store) {
+    int tap[8];
+    load_taps(fi.pool_arg + pix * C + c, tap);
+    const int y0 = h * 2 - same_pad(Hi, 3, 2), x0 = w * 2 - same_pad(Wi, 3, 2);
+    const T* X = (const T*)fi.v.x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const size_t row = r0 + (size_t)(y0 + tap[j] / 3) * Wi + (x0 + tap[j] % 3);
+      v[j] = lazy_apply(to_f<T>(X[row * fi.v.ld + c + j]), af[j], fi.v.act);
+    }
   } else {
-    int arg[8];
-    pool_window<T>(fi.v, af, r0, Hi, Wi, same_pad(Hi, 3, 2), same_pad(Wi, 3, 2), h, w, c, 8, v, arg);
+    int arg[8], tap[8];
+    pool_window<T>(fi.v, af, r0, Hi, Wi, same_pad(Hi, 3, 2), same_pad(Wi, 3, 2), h, w, c, 8, v, arg, tap);
+    if (store && fi.pool_arg) store_taps(fi.pool_arg + pix * C + c, tap);
   }
 }
 
@@ -523,7 +580,7 @@ __global__ __launch_bounds__(256) void k_fuse_fwd(FuseArgs g) {
     float2 af[8];
     affine8_lds(aft + i * g.C, cv * 8, af);
     float v[8];
-    fuse_input_value<T>(fi, af, n, h, w, g.H, g.W, cv * 8, v);
+    fuse_input_value<T>(fi, af, n, h, w, g.H, g.W, cv * 8, v, (size_t)pix, g.C, true);
     const float wi = g.w[i];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -565,7 +622,7 @@ __global__ __launch_bounds__(256) void k_fuse_bwd(FuseArgs g) {
         float2 af[8];
         affine8_lds(aft + i * g.C, cv * 8, af);
         float v[8];
-        fuse_input_value<T>(fi, af, n, h, w, g.H, g.W, cv * 8, v);
+        fuse_input_value<T>(fi, af, n, h, w, g.H, g.W, cv * 8, v, (size_t)pix, g.C, false);
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += dF[j] * (v[j] - F[j]);
@@ -623,7 +680,8 @@ __global__ __launch_bounds__(256) void k_fuse_bwd(FuseArgs g) {
   } else {
     float2 af[8];
     affine8_lds(aft + i * g.C, cv * 8, af);
-    pool_bwd_gather<T>(fi.v, af, dF, (size_t)n * Hi * Wi, o0, Hi, Wi, g.H, g.W, g.C, iy, ix, cv * 8, wn, d);
+    pool_bwd_gather<T>(fi.v, af, dF, (size_t)n * Hi * Wi, o0, Hi, Wi, g.H, g.W, g.C, iy, ix, cv * 8, wn, d,
+                       fi.pool_arg);
   }
   acc8m((T*)fi.dx + (size_t)pix * g.C + cv * 8, 8, d, fi.accumulate);
 }

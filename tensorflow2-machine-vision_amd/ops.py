@@ -231,10 +231,15 @@ def bifpn_fuse(eng: Engine, P: ParamStore, inputs: Sequence[Tuple[Act, int]], wn
     wvec = P.view(wnames[0])  # the node's WSM_0..WSM_{n-1} scalars as one [n] parameter
     assert wvec.numel() == n
     fi = (L.FuseInput * n)()
+    # max-pooled inputs: the forward records each output's window tap (1 byte per element)
+    # so the backward neither re-evaluates the 3x3 windows nor re-applies their lazy BN/swish
+    taps = [eng.empty(B * H * W, C, dtype=torch.uint8) if (mode == L.MODE_MAXPOOL and eng.training) else None
+            for (_, mode) in inputs]
     for i, (a, mode) in enumerate(inputs):
         assert a.pyr.nseg == 1 and a.C == C
         fi[i].v = a.lazy()
         fi[i].H, fi[i].W, fi[i].mode = a.pyr.H, a.pyr.W, mode
+        fi[i].pool_arg = taps[i].data_ptr() if taps[i] is not None else None
     pyr = Pyr(B, [(H, W)])
     y = eng.empty(pyr.rows, C)
     L.call("edet_bifpn_fuse_fwd", eng.dt, n, fi, vp(wvec), B, H, W, C, vp(y), stream())
@@ -252,6 +257,7 @@ def bifpn_fuse(eng: Engine, P: ParamStore, inputs: Sequence[Tuple[Act, int]], wn
             fb[i].H, fb[i].W, fb[i].mode = a.pyr.H, a.pyr.W, mode
             fb[i].dx = dx.data_ptr()
             fb[i].accumulate = acc
+            fb[i].pool_arg = taps[i].data_ptr() if taps[i] is not None else None
         L.call("edet_bifpn_fuse_bwd", eng.dt, n, fb, vp(wvec), B, H, W, C, vp(y), vp(dF),
                vp(P.grad(wnames[0])), stream())
 

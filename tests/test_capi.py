@@ -28,13 +28,13 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.Pyramid) == 4 * (2 + 3 * 5)
     assert ctypes.sizeof(_lib.BN) == 8 * 20 + 8
     assert ctypes.sizeof(_lib.Lazy) == 8 + 8 + ctypes.sizeof(_lib.BN) + 8
-    assert ctypes.sizeof(_lib.FuseInput) == ctypes.sizeof(_lib.Lazy) + 8 + 16
+    assert ctypes.sizeof(_lib.FuseInput) == ctypes.sizeof(_lib.Lazy) + 8 + 16 + 8  # + pool_arg
     assert ctypes.sizeof(_lib.Sched) == 40
 
 
 def test_error_path_without_gpu():
     lib = _lib.lib()
-    assert lib.fns["edet_abi_version"]() == 2
+    assert lib.fns["edet_abi_version"]() == 3
     # argument validation happens before any HIP call
     rc = lib.fns["edet_conv1x1_fwd"](0, None, None, 8, None, 8, None, None, 8, 0, None, None)
     assert rc == -1 and "null" in lib.last_error()

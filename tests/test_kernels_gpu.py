@@ -332,6 +332,49 @@ def test_bifpn_fuse(dt):
 
 
 @pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("pool_in", [(16, 14), (15, 13)])
+def test_bifpn_fuse_stored_pool_taps(dt, pool_in):
+    """The forward's recorded max-pool window taps (edet_fuse_input.pool_arg) give the same
+    backward as re-evaluating the windows: input gradients bit-exact, the weight gradient up to
+    the order of its cross-block fp32 atomics."""
+    rng = np.random.default_rng(12)
+    B, C, H, W = 2, 64, 8, 7
+    specs = [((H, W), L.MODE_SAME), (pool_in, L.MODE_MAXPOOL)]
+    assert all(((h + 1) // 2, (w + 1) // 2) == (H, W) for (h, w), m in specs if m == L.MODE_MAXPOOL)
+    descs = []
+    for i, ((h, w), mode) in enumerate(specs):
+        pyr = Pyr(B, [(h, w)])
+        x = pyr_data(rng, pyr, C, dt, scale=2.0)
+        descs.append((LazyDesc(x, pyr, C, bn=make_bn(x, pyr, C, rng), act=1), pyr, h, w, mode))
+    wv = g(torch.tensor([0.9, 1.2]))
+    dout = g(rnd(rng, B * H * W, C), dt)
+    res = []
+    for stored in (False, True):
+        taps = torch.full((B * H * W, C), 77, dtype=torch.uint8, device=DEV)
+        fi = (L.FuseInput * 2)()
+        dxs = []
+        for i, (d, pyr, h, w, mode) in enumerate(descs):
+            fi[i].v, fi[i].H, fi[i].W, fi[i].mode = d.c, h, w, mode
+            dx = torch.zeros(pyr.rows, C, dtype=TDT[dt], device=DEV)
+            dxs.append(dx)
+            fi[i].dx, fi[i].accumulate = dx.data_ptr(), 0
+            fi[i].pool_arg = taps.data_ptr() if (stored and mode == L.MODE_MAXPOOL) else None
+        out = torch.empty(B * H * W, C, dtype=TDT[dt], device=DEV)
+        L.call("edet_bifpn_fuse_fwd", DT[dt], 2, fi, vp(wv), B, H, W, C, vp(out), stream())
+        dw = zeros(2)
+        L.call("edet_bifpn_fuse_bwd", DT[dt], 2, fi, vp(wv), B, H, W, C, vp(out), vp(dout), vp(dw), stream())
+        torch.cuda.synchronize()
+        if stored:
+            assert int(taps.max()) <= 8  # every output recorded a tap of its 3x3 window
+        res.append((out.clone(), [d.clone() for d in dxs], dw.clone()))
+    (o0, d0, w0), (o1, d1, w1) = res
+    assert torch.equal(o0, o1)
+    for a, b in zip(d0, d1):
+        assert torch.equal(a, b)
+    assert torch.allclose(w0, w1, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("kind", ["gate", "pyramid"])
 def test_lazy_materialize(dt, kind):
     rng = np.random.default_rng(31)
