@@ -18,6 +18,8 @@ from __future__ import annotations
 
 from typing import List, Optional, Sequence, Tuple
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -109,6 +111,11 @@ def stem(eng: Engine, P: ParamStore, x: torch.Tensor, wname: str, bn: BNParam) -
 
 
 # --------------------------------------------------------------------------- 1x1 conv
+# output width from which the weight gradient reads a materialized copy of a lazy A operand
+# (scripts/kbench.py; EDET_WGRAD_MATERIALIZE_N overrides for A/B timing)
+WGRAD_MATERIALIZE_N = int(os.environ.get("EDET_WGRAD_MATERIALIZE_N", "64"))
+
+
 def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optional[str] = None,
             bns: Optional[List[BNParam]] = None, act: int = L.ACT_NONE, ldy: Optional[int] = None,
             out_buf: Optional[torch.Tensor] = None, name: str = "") -> Act:
@@ -127,7 +134,15 @@ def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optio
             return
         d, ld = value_grad_to_raw(eng, out, rec)
         with eng.side(x.raw, x.gate, d):
-            L.call("edet_conv1x1_wgrad", eng.dt, x.lazy(), x.pyr.c, K, vp(d), ld, N, vp(P.grad(wname)),
+            a = x.lazy()
+            if N >= WGRAD_MATERIALIZE_N and x.has_transform:
+                # the weight gradient re-applies A's lazy transform once per 64-column tile
+                # (N/64 times); for wide outputs one materialize pass is cheaper (same bf16
+                # operand the kernel would stage, so dW is unchanged)
+                xa = eng.empty(x.pyr.rows, K)
+                L.call("edet_lazy_materialize", eng.dt, a, x.pyr.c, K, vp(xa), stream())
+                a = Act(xa, x.pyr, K).lazy()
+            L.call("edet_conv1x1_wgrad", eng.dt, a, x.pyr.c, K, vp(d), ld, N, vp(P.grad(wname)),
                    vp(P.grad(bname) if bname else None), stream())
         s = stream()
         dx, acc = eng.tape.dst(x)
