@@ -374,12 +374,17 @@ def main():
     if args.workload == "backbone":
         return bench_backbone(args)
 
+    # EDET_DP_BACKEND=gloo with more ranks than GPUs rehearses the N > 1 path on one GPU
+    # (ranks share devices round-robin); the default is one rank per GPU over RCCL
+    backend = os.environ.get("EDET_DP_BACKEND", "nccl")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     from tf2mv_amd import dist as dp
 
-    ctx = dp.init_from_env("nccl", dev)  # RCCL over xGMI for N > 1
+    ctx = dp.init_from_env(backend, dev)  # RCCL over xGMI for N > 1
     world, rank = ctx.world, ctx.rank
 
     from tf2mv_amd.anchors import Anchors
