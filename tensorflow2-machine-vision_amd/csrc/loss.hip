@@ -42,15 +42,17 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 
 // focal loss value and d/dx for one logit (focal_loss.py:42-52, TF sigmoid CE formulation)
 __device__ __forceinline__ void focal_elem(float x, float y, float alpha, float gamma, bool g15, float& fl, float& dfl) {
+  // v_rcp_f32 / v_sqrt_f32 (1 ulp) instead of the correctly rounded division and square root
+  // the build flags select for '/' and sqrtf: this kernel is VALU-bound over 127 M logits
   const float z = __expf(-fabsf(x));
-  const float r = 1.f / (1.f + z);
+  const float r = __builtin_amdgcn_rcpf(1.f + z);
   const float p = x >= 0.f ? r : z * r;                  // sigmoid(x)
   const float pt = y * p + (1.f - y) * (1.f - p);
   const float at = y * alpha + (1.f - y) * (1.f - alpha);
   const float om = fmaxf(1.f - pt, 0.f);
   float mod, dmodf;                                      // (1-pt)^g and g*(1-pt)^(g-1)
   if (g15) {
-    const float sq = sqrtf(om);
+    const float sq = __builtin_amdgcn_sqrtf(om);
     mod = om * sq;
     dmodf = 1.5f * sq;
   } else {
@@ -91,13 +93,18 @@ __global__ __launch_bounds__(256) void k_loss(LossArgs g) {
         float x[8], d[8];
         ld8(px, x);
         const int32_t* tr = g.cls_t + (size_t)m * g.A;
+        // (anchor, class) of the vector's first column; the next 7 step without a division
+        // and, with NC >= 8, stay within two anchors whose targets are read once
+        const int a0 = cv / g.NC;
+        int a = a0, c = cv - a0 * g.NC;
+        const int ta = tr[a0], tb = (a0 + 1 < g.A) ? tr[a0 + 1] : -1;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int col = cv + j;
           d[j] = 0.f;
+          if (j > 0 && ++c == g.NC) { c = 0; ++a; }
           if (col < AN) {
-            const int a = col / g.NC, c = col - a * g.NC;
-            const float y = (tr[a] == c) ? 1.f : 0.f;
+            const float y = ((g.NC >= 8 ? (a == a0 ? ta : tb) : tr[a]) == c) ? 1.f : 0.f;
             float fl, dfl;
             focal_elem(x[j], y, g.alpha, g.gamma, g15, fl, dfl);
             s += fl;
