@@ -581,10 +581,10 @@ __global__ __launch_bounds__(256) void k_fuse_fwd(FuseArgs g) {
     affine8_lds(aft + i * g.C, cv * 8, af);
     float v[8];
     fuse_input_value<T>(fi, af, n, h, w, g.H, g.W, cv * 8, v, (size_t)pix, g.C, true);
-    const float wi = g.w[i];
+    const float wn = g.w[i] / den;  // one division per input, not per element
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float t = v[j] * wi / den;
+      const float t = v[j] * wn;
       o[j] = (i == 0) ? t : o[j] + t;
     }
   }
@@ -607,6 +607,7 @@ __global__ __launch_bounds__(256) void k_fuse_bwd(FuseArgs g) {
     // walks the pixels and keeps partials in registers: one block per 256 vectors put
     // thousands of same-address atomics on the 3 weights.
     float part[3] = {0.f, 0.f, 0.f};
+    const float rden = 1.f / den;
     const long total = (long)g.B * g.H * g.W * nv;
     for (long idx = (long)b * 256 + tid; idx < total; idx += (long)g.nb_w * 256) {
       const int cv = (int)(idx % nv);
@@ -626,7 +627,7 @@ __global__ __launch_bounds__(256) void k_fuse_bwd(FuseArgs g) {
         float s = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += dF[j] * (v[j] - F[j]);
-        part[i] += s / den;
+        part[i] += s * rden;
       }
     }
     for (int i = 0; i < g.n_in; ++i) {
