@@ -456,29 +456,43 @@ __global__ __launch_bounds__(256) void k_se_dz1(int B, int C, int R, const float
   }
 }
 
-// backward, pass 2 (one thread per element of the largest output):
+// backward, pass 2 (dw2 / dw1: a half-wave per (c, r) over the images; dsq, db2, db1: a thread
+// per element):
 //   dw2[c][r] += sum_n dz2[n][c] swish(z1[n][r])     dw1[r][c] += sum_n dz1[n][r] s[n][c]
 //   db2[c]    += sum_n dz2[n][c]                     db1[r]    += sum_n dz1[n][r]
 //   dsq[n][c]  = sum_r dz1[n][r] w1[r][c] / HW
-__global__ __launch_bounds__(256) void k_se_wgrad(int B, int C, int R, int HW, const double* s, const float* z1,
-                                                  const float* gate, const double* dgate, const float* dz1,
-                                                  const float* w1, float* dw1, float* db1, float* dw2, float* db2,
-                                                  float* dsq) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx < C * R) {
-    const int c = idx / R, r = idx - c * R;
+__global__ __launch_bounds__(256) void k_se_wgrad(int B, int C, int R, int HW, int nA, const double* s,
+                                                  const float* z1, const float* gate, const double* dgate,
+                                                  const float* dz1, const float* w1, float* dw1, float* db1,
+                                                  float* dw2, float* db2, float* dsq) {
+  if ((int)blockIdx.x < nA) {
+    // dw2[c][r], dw1[r][c]: one half-wave per (c, r), its 32 lanes over the images, then a
+    // 32-lane tree (the per-thread loop over B serialised B dependent load rounds)
+    const int half = threadIdx.x >> 5, ln = threadIdx.x & 31;
+    const int item = blockIdx.x * 8 + half;
     float a2 = 0.f, a1 = 0.f;
-#pragma unroll 8
-    for (int n = 0; n < B; ++n) {
-      const float gv = gate[(size_t)n * C + c];
-      const float d2 = (float)dgate[(size_t)n * C + c] * gv * (1.f - gv);
-      const float z = z1[(size_t)n * R + r];
-      a2 += d2 * (z * sigmoidf_(z));
-      a1 += dz1[(size_t)n * R + r] * (float)s[(size_t)n * C + c];
+    const bool live = item < C * R;
+    const int c = live ? item / R : 0, r = live ? item - c * R : 0;
+    if (live)
+      for (int n = ln; n < B; n += 32) {
+        const float gv = gate[(size_t)n * C + c];
+        const float d2 = (float)dgate[(size_t)n * C + c] * gv * (1.f - gv);
+        const float z = z1[(size_t)n * R + r];
+        a2 += d2 * (z * sigmoidf_(z));
+        a1 += dz1[(size_t)n * R + r] * (float)s[(size_t)n * C + c];
+      }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      a2 += __shfl_xor(a2, o, 64);
+      a1 += __shfl_xor(a1, o, 64);
     }
-    dw2[(size_t)c * R + r] += a2;
-    dw1[(size_t)r * C + c] += a1;
+    if (live && ln == 0) {
+      dw2[(size_t)c * R + r] += a2;
+      dw1[(size_t)r * C + c] += a1;
+    }
+    return;
   }
+  const int idx = (blockIdx.x - nA) * 256 + threadIdx.x;
   if (idx < B * C) {
     const int n = idx / C, c = idx - n * C;
     float a = 0.f;
@@ -752,8 +766,8 @@ int edet_se_bwd(int B, int C, int R, int HW, const double* s, const float* z1,
                "se_bwd: null argument");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_se_dz1, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, z1, gate, dgate, w2, dz1);
-  const int n = std::max(C * R, B * C);
-  hipLaunchKernelGGL(k_se_wgrad, dim3(cdiv(n, 256)), dim3(256), 0, st, B, C, R, HW, s, z1, gate, dgate, dz1, w1,
+  const int nA = cdiv(C * R, 8), nB = cdiv(std::max(B * C, std::max(C, R)), 256);
+  hipLaunchKernelGGL(k_se_wgrad, dim3(nA + nB), dim3(256), 0, st, B, C, R, HW, nA, s, z1, gate, dgate, dz1, w1,
                      dw1, db1, dw2, db2, dsq);
   return check_launch("edet se_bwd");
 }
