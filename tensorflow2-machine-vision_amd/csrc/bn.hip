@@ -386,18 +386,27 @@ __global__ __launch_bounds__(256) void k_gate_bn_reduce(LArgs g) {
 
 __global__ __launch_bounds__(256) void k_se_bn_combine(int B, int C, const float* gate, const float* dsq,
                                                        const double* s5, double* dgamma, double* dbeta) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  // a half-wave per channel, its lanes over the images (one thread looping B images was B
+  // dependent load rounds on a handful of blocks)
+  const int half = threadIdx.x >> 5, ln = threadIdx.x & 31;
+  const int c = blockIdx.x * 8 + half;
   double gb = 0.0, gg = 0.0;
-#pragma unroll 8
-  for (int n = 0; n < B; ++n) {
-    const double gt = gate[(size_t)n * C + c], ds = dsq[(size_t)n * C + c];
-    const size_t i = (size_t)n * C + c, BC = (size_t)B * C;
-    gb += gt * s5[1 * BC + i] + ds * s5[2 * BC + i];
-    gg += gt * s5[3 * BC + i] + ds * s5[4 * BC + i];
+  if (c < C)
+    for (int n = ln; n < B; n += 32) {
+      const double gt = gate[(size_t)n * C + c], ds = dsq[(size_t)n * C + c];
+      const size_t i = (size_t)n * C + c, BC = (size_t)B * C;
+      gb += gt * s5[1 * BC + i] + ds * s5[2 * BC + i];
+      gg += gt * s5[3 * BC + i] + ds * s5[4 * BC + i];
+    }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) {
+    gb += __shfl_xor(gb, o, 64);
+    gg += __shfl_xor(gg, o, 64);
   }
-  dbeta[c] += gb;
-  dgamma[c] += gg;
+  if (c < C && ln == 0) {
+    dbeta[c] += gb;
+    dgamma[c] += gg;
+  }
 }
 
 // SE excite: z1 = W1 s + b1 ; gate = sigmoid(W2 swish(z1) + b2)   (layers/se.py:36-39).
@@ -743,7 +752,7 @@ int edet_gate_bn_reduce(int dtype, const edet_lazy* x, int B, int HW, int C, con
 int edet_se_bn_combine(int B, int C, const float* gate, const float* dsq, const double* sums5,
                        const edet_bngrad64* acc, edet_stream_t stream) {
   EDET_REQUIRE(gate && dsq && sums5 && acc && acc->dgamma[0] && acc->dbeta[0], "se_bn_combine: null argument");
-  hipLaunchKernelGGL(k_se_bn_combine, dim3(cdiv(C, 256)), dim3(256), 0, (hipStream_t)stream, B, C, gate, dsq, sums5,
+  hipLaunchKernelGGL(k_se_bn_combine, dim3(cdiv(C, 8)), dim3(256), 0, (hipStream_t)stream, B, C, gate, dsq, sums5,
                      acc->dgamma[0], acc->dbeta[0]);
   return check_launch("edet se_bn_combine");
 }
