@@ -793,6 +793,14 @@ __global__ __launch_bounds__(256) void k_dw2_dgrad(DwArgs g, DwGeom geo) {
 template <int CPT, typename T> __device__ __forceinline__ void ldv(const T* p, float* o) {
   if constexpr (CPT == 8) {
     ld8(p, o);
+  } else if constexpr (CPT == 2) {
+    if constexpr (sizeof(T) == 2) {
+      const uint32_t v = *reinterpret_cast<const uint32_t*>(p);
+      o[0] = __uint_as_float(v << 16); o[1] = __uint_as_float(v & 0xffff0000u);
+    } else {
+      const float2 a = *reinterpret_cast<const float2*>(p);
+      o[0] = a.x; o[1] = a.y;
+    }
   } else if constexpr (sizeof(T) == 2) {
     uint2 v = *reinterpret_cast<const uint2*>(p);
     o[0] = __uint_as_float(v.x << 16); o[1] = __uint_as_float(v.x & 0xffff0000u);
@@ -805,6 +813,9 @@ template <int CPT, typename T> __device__ __forceinline__ void ldv(const T* p, f
 template <int CPT, typename T> __device__ __forceinline__ void stv(T* p, const float* v) {
   if constexpr (CPT == 8) {
     st8(p, v);
+  } else if constexpr (CPT == 2) {
+    if constexpr (sizeof(T) == 2) *reinterpret_cast<uint32_t*>(p) = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    else *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
   } else if constexpr (sizeof(T) == 2) {
     *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
                                               (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
@@ -819,7 +830,7 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo) {
   constexpr int DLO = -((K - 1) / S), DHR = (PH - 1) / S, DHC = (PW - 1) / S;
   const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
   if (rr >= geo.R) return;
-  const int c = tv * CPT, C = g.C;
+  const int c = (blockIdx.y * geo.TPR + tv) * CPT, C = g.C;  // channel blocks over blockIdx.y
   const T* DY = (const T*)g.dy;
   T* DX = (T*)g.dx;
   float w[K * K][CPT];
@@ -895,9 +906,17 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo) {
 
 template <typename T, int K, int S>
 static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s) {
-  constexpr int CPT = K == 3 ? 8 : 4;
+#ifndef EDET_DW4_K5_CPT
+#define EDET_DW4_K5_CPT 4
+#endif
+  // k5: 4 channels per thread (25 fp32 weights each in registers); 2 channels measured
+  // faster only at C = 1152 (EDET_DW4_K5_CPT, A/B)
+  constexpr int CPT = K == 3 ? 8 : EDET_DW4_K5_CPT;
   DwGeom geo;
-  geo.TPR = g.C / CPT;
+  // channel vectors per pixel row split over blockIdx.y until a row fits a block
+  int ncs = 1;
+  while (g.C / CPT / ncs > 256 || (g.C / CPT) % ncs) ++ncs;
+  geo.TPR = g.C / CPT / ncs;
   geo.R = std::max(1, 256 / geo.TPR);
   long patches = 0;
   for (int i = 0; i < g.pin.nseg; ++i) {
@@ -905,7 +924,7 @@ static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s) {
     patches += (long)g.pin.batch * cdiv(g.pin.H[i] + pt, 2) * cdiv(g.pin.W[i] + pl, 2);
   }
   const int grid = (int)std::max<long>(1, std::min<long>(4096, (patches + geo.R - 1) / geo.R));
-  if (patches) hipLaunchKernelGGL((k_dw4_dgrad<T, K, S, CPT, 2, 2>), dim3(grid), dim3(geo.TPR * geo.R), 0, s, g, geo);
+  if (patches) hipLaunchKernelGGL((k_dw4_dgrad<T, K, S, CPT, 2, 2>), dim3(grid, ncs), dim3(geo.TPR * geo.R), 0, s, g, geo);
   return check_launch("edet dwconv dgrad");
 }
 
@@ -942,7 +961,7 @@ static int dw_env_grid(int which) {
 static DwForm dw_form(int which, int K, int S, int C) {
   static const int force[3] = {dw_env("EDET_DW_FWD"), dw_env("EDET_DW_DGRAD"), dw_env("EDET_DW_WGRAD")};
   const bool direct_ok = C <= 2048;
-  const bool dw4_ok = C / (K == 3 ? 8 : 4) <= 256;
+  const bool dw4_ok = C % 8 == 0;  // channel rows split over blockIdx.y past 256 vectors
   int f = force[which];
   if (which == 0) {
     if (f == DW_TILE || f == DW_DW3 || (f == DW_DIRECT && direct_ok)) return (DwForm)f;
