@@ -1232,6 +1232,183 @@ static int dispatch_pwb(const GemmArgs& g, hipStream_t s, bool& done) {
   return launch_pwb<T, 1, true, LAZY>(g, p, s);
 }
 
+// ------------------------------------------------------------------ wave-streaming small-K GEMM
+// For K <= 32 (the stage 0-1 convs: 2M x 16 -> 96, 524K x 24 -> 144, 2M x 32 -> 16) the
+// GEMM is a pure stream: the outputs are 3-6x the inputs.  Every wave works alone, with no
+// LDS and no barrier in the row loop: it keeps the weights as MFMA A-fragments in registers
+// (W[n][k], 16 channels per fragment, K zero-padded to 32) and for each 16-row group loads its
+// A rows straight into the B-fragment layout (lane = row, 8 consecutive k), applies the lazy
+// BN/act/gate transform in registers, and issues one v_mfma_f32_16x16x32_bf16 per fragment.
+// With A as the B operand each lane holds 4 consecutive output channels of one row: 8-byte
+// stores, whole rows written by one wave back to back.  BN statistics stay in registers per
+// lane until the end (one lane tree, one LDS pass and one fp64 atomic per channel per block).
+#ifndef EDET_GS_PF
+#define EDET_GS_PF 2
+#endif
+constexpr int GS_PF = EDET_GS_PF;  // row groups in flight ahead of the one being computed
+template <typename T, int NF, bool LAZY>
+__global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
+  __shared__ float red[2][4][NF * 16];
+  constexpr int LDW = NF * 16 + 8;  // wave-private output staging row (bf16), padded
+  __shared__ __attribute__((aligned(16))) uint16_t stg[4][16 * LDW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint16_t* cw = stg[wave];
+  const int kq = 8 * (lane >> 4);  // this lane's 8 k values
+  const int K = g.K, N = g.N, M = g.M;
+  const T* A = (const T*)g.a;
+  const T* Wt = (const T*)g.b;
+  T* Y = (T*)g.c;
+  // weights: fragment f holds W[16 f + (lane & 15)][kq .. kq + 8]
+  bf16x8_t wf[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const int n = 16 * f + (lane & 15);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (n < N && kq < K) v = *reinterpret_cast<const uint4*>(Wt + (size_t)n * g.ldb + kq);
+    wf[f] = __builtin_bit_cast(bf16x8_t, v);
+  }
+  float bias[NF][4];
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = 16 * f + 4 * (lane >> 4) + r;
+      bias[f][r] = (g.bias && n < N) ? g.bias[n] : 0.f;
+    }
+  float2 af[8];
+  if constexpr (LAZY) {
+    const float inv = 1.f / (float)M;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) af[j] = kq + j < K ? bn_affine(g.lz.bn, 0, kq + j, inv) : make_float2(1.f, 0.f);
+  }
+  const int hw = g.pyr.H[0] * g.pyr.W[0];
+  float ss[NF][4], sq[NF][4];
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { ss[f][r] = 0.f; sq[f][r] = 0.f; }
+  const int ngroups = (M + 15) / 16, gstride = gridDim.x * 4;
+  // the next groups' A rows are fetched before this group's stores are issued (vmcnt
+  // counts loads and stores in order: a load issued after the stores would wait for them)
+  auto fetch = [&](int grp) {
+    const int row = grp * 16 + (lane & 15);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (kq < K && grp < ngroups) v = *reinterpret_cast<const uint4*>(A + (size_t)(row < M ? row : 0) * g.lda + kq);
+    return v;
+  };
+  uint4 pre[GS_PF];
+#pragma unroll
+  for (int u = 0; u < GS_PF; ++u) pre[u] = fetch(blockIdx.x * 4 + wave + u * gstride);
+  for (int grp = blockIdx.x * 4 + wave; grp < ngroups; grp += gstride) {
+    const int row = grp * 16 + (lane & 15);
+    const bool live = row < M;
+    uint4 raw = pre[0];
+#pragma unroll
+    for (int u = 0; u + 1 < GS_PF; ++u) pre[u] = pre[u + 1];
+    pre[GS_PF - 1] = fetch(grp + GS_PF * gstride);
+    if constexpr (LAZY) {
+      float x[8];
+      const uint32_t w4[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        x[2 * i] = __uint_as_float(w4[i] << 16);
+        x[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+      }
+      float gt[8];
+      if (g.lz.gate && kq < K) ld8(g.lz.gate + (size_t)((live ? row : 0) / hw) * K + kq, gt);
+      uint16_t o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float u = lazy_apply(x[j], af[j], g.lz.act);
+        if (g.lz.gate) u *= (kq < K ? gt[j] : 0.f);
+        o[j] = kq + j < K ? f2bf(u) : (uint16_t)0;
+      }
+      raw = *reinterpret_cast<uint4*>(o);
+    }
+    const bf16x8_t bfrag = __builtin_bit_cast(bf16x8_t, raw);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      floatx4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[f], bfrag, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const int n0 = 16 * f + 4 * (lane >> 4);
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = d[r] + bias[f][r];
+        if (live) { ss[f][r] += v[r]; sq[f][r] += v[r] * v[r]; }
+      }
+      *reinterpret_cast<uint2*>(cw + (lane & 15) * LDW + n0) =
+          make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+    }
+    // the 16 x N tile leaves as 16-byte vectors, a whole row range per store instruction
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int vpr = N / 8, row0 = grp * 16;
+    for (int e = lane; e < 16 * vpr; e += 64) {
+      const int rl = e / vpr, c8 = (e - rl * vpr) * 8;
+      if (row0 + rl < M)
+        *reinterpret_cast<uint4*>(Y + (size_t)(row0 + rl) * g.ldc + c8) = *reinterpret_cast<const uint4*>(cw + rl * LDW + c8);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (!g.has_stats) return;  // block-uniform
+  // lanes sharing (lane >> 4) hold the same 4 channels of 16 different rows
+#pragma unroll
+  for (int f = 0; f < NF; ++f)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a = ss[f][r], b = sq[f][r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
+      if ((lane & 15) == 0) {
+        red[0][wave][16 * f + 4 * (lane >> 4) + r] = a;
+        red[1][wave][16 * f + 4 * (lane >> 4) + r] = b;
+      }
+    }
+  __syncthreads();
+  for (int n = threadIdx.x; n < N; n += 256) {
+    const float a = (red[0][0][n] + red[0][1][n]) + (red[0][2][n] + red[0][3][n]);
+    const float b = (red[1][0][n] + red[1][1][n]) + (red[1][2][n] + red[1][3][n]);
+    stat_add(g.stats.sum[0] + n, (double)a);
+    stat_add(g.stats.sq[0] + n, (double)b);
+  }
+}
+
+template <typename T, bool LAZY, int NF>
+static int launch_gemm_s(const GemmArgs& g, hipStream_t s) {
+  static const int blk_env = getenv("EDET_GS_BLOCKS") ? atoi(getenv("EDET_GS_BLOCKS")) : 0;  // A/B only
+  const int ngroups = (g.M + 15) / 16;
+  // 512 blocks (2 per CU): measured best over 512..2048 in the D0 step (scripts/kbench.py)
+  const int grid = std::max(1, std::min(cdiv(ngroups, 4), blk_env > 0 ? blk_env : 512));
+  hipLaunchKernelGGL((k_gemm_s<T, NF, LAZY>), dim3(grid), dim3(256), 0, s, g);
+  return check_launch("edet gemm_s");
+}
+
+// K <= 32, N <= 160 (NF <= 10 fragments), one segment, bf16, plain store
+template <typename T, bool LAZY>
+static int dispatch_gemm_s(const GemmArgs& g, hipStream_t s, bool& done) {
+  done = false;
+  static const int off = getenv("EDET_NO_GEMM_S") ? atoi(getenv("EDET_NO_GEMM_S")) : 0;  // A/B only
+  if (off || sizeof(T) != 2 || g.K > 32 || g.K % 8 || g.N > 160 || g.N % 8 || g.pyr.nseg != 1 || g.accumulate ||
+      g.ldc % 8 || g.lda % 8 || g.ldb % 8)
+    return EDET_OK;
+  done = true;
+  switch ((g.N + 15) / 16) {
+    case 1: return launch_gemm_s<T, LAZY, 1>(g, s);
+    case 2: return launch_gemm_s<T, LAZY, 2>(g, s);
+    case 3: return launch_gemm_s<T, LAZY, 3>(g, s);
+    case 4: return launch_gemm_s<T, LAZY, 4>(g, s);
+    case 5: return launch_gemm_s<T, LAZY, 5>(g, s);
+    case 6: return launch_gemm_s<T, LAZY, 6>(g, s);
+    case 7: return launch_gemm_s<T, LAZY, 7>(g, s);
+    case 8: return launch_gemm_s<T, LAZY, 8>(g, s);
+    case 9: return launch_gemm_s<T, LAZY, 9>(g, s);
+    default: return launch_gemm_s<T, LAZY, 10>(g, s);
+  }
+}
+
 // ------------------------------------------------------------------ launch helpers
 template <typename T, int BM, int BN, bool LAZY, int KC = 32>
 static int launch_gemm(GemmArgs g, hipStream_t s) {
@@ -1298,6 +1475,11 @@ static int dispatch_gemm_kloop(GemmArgs g, hipStream_t s) {
 
 template <typename T, bool LAZY>
 static int dispatch_gemm(GemmArgs g, hipStream_t s) {
+  {
+    bool done = false;
+    const int rc = dispatch_gemm_s<T, LAZY>(g, s, done);
+    if (done || rc) return rc;
+  }
 #ifndef EDET_NO_PWB
   {
     bool done = false;
