@@ -1246,7 +1246,7 @@ static int dispatch_pwb(const GemmArgs& g, hipStream_t s, bool& done) {
 #define EDET_GS_PF 2
 #endif
 constexpr int GS_PF = EDET_GS_PF;  // row groups in flight ahead of the one being computed
-template <typename T, int NF, bool LAZY>
+template <typename T, int NF, int KS, bool LAZY>
 __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   __shared__ float red[2][4][NF * 16];
   constexpr int LDW = NF * 16 + 8;  // wave-private output staging row (bf16), padded
@@ -1258,15 +1258,17 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   const T* A = (const T*)g.a;
   const T* Wt = (const T*)g.b;
   T* Y = (T*)g.c;
-  // weights: fragment f holds W[16 f + (lane & 15)][kq .. kq + 8]
-  bf16x8_t wf[NF];
+  // weights: fragment (ks, f) holds W[16 f + (lane & 15)][32 ks + kq .. + 8]
+  bf16x8_t wf[KS][NF];
 #pragma unroll
-  for (int f = 0; f < NF; ++f) {
-    const int n = 16 * f + (lane & 15);
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (n < N && kq < K) v = *reinterpret_cast<const uint4*>(Wt + (size_t)n * g.ldb + kq);
-    wf[f] = __builtin_bit_cast(bf16x8_t, v);
-  }
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int n = 16 * f + (lane & 15), k = 32 * ks + kq;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n < N && k < K) v = *reinterpret_cast<const uint4*>(Wt + (size_t)n * g.ldb + k);
+      wf[ks][f] = __builtin_bit_cast(bf16x8_t, v);
+    }
   float bias[NF][4];
 #pragma unroll
   for (int f = 0; f < NF; ++f)
@@ -1275,11 +1277,14 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
       const int n = 16 * f + 4 * (lane >> 4) + r;
       bias[f][r] = (g.bias && n < N) ? g.bias[n] : 0.f;
     }
-  float2 af[8];
+  float2 af[KS][8];
   if constexpr (LAZY) {
     const float inv = 1.f / (float)M;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) af[j] = kq + j < K ? bn_affine(g.lz.bn, 0, kq + j, inv) : make_float2(1.f, 0.f);
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        af[ks][j] = 32 * ks + kq + j < K ? bn_affine(g.lz.bn, 0, 32 * ks + kq + j, inv) : make_float2(1.f, 0.f);
   }
   const int hw = g.pyr.H[0] * g.pyr.W[0];
   float ss[NF][4], sq[NF][4];
@@ -1290,45 +1295,60 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   const int ngroups = (M + 15) / 16, gstride = gridDim.x * 4;
   // the next groups' A rows are fetched before this group's stores are issued (vmcnt
   // counts loads and stores in order: a load issued after the stores would wait for them)
-  auto fetch = [&](int grp) {
+  auto fetch = [&](int grp, uint4* v) {
     const int row = grp * 16 + (lane & 15);
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (kq < K && grp < ngroups) v = *reinterpret_cast<const uint4*>(A + (size_t)(row < M ? row : 0) * g.lda + kq);
-    return v;
-  };
-  uint4 pre[GS_PF];
 #pragma unroll
-  for (int u = 0; u < GS_PF; ++u) pre[u] = fetch(blockIdx.x * 4 + wave + u * gstride);
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = 32 * ks + kq;
+      v[ks] = make_uint4(0, 0, 0, 0);
+      if (k < K && grp < ngroups) v[ks] = *reinterpret_cast<const uint4*>(A + (size_t)(row < M ? row : 0) * g.lda + k);
+    }
+  };
+  uint4 pre[GS_PF][KS];
+#pragma unroll
+  for (int u = 0; u < GS_PF; ++u) fetch(blockIdx.x * 4 + wave + u * gstride, pre[u]);
   for (int grp = blockIdx.x * 4 + wave; grp < ngroups; grp += gstride) {
     const int row = grp * 16 + (lane & 15);
     const bool live = row < M;
-    uint4 raw = pre[0];
+    uint4 raw[KS];
 #pragma unroll
-    for (int u = 0; u + 1 < GS_PF; ++u) pre[u] = pre[u + 1];
-    pre[GS_PF - 1] = fetch(grp + GS_PF * gstride);
-    if constexpr (LAZY) {
-      float x[8];
-      const uint32_t w4[4] = {raw.x, raw.y, raw.z, raw.w};
+    for (int ks = 0; ks < KS; ++ks) raw[ks] = pre[0][ks];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        x[2 * i] = __uint_as_float(w4[i] << 16);
-        x[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+    for (int u = 0; u + 1 < GS_PF; ++u)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) pre[u][ks] = pre[u + 1][ks];
+    fetch(grp + GS_PF * gstride, pre[GS_PF - 1]);
+    bf16x8_t bfrag[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      uint4 rv = raw[ks];
+      if constexpr (LAZY) {
+        const int k0 = 32 * ks + kq;
+        float x[8];
+        const uint32_t w4[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          x[2 * i] = __uint_as_float(w4[i] << 16);
+          x[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+        }
+        float gt[8];
+        if (g.lz.gate && k0 < K) ld8(g.lz.gate + (size_t)((live ? row : 0) / hw) * K + k0, gt);
+        uint16_t o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float u = lazy_apply(x[j], af[ks][j], g.lz.act);
+          if (g.lz.gate) u *= (k0 < K ? gt[j] : 0.f);
+          o[j] = k0 + j < K ? f2bf(u) : (uint16_t)0;
+        }
+        rv = *reinterpret_cast<uint4*>(o);
       }
-      float gt[8];
-      if (g.lz.gate && kq < K) ld8(g.lz.gate + (size_t)((live ? row : 0) / hw) * K + kq, gt);
-      uint16_t o[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float u = lazy_apply(x[j], af[j], g.lz.act);
-        if (g.lz.gate) u *= (kq < K ? gt[j] : 0.f);
-        o[j] = kq + j < K ? f2bf(u) : (uint16_t)0;
-      }
-      raw = *reinterpret_cast<uint4*>(o);
+      bfrag[ks] = __builtin_bit_cast(bf16x8_t, rv);
     }
-    const bf16x8_t bfrag = __builtin_bit_cast(bf16x8_t, raw);
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-      floatx4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[f], bfrag, floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      floatx4 d = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][f], bfrag[ks], d, 0, 0, 0);
       const int n0 = 16 * f + 4 * (lane >> 4);
       float v[4];
 #pragma unroll
@@ -1376,37 +1396,50 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   }
 }
 
-template <typename T, bool LAZY, int NF>
+template <typename T, bool LAZY, int NF, int KS>
 static int launch_gemm_s(const GemmArgs& g, hipStream_t s) {
   static const int blk_env = getenv("EDET_GS_BLOCKS") ? atoi(getenv("EDET_GS_BLOCKS")) : 0;  // A/B only
   const int ngroups = (g.M + 15) / 16;
   // 512 blocks (2 per CU): measured best over 512..2048 in the D0 step (scripts/kbench.py)
   const int grid = std::max(1, std::min(cdiv(ngroups, 4), blk_env > 0 ? blk_env : 512));
-  hipLaunchKernelGGL((k_gemm_s<T, NF, LAZY>), dim3(grid), dim3(256), 0, s, g);
+  hipLaunchKernelGGL((k_gemm_s<T, NF, KS, LAZY>), dim3(grid), dim3(256), 0, s, g);
   return check_launch("edet gemm_s");
 }
 
-// K <= 32, N <= 160 (NF <= 10 fragments), one segment, bf16, plain store
+template <typename T, bool LAZY, int KS>
+static int launch_gemm_s_n(const GemmArgs& g, hipStream_t s) {
+  switch ((g.N + 15) / 16) {
+    case 1: return launch_gemm_s<T, LAZY, 1, KS>(g, s);
+    case 2: return launch_gemm_s<T, LAZY, 2, KS>(g, s);
+    case 3: return launch_gemm_s<T, LAZY, 3, KS>(g, s);
+    case 4: return launch_gemm_s<T, LAZY, 4, KS>(g, s);
+    case 5: return launch_gemm_s<T, LAZY, 5, KS>(g, s);
+    case 6: return launch_gemm_s<T, LAZY, 6, KS>(g, s);
+    case 7: return launch_gemm_s<T, LAZY, 7, KS>(g, s);
+    case 8: return launch_gemm_s<T, LAZY, 8, KS>(g, s);
+    case 9: return launch_gemm_s<T, LAZY, 9, KS>(g, s);
+    default: return launch_gemm_s<T, LAZY, 10, KS>(g, s);
+  }
+}
+
+// K <= 32 and N <= 160 with statistics or a lazy A (one segment); also 32 < K <= 64, N <= 96
+// for the plain statistics-free GEMMs (the 1x1 dgrads), on pyramids too: rows between
+// segments are padding and only ever written
 template <typename T, bool LAZY>
 static int dispatch_gemm_s(const GemmArgs& g, hipStream_t s, bool& done) {
   done = false;
   static const int off = getenv("EDET_NO_GEMM_S") ? atoi(getenv("EDET_NO_GEMM_S")) : 0;  // A/B only
-  if (off || sizeof(T) != 2 || g.K > 32 || g.K % 8 || g.N > 160 || g.N % 8 || g.pyr.nseg != 1 || g.accumulate ||
-      g.ldc % 8 || g.lda % 8 || g.ldb % 8)
-    return EDET_OK;
-  done = true;
-  switch ((g.N + 15) / 16) {
-    case 1: return launch_gemm_s<T, LAZY, 1>(g, s);
-    case 2: return launch_gemm_s<T, LAZY, 2>(g, s);
-    case 3: return launch_gemm_s<T, LAZY, 3>(g, s);
-    case 4: return launch_gemm_s<T, LAZY, 4>(g, s);
-    case 5: return launch_gemm_s<T, LAZY, 5>(g, s);
-    case 6: return launch_gemm_s<T, LAZY, 6>(g, s);
-    case 7: return launch_gemm_s<T, LAZY, 7>(g, s);
-    case 8: return launch_gemm_s<T, LAZY, 8>(g, s);
-    case 9: return launch_gemm_s<T, LAZY, 9>(g, s);
-    default: return launch_gemm_s<T, LAZY, 10>(g, s);
+  if (off || sizeof(T) != 2 || g.K % 8 || g.N % 8 || g.accumulate || g.ldc % 8 || g.lda % 8 || g.ldb % 8) return EDET_OK;
+  const bool plain = !LAZY && !g.has_stats;
+  if (g.K <= 32 && g.N <= 160 && (g.pyr.nseg == 1 || plain)) {
+    done = true;
+    return launch_gemm_s_n<T, LAZY, 1>(g, s);
   }
+  if (plain && g.K <= 64 && g.N <= 96) {
+    done = true;
+    return launch_gemm_s_n<T, LAZY, 2>(g, s);
+  }
+  return EDET_OK;
 }
 
 // ------------------------------------------------------------------ launch helpers
