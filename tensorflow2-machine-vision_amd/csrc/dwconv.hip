@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
   for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(Wp[(size_t)i * g.C + c0 + c]) : 0.f;
   T* Y = (T*)g.y;
   float s = 0.f, q = 0.f;
-  int cur_seg = -1;
+  int cur_seg = -1, xf_seg = -1, xf_img = -1;
 
   for (int t = w / g.ncb; t < g.tiles_total; t += G) {
     int seg, n, ty, tx;
@@ -173,8 +173,15 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
     }
     Stage<T, IH, IW> st;
     st.fetch(g, seg, n, oy0 * S - pt, ox0 * S - pl, c0);
-    prep_xf(g, xf, gt, seg, n, c0);
-    __syncthreads();
+    // affine / gate only when the segment / image changes (block-uniform): a block walks
+    // ~20 tiles of one image, and the re-derivation was a dependent global round trip and a
+    // barrier per tile
+    if (seg != xf_seg || (g.lz.gate && n != xf_img)) {
+      prep_xf(g, xf, gt, seg, n, c0);
+      xf_seg = seg;
+      xf_img = n;
+      __syncthreads();
+    }
     st.commit(g, tile, xf, gt);
     __syncthreads();
 
@@ -332,6 +339,7 @@ __global__ __launch_bounds__(256) void k_dw_wgrad(DwArgs g) {
   float acc[K * K];
 #pragma unroll
   for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
+  int xf_seg = -1, xf_img = -1;
 
   for (int t = t_begin; t < t_end; ++t) {
     int seg, n, ty, tx;
@@ -342,8 +350,12 @@ __global__ __launch_bounds__(256) void k_dw_wgrad(DwArgs g) {
     __syncthreads();
     Stage<T, IH, IW> st;
     st.fetch(g, seg, n, oy0 * S - pt, ox0 * S - pl, c0);
-    prep_xf(g, xf, gt, seg, n, c0);
-    __syncthreads();
+    if (seg != xf_seg || (g.lz.gate && n != xf_img)) {  // block-uniform, as in k_dw_fwd
+      prep_xf(g, xf, gt, seg, n, c0);
+      xf_seg = seg;
+      xf_img = n;
+      __syncthreads();
+    }
     st.commit(g, lds, xf, gt);
     const int oy = oy0 + r;
     const size_t obase = (size_t)g.pout.row_off[seg] + (size_t)n * OH * OW;
