@@ -350,6 +350,17 @@ __global__ __launch_bounds__(256) void k_dw_wgrad(DwArgs g) {
     __syncthreads();
     Stage<T, IH, IW> st;
     st.fetch(g, seg, n, oy0 * S - pt, ox0 * S - pl, c0);
+    // this tile's dy values go out with the halo loads (select-predicated), not after commit
+    const int oy = oy0 + r;
+    const size_t obase = (size_t)g.pout.row_off[seg] + (size_t)n * OH * OW;
+    T dyr[DTS];
+#pragma unroll
+    for (int j = 0; j < DTS; ++j) {
+      const int ox = ox0 + j;
+      const bool in = oy < OH && ox < OW && cvalid;
+      dyr[j] = DY[in ? (obase + (size_t)oy * OW + ox) * g.C + c0 + c : 0];
+      if (!in) dyr[j] = from_f<T>(0.f);
+    }
     if (seg != xf_seg || (g.lz.gate && n != xf_img)) {  // block-uniform, as in k_dw_fwd
       prep_xf(g, xf, gt, seg, n, c0);
       xf_seg = seg;
@@ -357,14 +368,9 @@ __global__ __launch_bounds__(256) void k_dw_wgrad(DwArgs g) {
       __syncthreads();
     }
     st.commit(g, lds, xf, gt);
-    const int oy = oy0 + r;
-    const size_t obase = (size_t)g.pout.row_off[seg] + (size_t)n * OH * OW;
     float dyv[DTS];
 #pragma unroll
-    for (int j = 0; j < DTS; ++j) {
-      const int ox = ox0 + j;
-      dyv[j] = (oy < OH && ox < OW && cvalid) ? to_f<T>(DY[(obase + (size_t)oy * OW + ox) * g.C + c0 + c]) : 0.f;
-    }
+    for (int j = 0; j < DTS; ++j) dyv[j] = to_f<T>(dyr[j]);
     __syncthreads();
 #pragma unroll
     for (int kh = 0; kh < K; ++kh)
