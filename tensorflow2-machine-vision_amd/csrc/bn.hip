@@ -197,8 +197,16 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
   if (cur_seg >= 0) flush_reduce<T>(g, geo, cur_seg, rr, tv, red, s, q);
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g) {
+// Persistent over chunks like the reduce (block b takes chunks b, b+grid, ...): the
+// per-channel tables (fp64 statistics -> affine, mean/rstd, dgamma/M, dbeta/M) are rebuilt
+// only when the segment changes.  The BN / swish / gate / dsq cases are compile-time (F) and
+// each thread folds its 8 channels' tables into registers once per chunk:
+//   u = x*sc + sh,   dx = sc*du + kb*x + kc   with kb = -sc*rstd*dgamma/M,
+//   kc = -sc*dbeta/M + sc*rstd*mean*dgamma/M   (= sc*(du - dbeta/M - xhat*dgamma/M))
+// so the row loop is loads, ~10 VALU per element and stores (no LDS, no per-element branches).
+enum { AF_BN = 1, AF_ACT = 2, AF_GATE = 4, AF_DSQ = 8 };
+template <typename T, int F>
+__global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g, int nchunks) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int C = g.C;
   float2* af = reinterpret_cast<float2*>(smem);
@@ -206,47 +214,73 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g) {
   float2* gb = mr + C;
   const RowGeom geo = g.geo;
   const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
-  int seg, chunk;
-  chunk_lookup(g.p, geo.CH, blockIdx.x, seg, chunk);
-  const int rows = seg_rows(g.p, seg);
-  load_tables(g.lz, seg, 1.f / (float)rows, C, af, mr, gb, &g.acc);
-  if (g.has_grads && chunk == 0)  // one writer per segment: fp32 parameter gradients
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      g.grads.a[seg][c] += (float)g.acc.dgamma[seg][c];
-      g.grads.b[seg][c] += (float)g.acc.dbeta[seg][c];
-    }
-  __syncthreads();
-  if (rr >= geo.R) return;
-  const int off = g.p.row_off[seg];
-  const int m_begin = off + chunk * geo.CH, m_end = min(off + rows, m_begin + geo.CH);
-  const int hw = g.p.H[seg] * g.p.W[seg];
   const int NV = C / 8;
   T* DX = (T*)g.dx;
-  const bool bn = g.lz.bn.enabled;
-#pragma unroll
-  for (int v = 0; v < RVPT; ++v) {
-    const int cv = tv + v * geo.TPR;
-    if (!(v < geo.VPT && cv < NV)) continue;
-    const int c = cv * 8;
-    // EU rows per trip, all loads before any store (vmcnt orders loads behind earlier stores)
-    for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
-      float du[EU][8], xh[EU][8];
-#pragma unroll
-      for (int u = 0; u < EU; ++u) {
-        const int mu = min(m + u * geo.R, m_end - 1);
-        lazy_du<T>(g, seg, mu, (mu - off) / hw, c, af, mr, du[u], xh[u]);
+  int cur_seg = -1;
+  for (int b = blockIdx.x; b < nchunks; b += gridDim.x) {
+    int seg, chunk;
+    chunk_lookup(g.p, geo.CH, b, seg, chunk);
+    const int rows = seg_rows(g.p, seg);
+    if (seg != cur_seg) {
+      if (cur_seg >= 0) __syncthreads();  // the previous segment's tables are still being read
+      load_tables(g.lz, seg, 1.f / (float)rows, C, af, mr, gb, &g.acc);
+      cur_seg = seg;
+      __syncthreads();
+    }
+    if (g.has_grads && chunk == 0)  // one writer per segment: fp32 parameter gradients
+      for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        g.grads.a[seg][c] += (float)g.acc.dgamma[seg][c];
+        g.grads.b[seg][c] += (float)g.acc.dbeta[seg][c];
       }
+    if (rr >= geo.R) continue;
+    const int off = g.p.row_off[seg];
+    const int m_begin = off + chunk * geo.CH, m_end = min(off + rows, m_begin + geo.CH);
+    const int hw = g.p.H[seg] * g.p.W[seg];
+    const float* dvsp = g.dv_scale ? g.dv_scale + seg * g.p.batch : nullptr;
 #pragma unroll
-      for (int u = 0; u < EU; ++u) {
-        const int mu = m + u * geo.R;
-        if (mu >= m_end) break;
-        float o[8];
+    for (int v = 0; v < RVPT; ++v) {
+      const int cv = tv + v * geo.TPR;
+      if (!(v < geo.VPT && cv < NV)) continue;
+      const int c = cv * 8;
+      float sc[8], sh[8], kb[8], kc[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float2 d = gb[c + j];
-          o[j] = bn ? af[c + j].x * (du[u][j] - d.y - xh[u][j] * d.x) : du[u][j];
+      for (int j = 0; j < 8; ++j) {
+        const float2 a = af[c + j];
+        sc[j] = a.x; sh[j] = a.y;
+        if (F & AF_BN) {
+          const float2 q = mr[c + j], d = gb[c + j];
+          kb[j] = -a.x * q.y * d.x;
+          kc[j] = -a.x * d.y - kb[j] * q.x;
         }
-        acc8m(DX + (size_t)mu * C + c, 8, o, g.accumulate);
+      }
+      // EU rows per trip, all loads before any store (vmcnt orders loads behind earlier stores)
+      for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
+        float x[EU][8], d[EU][8], gt[EU][8], ds[EU][8], dvs[EU];
+#pragma unroll
+        for (int u = 0; u < EU; ++u) {
+          const int mu = min(m + u * geo.R, m_end - 1);
+          const int n = (mu - off) / hw;
+          ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
+          ld8((const T*)g.dv + (size_t)mu * C + c, d[u]);
+          dvs[u] = dvsp ? dvsp[n] : 1.f;
+          if (F & AF_GATE) ld8(g.lz.gate + (size_t)n * C + c, gt[u]);
+          if (F & AF_DSQ) ld8(g.dsq + (size_t)n * C + c, ds[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < EU; ++u) {
+          const int mu = m + u * geo.R;
+          if (mu >= m_end) break;
+          float o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float gg = d[u][j] * dvs[u];
+            if (F & AF_GATE) gg *= gt[u][j];
+            if (F & AF_DSQ) gg += ds[u][j];
+            const float du = (F & AF_ACT) ? gg * dswishf_(x[u][j] * sc[j] + sh[j]) : gg;
+            o[j] = (F & AF_BN) ? sc[j] * du + kb[j] * x[u][j] + kc[j] : du;
+          }
+          acc8m(DX + (size_t)mu * C + c, 8, o, g.accumulate);
+        }
       }
     }
   }
@@ -648,6 +682,14 @@ static int lazy_checks(const edet_lazy* x, const edet_pyramid* p, int C) {
   return EDET_OK;
 }
 
+template <typename T, int F = 0>
+static void launch_apply(int f, dim3 grid, dim3 block, size_t lds, hipStream_t s, const LArgs& g, int nb) {
+  if constexpr (F < 16) {
+    if (f == F) hipLaunchKernelGGL((k_lazy_bwd_apply<T, F>), grid, block, lds, s, g, nb);
+    else launch_apply<T, F + 1>(f, grid, block, lds, s, g, nb);
+  }
+}
+
 }  // namespace edet
 
 using namespace edet;
@@ -696,7 +738,11 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 3 * C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_lazy_bwd_apply<T>, dim3(nb), row_block(g.geo), lds, (hipStream_t)stream, g);
+    // resident blocks per launch (0 = one block per chunk); A/B knob EDET_APPLY_GRID
+    static const int gcap = getenv("EDET_APPLY_GRID") ? atoi(getenv("EDET_APPLY_GRID")) : 2048;
+    const int grid = gcap > 0 && nb > gcap ? gcap : nb;
+    const int f = (x->bn.enabled ? AF_BN : 0) | (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0);
+    if (nb) launch_apply<T>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
     return check_launch("edet lazy_bwd_apply");
   });
 }
