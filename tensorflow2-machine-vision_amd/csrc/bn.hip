@@ -82,30 +82,6 @@ __device__ __forceinline__ void load_tables(const edet_lazy& lz, int seg, float 
   }
 }
 
-// du (gradient at the BN output) and xhat for the 8 channels at c of row m (image n)
-template <typename T>
-__device__ __forceinline__ void lazy_du(const LArgs& g, int seg, int m, int n, int c, const float2* af,
-                                        const float2* mr, float* du, float* xh) {
-  float x[8], d[8];
-  ld8((const T*)g.lz.x + (size_t)m * g.lz.ld + c, x);
-  ld8((const T*)g.dv + (size_t)m * g.C + c, d);
-  const float dvs = g.dv_scale ? g.dv_scale[seg * g.p.batch + n] : 1.f;
-  float gt[8], ds[8];
-  if (g.lz.gate) ld8(g.lz.gate + (size_t)n * g.C + c, gt);
-  if (g.dsq) ld8(g.dsq + (size_t)n * g.C + c, ds);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float2 a = af[c + j];
-    const float u = x[j] * a.x + a.y;
-    float gg = d[j] * dvs;
-    if (g.lz.gate) gg *= gt[j];
-    if (g.dsq) gg += ds[j];
-    du[j] = g.lz.act ? gg * dswishf_(u) : gg;
-    const float2 b = mr[c + j];
-    xh[j] = (x[j] - b.x) * b.y;
-  }
-}
-
 // Persistent over chunks (block b takes chunks b, b+grid, ...): per-thread partials live in
 // registers until the segment changes, so each block issues 2C atomics per segment.
 template <typename T>
@@ -139,7 +115,10 @@ __device__ __forceinline__ void flush_reduce(const LArgs& g, const RowGeom& geo,
   __syncthreads();
 }
 
-template <typename T>
+// compile-time cases of the lazy backward row kernels
+enum { AF_BN = 1, AF_ACT = 2, AF_GATE = 4, AF_DSQ = 8 };
+
+template <typename T, int F>
 __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int C = g.C;
@@ -168,26 +147,43 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
     const int off = g.p.row_off[seg];
     const int m_begin = off + chunk * geo.CH, m_end = min(off + rows, m_begin + geo.CH);
     const int hw = g.p.H[seg] * g.p.W[seg];
+    const float* dvsp = g.dv_scale ? g.dv_scale + seg * g.p.batch : nullptr;
     if (rr < geo.R) {
 #pragma unroll
       for (int v = 0; v < RVPT; ++v) {
         const int cv = tv + v * geo.TPR;
         if (!(v < geo.VPT && cv < NV)) continue;
+        const int c = cv * 8;
+        // the 8 channels' tables in registers for the whole chunk (as k_lazy_bwd_apply)
+        float sc[8], sh[8], mu_[8], rs[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float2 a = af[c + j], r = mr[c + j];
+          sc[j] = a.x; sh[j] = a.y; mu_[j] = r.x; rs[j] = r.y;
+        }
         for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
-          float du[EU][8], xh[EU][8];
+          float x[EU][8], d[EU][8], gt[EU][8], ds[EU][8], dvs[EU];
 #pragma unroll
           for (int u = 0; u < EU; ++u) {
             const int mu = min(m + u * geo.R, m_end - 1);
-            lazy_du<T>(g, seg, mu, (mu - off) / hw, cv * 8, af, mr, du[u], xh[u]);
+            const int n = (mu - off) / hw;
+            ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
+            ld8((const T*)g.dv + (size_t)mu * C + c, d[u]);
+            dvs[u] = dvsp ? dvsp[n] : 1.f;
+            if (F & AF_GATE) ld8(g.lz.gate + (size_t)n * C + c, gt[u]);
+            if (F & AF_DSQ) ld8(g.dsq + (size_t)n * C + c, ds[u]);
           }
 #pragma unroll
           for (int u = 0; u < EU; ++u) {
-            const float k = m + u * geo.R < m_end ? 1.f : 0.f;
+            const float k = m + u * geo.R < m_end ? dvs[u] : 0.f;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              const float d = du[u][j] * k;
-              s[v][j] += d;
-              q[v][j] += d * xh[u][j];
+              float gg = d[u][j] * k;
+              if (F & AF_GATE) gg *= gt[u][j];
+              if (F & AF_DSQ) gg += ds[u][j] * (k != 0.f ? 1.f : 0.f);
+              const float du = (F & AF_ACT) ? gg * dswishf_(x[u][j] * sc[j] + sh[j]) : gg;
+              s[v][j] += du;
+              q[v][j] += du * ((x[u][j] - mu_[j]) * rs[j]);
             }
           }
         }
@@ -204,7 +200,6 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
 //   u = x*sc + sh,   dx = sc*du + kb*x + kc   with kb = -sc*rstd*dgamma/M,
 //   kc = -sc*dbeta/M + sc*rstd*mean*dgamma/M   (= sc*(du - dbeta/M - xhat*dgamma/M))
 // so the row loop is loads, ~10 VALU per element and stores (no LDS, no per-element branches).
-enum { AF_BN = 1, AF_ACT = 2, AF_GATE = 4, AF_DSQ = 8 };
 template <typename T, int F>
 __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g, int nchunks) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -683,6 +678,13 @@ static int lazy_checks(const edet_lazy* x, const edet_pyramid* p, int C) {
 }
 
 template <typename T, int F = 0>
+static void launch_reduce(int f, dim3 grid, dim3 block, size_t lds, hipStream_t s, const LArgs& g, int nb) {
+  if constexpr (F < 16) {
+    if (f == F) hipLaunchKernelGGL((k_lazy_bwd_reduce<T, F>), grid, block, lds, s, g, nb);
+    else launch_reduce<T, F + 2>(f, grid, block, lds, s, g, nb);
+  }
+}
+template <typename T, int F = 0>
 static void launch_apply(int f, dim3 grid, dim3 block, size_t lds, hipStream_t s, const LArgs& g, int nb) {
   if constexpr (F < 16) {
     if (f == F) hipLaunchKernelGGL((k_lazy_bwd_apply<T, F>), grid, block, lds, s, g, nb);
@@ -715,7 +717,8 @@ int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, i
   const size_t lds = 2 * C * sizeof(float2) + 2 * (size_t)g.geo.R * C * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
     const int grid = nb < 1024 ? nb : 1024;
-    if (nb) hipLaunchKernelGGL(k_lazy_bwd_reduce<T>, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
+    const int f = (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0);
+    if (nb) launch_reduce<T>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
     return check_launch("edet lazy_bwd_reduce");
   });
 }
