@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g, int nchunks) {
 }
 
 // out[n][c] += (scale) * sum_hw f(row)   -- SE squeeze (mean of v(x)) or gate grad (dv * v(x))
-template <typename T, bool GATEGRAD>
+template <typename T, bool GATEGRAD, bool ACT>
 __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int C = g.C;
@@ -306,6 +306,9 @@ __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
       const int cv = tv + v * geo.TPR;
       if (!(v < geo.VPT && cv < NV)) continue;
       const int c = cv * 8;
+      float2 a8[8];  // the 8 channels' affine in registers
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a8[j] = af[c + j];
       for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
         float x[EU][8], d[EU][8];
 #pragma unroll
@@ -319,7 +322,7 @@ __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
           const float k = m + u * geo.R < m_end ? 1.f : 0.f;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float val = lazy_apply(x[u][j], af[c + j], g.lz.act) * k;
+            const float val = lazy_apply(x[u][j], a8[j], ACT) * k;
             s[v][j] += GATEGRAD ? d[u][j] * val : val;
           }
         }
@@ -370,6 +373,12 @@ __global__ __launch_bounds__(256) void k_gate_bn_reduce(LArgs g) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) a[q][j] = 0.f;
   if (live) {
+    float sc[8], sh[8], mu_[8], rs[8];  // the 8 channels' tables in registers
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float2 t = af[c + j], b = mr[c + j];
+      sc[j] = t.x; sh[j] = t.y; mu_[j] = b.x; rs[j] = b.y;
+    }
     for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
       float x[EU][8], d[EU][8];
 #pragma unroll
@@ -383,11 +392,10 @@ __global__ __launch_bounds__(256) void k_gate_bn_reduce(LArgs g) {
         const float k = m + u * geo.R < m_end ? 1.f : 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float2 t = af[c + j], b = mr[c + j];
-          const float uu = x[u][j] * t.x + t.y;
+          const float uu = x[u][j] * sc[j] + sh[j];
           const float sg = sigmoidf_(uu);
           const float sw = uu * sg, dsw = sg * (1.f + uu * (1.f - sg)) * k;
-          const float xh = (x[u][j] - b.x) * b.y;
+          const float xh = (x[u][j] - mu_[j]) * rs[j];
           const float dd = d[u][j] * k;
           a[0][j] += dd * sw;
           a[1][j] += dd * dsw;
@@ -600,7 +608,7 @@ __global__ __launch_bounds__(256) void k_residual(LArgs g) {
 // out = v(x) = act(bn(x)) * gate, written once.  Used for the SE-gated depthwise output that
 // both the project conv's forward GEMM and its weight gradient read: applying the transform in
 // their A-operand loads cost more than this extra pass (it was recomputed per column tile).
-template <typename T>
+template <typename T, bool ACT, bool GATE>
 __global__ __launch_bounds__(256) void k_materialize(LArgs g) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int C = g.C;
@@ -623,13 +631,16 @@ __global__ __launch_bounds__(256) void k_materialize(LArgs g) {
     const int cv = tv + v * geo.TPR;
     if (!(v < geo.VPT && cv < NV)) continue;
     const int c = cv * 8;
+    float2 a8[8];  // the 8 channels' affine in registers
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a8[j] = ax[c + j];
     for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
       float x[EU][8], gt[EU][8];
 #pragma unroll
       for (int u = 0; u < EU; ++u) {
         const int mu = min(m + u * geo.R, m_end - 1);
         ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
-        if (g.lz.gate) ld8(g.lz.gate + (size_t)((mu - off) / hw) * C + c, gt[u]);
+        if (GATE) ld8(g.lz.gate + (size_t)((mu - off) / hw) * C + c, gt[u]);
       }
 #pragma unroll
       for (int u = 0; u < EU; ++u) {
@@ -637,8 +648,8 @@ __global__ __launch_bounds__(256) void k_materialize(LArgs g) {
         if (mu >= m_end) break;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          x[u][j] = lazy_apply(x[u][j], ax[c + j], g.lz.act);
-          if (g.lz.gate) x[u][j] *= gt[u][j];
+          x[u][j] = lazy_apply(x[u][j], a8[j], ACT);
+          if (GATE) x[u][j] *= gt[u][j];
         }
         st8(OUT + (size_t)mu * C + c, x[u]);
       }
@@ -763,8 +774,10 @@ static int img_reduce(int dtype, bool gategrad, const edet_lazy* x, int B, int H
   const int nb = B * g.chunks_per_img;
   const size_t lds = C * sizeof(float2) + (size_t)g.geo.R * C * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (gategrad) hipLaunchKernelGGL((k_img_reduce<T, true>), dim3(nb), row_block(g.geo), lds, s, g);
-    else hipLaunchKernelGGL((k_img_reduce<T, false>), dim3(nb), row_block(g.geo), lds, s, g);
+    if (gategrad && x->act) hipLaunchKernelGGL((k_img_reduce<T, true, true>), dim3(nb), row_block(g.geo), lds, s, g);
+    else if (gategrad) hipLaunchKernelGGL((k_img_reduce<T, true, false>), dim3(nb), row_block(g.geo), lds, s, g);
+    else if (x->act) hipLaunchKernelGGL((k_img_reduce<T, false, true>), dim3(nb), row_block(g.geo), lds, s, g);
+    else hipLaunchKernelGGL((k_img_reduce<T, false, false>), dim3(nb), row_block(g.geo), lds, s, g);
     return check_launch("edet se reduce");
   });
 }
@@ -860,7 +873,11 @@ int edet_lazy_materialize(int dtype, const edet_lazy* x, const edet_pyramid* p, 
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_materialize<T>, dim3(nb), row_block(g.geo), lds, (hipStream_t)stream, g);
+    const hipStream_t st = (hipStream_t)stream;
+    if (nb && x->act && x->gate) hipLaunchKernelGGL((k_materialize<T, true, true>), dim3(nb), row_block(g.geo), lds, st, g);
+    else if (nb && x->act) hipLaunchKernelGGL((k_materialize<T, true, false>), dim3(nb), row_block(g.geo), lds, st, g);
+    else if (nb && x->gate) hipLaunchKernelGGL((k_materialize<T, false, true>), dim3(nb), row_block(g.geo), lds, st, g);
+    else if (nb) hipLaunchKernelGGL((k_materialize<T, false, false>), dim3(nb), row_block(g.geo), lds, st, g);
     return check_launch("edet lazy_materialize");
   });
 }
