@@ -80,6 +80,14 @@ struct Stage {
     }
   }
   __device__ __forceinline__ void commit(const DwArgs& g, float* tile, const float2* xf, const float* gt) const {
+    // a thread's 8 channels are the same for every u (256 % 4 == 0): their affine and gate in
+    // registers once (read per element, the tile stores made the compiler reload them)
+    const int cv0 = (threadIdx.x & 3) * 8;
+    float2 a8[8];
+    float g8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a8[j] = xf[cv0 + j]; g8[j] = gt[cv0 + j]; }
+    const int act = g.lz.act;
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
       const int v = threadIdx.x + u * 256;
@@ -101,7 +109,7 @@ struct Stage {
       }
       const bool in = (ok >> u) & 1;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) vals[j] = in ? lazy_apply(vals[j], xf[cv + j], g.lz.act) * gt[cv + j] : 0.f;
+      for (int j = 0; j < 8; ++j) vals[j] = in ? lazy_apply(vals[j], a8[j], act) * g8[j] : 0.f;
       float* d = tile + pix * DCB + cv;
       reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
       reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
@@ -499,6 +507,12 @@ __global__ __launch_bounds__(256) void k_dw3(DwArgs g) {
     }
   };
   auto commit = [&](int buf) {
+    // this thread's 8 channels are the same for every u: affine in registers once
+    const int cv0 = (tid & 3) * 8;
+    float2 a8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a8[j] = xf[cv0 + j];
+    const int act = g.lz.act;
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
       const int v = tid + u * 256;
@@ -510,7 +524,7 @@ __global__ __launch_bounds__(256) void k_dw3(DwArgs g) {
         const float gv[8] = {rg[u][0].x, rg[u][0].y, rg[u][0].z, rg[u][0].w, rg[u][1].x, rg[u][1].y, rg[u][1].z, rg[u][1].w};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          vals[j] = lazy_apply(vals[j], xf[cv + j], g.lz.act);
+          vals[j] = lazy_apply(vals[j], a8[j], act);
           if (has_gate) vals[j] *= gv[j];
         }
       } else {
