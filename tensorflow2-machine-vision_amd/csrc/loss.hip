@@ -66,6 +66,26 @@ __device__ __forceinline__ void focal_elem(float x, float y, float alpha, float 
   dfl = at * (-dmodf * dpt * ce + mod * (p - y));
 }
 
+// gamma = 1.5 with a 0/1 target, branch-free and cancellation-free (same value as focal_elem):
+// with z = exp(-|x|), r = 1/(1+z): sigmoid = x >= 0 ? r : z r, and
+//   q  = 1 - pt = (x >= 0) != y ? r : z r           (the modulating base, exact)
+//   ce = log(1+z) + max(y ? -x : x, 0)
+//   p (1-p) = z r^2,   p - y = (y ? -1 : 1) q,   dpt = -(y ? -1 : 1) p (1-p)
+//   fl  = at q^1.5 ce
+//   dfl = at (y ? -1 : 1) sqrt(q) (1.5 p (1-p) ce + q^2)
+// kpos / kneg fold at * sign * (1 / normaliser) for y = 1 / y = 0.
+__device__ __forceinline__ void focal_elem15(float x, bool y, float apos, float aneg, float kpos, float kneg,
+                                             float& fl, float& dfl) {
+  const float z = __expf(-fabsf(x));
+  const float r = __builtin_amdgcn_rcpf(1.f + z);
+  const float zr = z * r;
+  const float q = ((x >= 0.f) != y) ? r : zr;
+  const float sq = __builtin_amdgcn_sqrtf(q);
+  const float ce = __logf(1.f + z) + fmaxf(y ? -x : x, 0.f);
+  fl = (y ? apos : aneg) * q * sq * ce;
+  dfl = (y ? kpos : kneg) * sq * fmaf(1.5f * zr * r, ce, q * q);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_loss(LossArgs g) {
   __shared__ float red[4];
@@ -104,11 +124,16 @@ __global__ __launch_bounds__(256) void k_loss(LossArgs g) {
           d[j] = 0.f;
           if (j > 0 && ++c == g.NC) { c = 0; ++a; }
           if (col < AN) {
-            const float y = ((g.NC >= 8 ? (a == a0 ? ta : tb) : tr[a]) == c) ? 1.f : 0.f;
+            const bool yb = (g.NC >= 8 ? (a == a0 ? ta : tb) : tr[a]) == c;
             float fl, dfl;
-            focal_elem(x[j], y, g.alpha, g.gamma, g15, fl, dfl);
+            if (g15) {
+              focal_elem15(x[j], yb, g.alpha, 1.f - g.alpha, -g.alpha * inv, (1.f - g.alpha) * inv, fl, dfl);
+              d[j] = dfl;
+            } else {
+              focal_elem(x[j], yb ? 1.f : 0.f, g.alpha, g.gamma, g15, fl, dfl);
+              d[j] = dfl * inv;
+            }
             s += fl;
-            d[j] = dfl * inv;
           }
         }
         if (D) st8(px, d);
