@@ -24,6 +24,9 @@ constexpr int RVPT = 2;  // vectors per thread (C <= 4096)
 #define EDET_APPLY_EU 2
 #endif
 constexpr int EU = EDET_APPLY_EU;
+// the BN-backward reduce and the materialize pass take four rows per trip (reduce 1.59 -> 1.51,
+// materialize 0.61 -> 0.58 ms/step; apply unchanged, the SE-fused reduce slower at four)
+constexpr int EUR = 4;
 
 struct RowGeom {
   int TPR, R, VPT, CH;  // threads per row, rows per pass, vectors per thread, rows per chunk
@@ -161,10 +164,10 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
           const float2 a = af[c + j], r = mr[c + j];
           sc[j] = a.x; sh[j] = a.y; mu_[j] = r.x; rs[j] = r.y;
         }
-        for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
-          float x[EU][8], d[EU][8], gt[EU][8], ds[EU][8], dvs[EU];
+        for (int m = m_begin + rr; m < m_end; m += EUR * geo.R) {
+          float x[EUR][8], d[EUR][8], gt[EUR][8], ds[EUR][8], dvs[EUR];
 #pragma unroll
-          for (int u = 0; u < EU; ++u) {
+          for (int u = 0; u < EUR; ++u) {
             const int mu = min(m + u * geo.R, m_end - 1);
             const int n = (mu - off) / hw;
             ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
             if (F & AF_DSQ) ld8(g.dsq + (size_t)n * C + c, ds[u]);
           }
 #pragma unroll
-          for (int u = 0; u < EU; ++u) {
+          for (int u = 0; u < EUR; ++u) {
             const float k = m + u * geo.R < m_end ? dvs[u] : 0.f;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -634,16 +637,16 @@ __global__ __launch_bounds__(256) void k_materialize(LArgs g) {
     float2 a8[8];  // the 8 channels' affine in registers
 #pragma unroll
     for (int j = 0; j < 8; ++j) a8[j] = ax[c + j];
-    for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
-      float x[EU][8], gt[EU][8];
+    for (int m = m_begin + rr; m < m_end; m += EUR * geo.R) {
+      float x[EUR][8], gt[EUR][8];
 #pragma unroll
-      for (int u = 0; u < EU; ++u) {
+      for (int u = 0; u < EUR; ++u) {
         const int mu = min(m + u * geo.R, m_end - 1);
         ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
         if (GATE) ld8(g.lz.gate + (size_t)((mu - off) / hw) * C + c, gt[u]);
       }
 #pragma unroll
-      for (int u = 0; u < EU; ++u) {
+      for (int u = 0; u < EUR; ++u) {
         const int mu = m + u * geo.R;
         if (mu >= m_end) break;
 #pragma unroll
