@@ -504,10 +504,17 @@ class EfficientDetNetTrain(EfficientDetNet):
         pyr = Pyr(B, [self.level_hw[l] for l in self.levels])
         t = self._targets(data, pyr)
         # N+ = sum(masks) + 1 (the +1 is added by the loss kernel); padding rows are never read
+        self._count_positives(t, pyr, self.scalars[5:6], s)
+        return t, pyr
+
+    def _count_positives(self, t, pyr, out, s):
+        if pyr.rows == sum(pyr.seg_rows(seg) for seg in range(pyr.nseg)):
+            # levels back to back (every level a multiple of 128 rows, D0 at 512 included): one launch
+            L.call("edet_count_positives", vp(t.mask), pyr.rows * self.A, vp(out), s)
+            return
         for seg in range(pyr.nseg):
             sl = pyr.seg_slice(seg)
-            L.call("edet_count_positives", vp(t.mask[sl]), pyr.seg_rows(seg) * self.A, vp(self.scalars[5:6]), s)
-        return t, pyr
+            L.call("edet_count_positives", vp(t.mask[sl]), pyr.seg_rows(seg) * self.A, vp(out), s)
 
     def compute_step(self, data, t, pyr):
         """Forward, fused loss (fwd+bwd) and backward with N+ already global in scalars[5]."""
@@ -566,9 +573,7 @@ class EfficientDetNetTrain(EfficientDetNet):
         s = stream()
         sc = torch.zeros(8, dtype=torch.float32, device=self.eng.device)
         parts = torch.zeros(2 * L.MAX_SEG, dtype=torch.float32, device=self.eng.device)
-        for seg in range(pyr.nseg):
-            sl = pyr.seg_slice(seg)
-            L.call("edet_count_positives", vp(t.mask[sl]), pyr.seg_rows(seg) * self.A, vp(sc[5:6]), s)
+        self._count_positives(t, pyr, sc[5:6], s)
         L.call("edet_detection_loss", self.eng.dt, vp(cls.raw), cls.ld, vp(box.raw), box.ld, pyr.c, self.A, self.NC,
                vp(t.cls), vp(t.box), vp(sc[5:6]), float(self.cfg.alpha), float(self.cfg.gamma), 0.1, 50.0, 1.0,
                None, None, vp(sc[0:1]), vp(parts), s)
