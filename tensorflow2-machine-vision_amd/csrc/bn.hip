@@ -772,7 +772,7 @@ static int img_reduce(int dtype, bool gategrad, const edet_lazy* x, int B, int H
   g.lz = *x; g.lz.gate = nullptr;  // the pre-gate value
   g.p.nseg = 1; g.p.batch = B; g.p.row_off[0] = 0; g.p.H[0] = HW; g.p.W[0] = 1;
   g.dv = dv; g.out64 = out64; g.C = C; g.hw = HW;
-  g.geo = row_geom(C);
+  g.geo = row_geom(C, 16);  // long chunks: each block ends in C fp64 atomics
   g.chunks_per_img = cdiv(HW, g.geo.CH);
   const int nb = B * g.chunks_per_img;
   const size_t lds = C * sizeof(float2) + (size_t)g.geo.R * C * sizeof(float);
