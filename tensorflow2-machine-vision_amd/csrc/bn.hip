@@ -724,13 +724,16 @@ int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, i
   LArgs g{};
   g.lz = *x; g.p = *p; g.acc = *acc; g.dv = dv; g.dv_scale = dv_scale; g.dsq = dsq; g.C = C;
   // Every block flushes 2C fp64 atomics to the same addresses, which serialise (~20 ns per
-  // block and address): long chunks and at most 1024 persistent blocks measured best
+  // block and address): long chunks and at most 512 persistent blocks measured best (r01g,
+  // four rows per trip: 256 / 384 / 512 / 768 / 1024 / 2048 -> 1.49 / 1.45 / 1.43 / 1.51 /
+  // 1.51 / 1.52 ms/step)
   // (scripts/row_probe.py: -20..-30 % on the C >= 240 and C = 16 layers, equal elsewhere).
   g.geo = row_geom(C, 16);
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 2 * C * sizeof(float2) + 2 * (size_t)g.geo.R * C * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    const int grid = nb < 1024 ? nb : 1024;
+    static const int rcap = getenv("EDET_REDUCE_GRID") ? atoi(getenv("EDET_REDUCE_GRID")) : 512;  // A/B only
+    const int grid = nb < rcap ? nb : rcap;
     const int f = (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0);
     if (nb) launch_reduce<T>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
     return check_launch("edet lazy_bwd_reduce");
