@@ -12,7 +12,7 @@
 
 namespace edet {
 
-constexpr int LCLS_ROWS = 16;
+constexpr int LCLS_ROWS = 32;  // rows per classification block (8 / 16 / 32 / 64: 363 / 197 / 191 / 200 us)
 constexpr int LBOX_ROWS = 256;
 
 struct LossArgs {
