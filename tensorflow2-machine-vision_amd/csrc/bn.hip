@@ -312,16 +312,16 @@ __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
       float2 a8[8];  // the 8 channels' affine in registers
 #pragma unroll
       for (int j = 0; j < 8; ++j) a8[j] = af[c + j];
-      for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
-        float x[EU][8], d[EU][8];
+      for (int m = m_begin + rr; m < m_end; m += EUR * geo.R) {
+        float x[EUR][8], d[EUR][8];
 #pragma unroll
-        for (int u = 0; u < EU; ++u) {
+        for (int u = 0; u < EUR; ++u) {
           const int mu = min(m + u * geo.R, m_end - 1);
           ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
           if (GATEGRAD) ld8((const T*)g.dv + (size_t)mu * C + c, d[u]);
         }
 #pragma unroll
-        for (int u = 0; u < EU; ++u) {
+        for (int u = 0; u < EUR; ++u) {
           const float k = m + u * geo.R < m_end ? 1.f : 0.f;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
