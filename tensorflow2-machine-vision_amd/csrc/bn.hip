@@ -382,16 +382,16 @@ __global__ __launch_bounds__(256) void k_gate_bn_reduce(LArgs g) {
       const float2 t = af[c + j], b = mr[c + j];
       sc[j] = t.x; sh[j] = t.y; mu_[j] = b.x; rs[j] = b.y;
     }
-    for (int m = m_begin + rr; m < m_end; m += EU * geo.R) {
-      float x[EU][8], d[EU][8];
+    for (int m = m_begin + rr; m < m_end; m += EUR * geo.R) {
+      float x[EUR][8], d[EUR][8];
 #pragma unroll
-      for (int u = 0; u < EU; ++u) {
+      for (int u = 0; u < EUR; ++u) {
         const int mu = min(m + u * geo.R, m_end - 1);
         ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
         ld8((const T*)g.dv + (size_t)mu * C + c, d[u]);
       }
 #pragma unroll
-      for (int u = 0; u < EU; ++u) {
+      for (int u = 0; u < EUR; ++u) {
         const float k = m + u * geo.R < m_end ? 1.f : 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
