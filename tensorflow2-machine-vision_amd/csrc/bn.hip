@@ -24,8 +24,10 @@ constexpr int RVPT = 2;  // vectors per thread (C <= 4096)
 #define EDET_APPLY_EU 2
 #endif
 constexpr int EU = EDET_APPLY_EU;
-// the BN-backward reduce and the materialize pass take four rows per trip (reduce 1.59 -> 1.51,
-// materialize 0.61 -> 0.58 ms/step; apply unchanged, the SE-fused reduce slower at four)
+// the reduce-type row kernels (BN-backward reduce, SE squeeze, SE-fused BN reduce) and the
+// materialize pass take four rows per trip (reduce 1.59 -> 1.51, materialize 0.61 -> 0.58
+// ms/step); apply is unchanged at four.  The SE-fused reduce was slower at four with ~8-pass
+// chunks and is faster (561 -> 542 us) at its 16-pass chunks.
 constexpr int EUR = 4;
 
 struct RowGeom {
