@@ -12,8 +12,9 @@ in HBM before the timed region.  The step is captured once in a HIP graph and re
 Prints ONE JSON line on rank 0 with value = images/s over all ranks, plus
   roofline     : dominant kernel's algorithmic bytes / its average launch duration (HIP
                  events around each launch of an instrumented eager step) vs 8 TB/s HBM
-  cpu_baseline : the oracle's fp32 train step (torch-CPU restatement of the reference
-                 semantics, not TF) on the host cores, bounded sample, rank 0 at N=1 only
+  cpu_baseline : BASELINE config 1 (D0 forward, one 512x512 image) through the oracle (fp32
+                 torch-CPU restatement of the reference semantics, not TF) on the host cores,
+                 median of 5 after 2 warm-ups, plus the oracle train step; rank 0 at N=1 only
 """
 import argparse
 import json
@@ -282,34 +283,92 @@ def pmc_traffic(kernel):
         return None
 
 
-def cpu_baseline(model, seconds=12.0):
-    """Oracle fp32 train step (forward + loss + backward) on the host cores, 1 image/iteration."""
+def _cpu_share():
+    """Host cores this process may use: the affinity set, capped by a cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(model, anchors, fwd_runs=10, train_runs=3):
+    """BASELINE config 1 on the host: the EfficientDet-D0 forward on one 512x512 image
+    (inference-mode BN, moving statistics (0, 1) as initialised) through the oracle -- the
+    fp32 torch-CPU restatement of the reference's TF2 semantics, not TF itself, which is not
+    installable here -- on every core this process may use; median of ``fwd_runs`` after two
+    warm-ups.  Second field: the oracle's fp32 train step (forward + loss + backward) on one
+    image with bench-like targets (7 GT boxes), median of ``train_runs`` after one warm-up."""
+    from oracle import ref_anchors as RA
     from oracle.ref_model import RefEfficientDet
-    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
-    torch.set_num_threads(threads)
-    ref = RefEfficientDet(model, model.state_dict(), dtype=torch.float32)
-    train_keys = [k for k in ref.p if not k.endswith(("moving_mean", "moving_variance"))]
-    for k in train_keys:
-        ref.p[k].requires_grad_(True)
-    S = model.cfg.image_size
+    cores = _cpu_share()
+    torch.set_num_threads(cores)
+    ref = RefEfficientDet(model.cfg, model.state_dict(), dtype=torch.float32)
+    cfg = model.cfg
+    S = cfg.image_size
     rng = np.random.default_rng(0)
     x = rng.random((1, S, S, 3), dtype=np.float32)
-    shapes = [(1,) + model.level_hw[l] + (9,) for l in model.levels]
-    yb = [np.zeros(s + (4,), np.float32) for s in shapes]
-    yc = [np.eye(model.NC, dtype=np.float32)[np.zeros(s, np.int64)] for s in shapes]
-    ym = [np.zeros(s + (1,), bool) for s in shapes]
-    n, t0 = 0, time.perf_counter()
-    while True:
-        box, cls = ref.forward(x, True)
-        loss, _ = ref.detection_loss(box, cls, yb, yc, ym)
-        torch.autograd.grad(loss, [ref.p[k] for k in train_keys], allow_unused=True)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 50:
-            break
-    return {"value": n / el, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} x 1-image 512x512 fp32 train steps (forward+loss+backward) of the oracle "
-                      f"(torch-CPU restatement of the reference TF2 semantics), {el:.1f} s"}
+
+    def med(fn, warm, runs):
+        for _ in range(warm):
+            fn()
+        ts = []
+        for _ in range(runs):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)), ts
+
+    with torch.no_grad():
+        fwd_s, fwd_ts = med(lambda: ref.forward(x, False), 2, fwd_runs)
+    # train-step field: realistic targets (bench.py's synthetic GT, oracle target encoding)
+    G = 7
+    boxes = np.zeros((G, 4), np.float32)
+    for k in range(G):
+        sz = np.exp(rng.uniform(np.log(16), np.log(400)))
+        ar = rng.uniform(0.5, 2.0)
+        h, w = sz * np.sqrt(ar), sz / np.sqrt(ar)
+        cy, cx = rng.uniform(0, S, 2)
+        boxes[k] = [cy - h / 2, cx - w / 2, cy + h / 2, cx + w / 2]
+    cls = rng.integers(1, cfg.num_classes, G)
+    lv = RA.generate_boxes(cfg.min_level, cfg.max_level, (S, S), cfg.num_scales, cfg.aspect_ratios, cfg.anchor_scale)
+    ob, oc, om, _ = RA.generate_targets(lv, boxes, cls, cfg.num_classes)
+    yb, yc, ym = [b[None] for b in ob], [c[None] for c in oc], [mm[None] for mm in om]
+    keys = [k for k in ref.p if not k.endswith(("moving_mean", "moving_variance"))]
+
+    def train_once():
+        for k in keys:
+            ref.p[k].requires_grad_(True)
+        box, cl = ref.forward(x, True)
+        loss, _ = ref.detection_loss(box, cl, yb, yc, ym)
+        torch.autograd.grad(loss, [ref.p[k] for k in keys], allow_unused=True)
+
+    tr_s, tr_ts = med(train_once, 1, train_runs)
+    npos = int(sum(np.asarray(m).sum() for m in ym))
+    return {"value": round(1.0 / fwd_s, 4), "unit": "images/s", "cores": cores, "kind": "port",
+            "config": "BASELINE config 1: EfficientDet-D0 forward, one 512x512 image, CPU",
+            "sample": f"median of {fwd_runs} single-image D0 forwards (inference BN) after 2 warm-ups, oracle fp32 "
+                      f"torch-CPU restatement of the reference TF2 semantics (not TF); runs "
+                      + ", ".join(f"{t:.3f}" for t in fwd_ts) + " s",
+            "cpu_model": _cpu_model(),
+            "train_step": {"value": round(1.0 / tr_s, 4), "unit": "images/s",
+                           "sample": f"median of {train_runs} one-image fp32 train steps (forward + focal/Huber "
+                                     f"loss + backward), 7 GT boxes -> {npos} positive anchors, after 1 warm-up"}}
 
 
 def bench_backbone(args):
@@ -396,7 +455,7 @@ def main():
     anchors = Anchors(cfg.min_level, cfg.max_level, (S, S), cfg.num_scales, cfg.aspect_ratios, cfg.anchor_scale, device=dev)
     ar = dp.make_allreduce(ctx)
     model = EfficientDetNetTrain(efficientnet_b0_blocks(), cfg, anchors, dtype=args.dtype, device=dev, seed=0,
-                                 world_size=world, grad_allreduce=ar, npos_allreduce=ar,
+                                 world_size=world, grad_allreduce=ar, npos_allreduce=ar, rank=rank,
                                  lr_schedule={"warmup_steps": 100, "total_steps": 10000,
                                               "adjusted_lr": 0.08 * B * world / 64})
     model.eng.overlap = bool(args.overlap)
@@ -412,30 +471,9 @@ def main():
 
     step = lambda: model.train_step(data)  # noqa: E731
     if args.graph:
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        if world == 1:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                model.train_step(data)
-            step = g.replay
-        else:
-            # prepare (targets, N+) | N+ all-reduce | forward+loss+backward | gradient
-            # all-reduce | optimizer: the collectives run between the captured graphs
-            g0, g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g0):
-                t_pyr = model.prepare_step(data)
-            with torch.cuda.graph(g1):
-                model.compute_step(data, *t_pyr)
-            with torch.cuda.graph(g2):
-                model.apply_gradients()
-
-            def step():
-                g0.replay()
-                ar(model.scalars[5:6])
-                g1.replay()
-                ar(model.P.g)
-                g2.replay()
+        # one graph at N = 1; at N > 1 prepare | N+ all-reduce | compute | gradient
+        # all-reduce | optimizer, the collectives between the captured graphs
+        step = dp.graphed_train_step(model, data, ar)
         torch.cuda.synchronize()
         log("[bench] graph captured")
 
@@ -444,7 +482,13 @@ def main():
     el = dp.timed(ctx, step, args.steps, torch.cuda.synchronize)
     el = dp.max_over_ranks(ctx, el, dev)
     value = world * B * args.steps / el
-    loss = float(model.scalars[0])
+    # global-batch loss: the replicas' data terms sum to it (Multi-GPU); each
+    # replica's scalars[0] also holds the (identical) L2 term once
+    lt = model.scalars[0:1].clone()
+    if ar is not None:
+        ar(lt)
+    l2 = float(model.sched.l2_weight) * 0.5 * float(model.scalars[2])
+    loss = float(lt) - (world - 1) * l2
     gnorm = float(model.scalars[3])
     log(f"[bench] {args.steps} steps in {el:.3f}s -> {value:.1f} img/s  loss={loss:.4f} gnorm={gnorm:.4f}")
 
@@ -452,6 +496,10 @@ def main():
     kernels = None
     if args.kernel_timing and rank == 0:
         es = 2 if args.dtype == "bf16" else 4
+        # the instrumented steps below run on rank 0 alone: snapshot the optimizer-visible
+        # state and restore it afterwards so rank 0 leaves in step with the other replicas
+        P = model.P
+        saved = [(t, t.clone()) for t in (P.w, P.v, P.ema, P.bn_mm, P.bn_mv, model.step_counter)]
         if ctx.distributed:
             model.grad_allreduce = None
             model.npos_allreduce = None
@@ -488,10 +536,15 @@ def main():
             log(f"[bench] roofline {kname}: {pr['launches']} launches, avg {pr['avg_launch_us']:.2f} us, "
                 f"{pr['bytes_per_launch'] / 1e6:.2f} MB/launch -> {ach:.1f} GB/s")
 
+        for t, c in saved:
+            t.copy_(c)
+        P.refresh_compute_copy()
+        model.grad_allreduce, model.npos_allreduce = ar, ar
+
     cpu = None
     if args.cpu_baseline and rank == 0 and world == 1:
         log("[bench] cpu baseline (oracle, fp32) ...")
-        cpu = cpu_baseline(model)
+        cpu = cpu_baseline(model, anchors)
         log(f"[bench] cpu baseline {cpu['value']:.3f} img/s on {cpu['cores']} threads")
 
     if rank == 0:
@@ -511,7 +564,7 @@ def main():
             "config": {"workload": f"{args.model} full train step {S}x{S}, B={B}/GPU, focal+Huber loss, SGD+EMA",
                        "model": args.model, "global_batch": B * world, "image_size": S,
                        "parallelism": f"dp{world}", "graph": bool(args.graph)},
-            "loss": round(loss, 5),
+            "loss": round(loss, 5),  # global-batch loss of the last timed step
             "gnorm": round(gnorm, 5),
             "roofline": roofline,
             "cpu_baseline": cpu,

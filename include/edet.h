@@ -281,15 +281,19 @@ int edet_detect_nms(int dtype, const float* boxes, const void* cls, int ldc, con
 /* ---- optimizer: L2 + clip_by_global_norm + SGD momentum + EMA, fused ----
  * scalars: [0] loss  [1] sum g^2  [2] sum w^2 (L2 params)  [3] gnorm  [4] lr  [5] npos
  * step: device int32 step counter (incremented by edet_opt_apply). */
-/* norm pass: scalars[1] += sum (g + l2*w)^2, scalars[2] += sum_{i<n_l2} w^2; block 0 also
- * writes scalars[4] = lr(step) and increments *step. */
+/* norm pass: writes EDET_OPT_NORM_BLOCKS per-block partial sums of (g + l2*w)^2 and of
+ * w^2 over the L2 prefix to partials[0..255] / partials[256..511] (fp64, device; no atomics);
+ * also writes scalars[4] = lr(step) and increments *step. */
+#define EDET_OPT_NORM_BLOCKS 256
 int edet_opt_norm(const float* w, const float* g, int64_t n, int64_t n_l2,
-                  const edet_sched* sched, float* scalars, int32_t* step,
+                  const edet_sched* sched, float* scalars, double* partials, int32_t* step,
                   edet_stream_t stream);
-/* apply pass: clip, SGD momentum, EMA; writes the `dtype` compute copy of w (nullable),
- * scalars[3] = gnorm (pre-clip), scalars[0] += l2 * sum w^2 / 2. */
+/* apply pass: folds the partials in one fixed order (bit-identical gnorm on every data-parallel
+ * replica), clip, SGD momentum, EMA; writes the `dtype` compute copy of w (nullable),
+ * scalars[1] = sum g^2, scalars[2] = sum w^2, scalars[3] = gnorm (pre-clip),
+ * scalars[0] += l2 * sum w^2 / 2. */
 int edet_opt_apply(float* w, const float* g, float* v, float* ema, int64_t n, int64_t n_l2,
-                   const edet_sched* sched, float* scalars, int dtype, void* wcompute,
+                   const edet_sched* sched, float* scalars, const double* partials, int dtype, void* wcompute,
                    edet_stream_t stream);
 int edet_cast_f32(int dtype, const float* src, void* dst, int64_t n, edet_stream_t stream);
 /* fp32 [N][K] 1x1 kernels -> `dtype` [K][roundup(N,8)] copies; table[e] = {src_off, dst_off, N, K}

@@ -1,10 +1,33 @@
 """torch-CPU restatement of the reference EfficientDet forward / loss / train step.
 
 TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).  Runs in float64 by default (float32 for
-the timed CPU baseline).  Layout NHWC at the interface, NCHW internally.  Parameters come as
-a dict keyed by the build's parameter names (same values the GPU model holds), in the build's
-storage layouts: stem [3][3][3][Co] (HWIO), 1x1 kernels [out][in], depthwise [k*k][C],
-SE kernels [R][C] / [C][R].
+the timed CPU baseline).  Layout NHWC at the interface, NCHW internally.
+
+Structure is derived HERE, from the config and the reference's own construction rules, never
+from the product's model object:
+  * block list        efficientnet/backbone_model.py:59-93 (first block of a stage takes the
+                      stage stride and input width, repeats s=1 / C_in = C_out) with
+                      utils/round_filters.py:2-12, utils/round_repeats.py:3-6
+  * block layers      layers/mb_conv_block.py:41-124 (conv2d / tpu_batch_normalization name
+                      counters :45-51, SE width max(1, int(C_in * se_ratio)) :98-101)
+  * reductions        backbone_model.py:119-139 (last block, or block before a stride-2 one)
+  * feature levels    efficientdet_net.py:80-85 (all_feats[min:max+1] + resample_p6/p7)
+  * resampling        layers/resample_feature_map.py:14-41: conv1x1+bias+BN iff the input's
+                      channel count differs from the target, max-pool iff taller than the
+                      level size, nearest resize iff shorter -- decided from the tensor that
+                      actually arrives, exactly like Keras' lazy build
+  * BiFPN topology    layers/bifpn.py:108-116 (the eight explicit node calls)
+  * heads             layers/class_net.py:54-103, layers/box_net.py:52-102 (shared convs,
+                      per-level BN 'class-%d-bn-%d', residual iff i > 0 and survival_prob)
+Parameters are created on first use, like Keras layers: ``param_specs(cfg)`` runs the forward
+on a 'meta' tensor and records every (name, shape, initialiser) in creation order.  A test
+checks that list against the product's parameter table, so a product that wires a BiFPN edge,
+a head BN or an endpoint differently from the reference rules cannot agree with this oracle.
+
+Naming and storage layouts (the build's checkpoint contract): 1x1 kernels
+[out][in]; depthwise kernels [k*k][C]; stem kernel HWIO [3][3][3][Co]; BN variables
+'<bn>/gamma', '/beta', '/moving_mean', '/moving_variance'; BiFPN fusion weights one vector
+'<node>/WSM' of the node's n_in scalars (the reference's WSM_0..WSM_{n-1}, bifpn.py:47-54).
 
 TF semantics restated:
   SAME padding   pad_before = floor(total/2), extra at bottom/right           (A1)
@@ -16,17 +39,70 @@ TF semantics restated:
   Huber          0.5 e^2 if |e|<=d else 0.5 d^2 + d(|e|-d)                   (A7)
   Keras mean     SUM_OVER_BATCH_SIZE = sum / #elements                        (A8)
   l2_loss        sum(t^2)/2; clip_by_global_norm; SGD momentum; EMA          (A9,A10)
-Reference file:line for each block is cited in the function docstrings.
 """
 from __future__ import annotations
 
 import math
 import re
-from typing import Dict, List, Optional, Sequence
+from collections import OrderedDict
+from typing import Dict, List, Optional
 
 import numpy as np
 import torch
 import torch.nn.functional as Fn
+
+# efficientnet/train.py:81-89 -- (num_repeat, kernel_size, strides, expand_ratio,
+# input_filters, output_filters, se_ratio), the EfficientDetBlockArgs field order
+B0_BLOCKS = [
+    (1, 3, (1, 1), 1, 32, 16, 0.25), (2, 3, (2, 2), 6, 16, 24, 0.25), (2, 5, (2, 2), 6, 24, 40, 0.25),
+    (3, 3, (2, 2), 6, 40, 80, 0.25), (3, 5, (1, 1), 6, 80, 112, 0.25), (4, 5, (2, 2), 6, 112, 192, 0.25),
+    (1, 3, (1, 1), 6, 192, 320, 0.25),
+]
+
+
+def round_filters(filters, width, divisor):
+    """utils/round_filters.py:2-12."""
+    filters = filters * width
+    new = max(divisor, int(filters + divisor / 2) // divisor * divisor)
+    if new < 0.9 * filters:
+        new += divisor
+    return int(new)
+
+
+def round_repeats(repeats, depth):
+    """utils/round_repeats.py:3-6."""
+    return int(math.ceil(depth * repeats))
+
+
+def _args(b):
+    """EfficientDetBlockArgs-like record (namedtuple or plain tuple) -> tuple of 7 fields."""
+    if hasattr(b, "num_repeat"):
+        return (b.num_repeat, b.kernel_size, tuple(b.strides), b.expand_ratio, b.input_filters, b.output_filters,
+                b.se_ratio)
+    return tuple(b)
+
+
+def block_list(cfg, blocks_args=None):
+    """BackboneModel._build (backbone_model.py:40-93): one record per MBConvBlock."""
+    blocks = []
+    for a in (blocks_args if blocks_args is not None else B0_BLOCKS):
+        rep, k, strides, e, cin, cout, se = _args(a)
+        cin = round_filters(cin, cfg.width_coefficient, cfg.depth_divisor)
+        cout = round_filters(cout, cfg.width_coefficient, cfg.depth_divisor)
+        rep = round_repeats(rep, cfg.depth_coefficient)
+        blocks.append(dict(k=k, s=strides[0], e=e, cin=cin, cout=cout, se=se))
+        for _ in range(rep - 1):
+            blocks.append(dict(k=k, s=1, e=e, cin=cout, cout=cout, se=se))
+    return blocks
+
+
+def _keras_counter_names(base):
+    """mb_conv_block.py:45-51: '', '_1', '_2', ... via the double-next counter."""
+    c = iter(range(1 << 30))
+
+    def nxt():
+        return base + ("" if not next(c) else "_" + str(next(c) // 2))
+    return nxt
 
 
 def same_pad(n, k, s):
@@ -53,20 +129,6 @@ class BNState:
         self.batch = {}  # name -> (mean, var_biased, count)
 
 
-def batch_norm(x, p, name, training, eps, bnstate: Optional[BNState]):
-    """Keras BatchNormalization on NCHW x (axis = channels)."""
-    g, b = p[name + "/gamma"], p[name + "/beta"]
-    if training:
-        mean = x.mean(dim=(0, 2, 3))
-        var = ((x - mean[None, :, None, None]) ** 2).mean(dim=(0, 2, 3))
-        if bnstate is not None:
-            bnstate.batch[name] = (mean.detach(), var.detach(), x.shape[0] * x.shape[2] * x.shape[3])
-    else:
-        mean, var = p[name + "/moving_mean"], p[name + "/moving_variance"]
-    inv = 1.0 / torch.sqrt(var + eps)
-    return (x - mean[None, :, None, None]) * (inv * g)[None, :, None, None] + b[None, :, None, None]
-
-
 def maxpool_same(x):
     """MaxPooling2D 3x3 s2 'SAME' (resample_feature_map.py:35-38): padded cells ignored."""
     pt, pb = same_pad(x.shape[2], 3, 2)
@@ -84,145 +146,212 @@ def resize_nearest(x, H, W):
     return x[:, :, iy][:, :, :, ix]
 
 
+# Keras initialisers, as (kind, *args) records:
+#   ('normal', std)        utils/conv_kernel_initializer.py:4-25  N(0, sqrt(2 / (kh*kw*out)))
+#   ('glorot', fan_in, fan_out)   keras default glorot_uniform, U(+-sqrt(6/(fi+fo)))
+#   ('vs_fan_in', fan_in)  tf.initializers.VarianceScaling(): truncated normal, scale 1, fan_in
+#   ('const', v)           zeros / ones / constant initialisers
+def _cki(kh, kw, out):
+    return ("normal", math.sqrt(2.0 / (kh * kw * out)))
+
+
 class RefEfficientDet:
     """Restatement of EfficientDetNet (efficientdet_net.py:10-95) + EfficientDetNetTrain."""
 
-    def __init__(self, model_desc, params: Dict[str, np.ndarray], dtype=torch.float64):
-        """model_desc: the GPU model object (used only for its *structure*: block specs,
-        level sizes, BiFPN topology, head repeats — all derived from config.py, which is
-        itself pinned against reference fixtures)."""
-        self.m = model_desc
-        self.cfg = model_desc.cfg
+    def __init__(self, cfg, params: Optional[Dict[str, np.ndarray]] = None, dtype=torch.float64, blocks_args=None):
+        self.cfg = cfg
         self.dtype = dtype
-        self.p = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in params.items()}
-        self.eps = self.cfg.batch_norm_epsilon
+        self.blocks = block_list(cfg, blocks_args)
+        first = _args((blocks_args if blocks_args is not None else B0_BLOCKS)[0])
+        self.stem_filters = round_filters(first[4], cfg.width_coefficient, cfg.depth_divisor)
+        self.eps = cfg.batch_norm_epsilon
+        self.F = cfg.fpn_num_filters
+        self.A = cfg.num_scales * len(cfg.aspect_ratios)
+        self.NC = cfg.num_classes
+        self.levels = list(range(cfg.min_level, cfg.max_level + 1))
+        ls = [cfg.image_size]  # global_params.py:206-208
+        for _ in range(cfg.max_level):
+            ls.append((ls[-1] + 1) // 2)
+        self.levels_size = ls
+        self.bb = cfg.backbone_name or "backbone"
+        n = len(self.blocks)
+        self.red_idx = [i for i in range(n) if i == n - 1 or self.blocks[i + 1]["s"] > 1]
+        self.recording = None
+        self.p = {}
+        if params is not None:
+            self.p = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in params.items()}
 
-    # ---- parameter helpers (build layouts -> torch conv weights)
-    def w1x1(self, name):  # [out][in] -> [out, in, 1, 1]
-        w = self.p[name]
-        return w[:, :, None, None]
+    # ---- parameters, created on first use (Keras lazy build)
+    def w(self, name, shape, init):
+        if self.recording is not None:
+            if name not in self.recording:
+                self.recording[name] = (tuple(shape), init)
+            else:
+                assert self.recording[name][0] == tuple(shape), (name, shape, self.recording[name])
+            return torch.zeros(shape, dtype=self.dtype, device="meta")
+        t = self.p[name]
+        assert tuple(t.shape) == tuple(shape), (name, tuple(t.shape), shape)
+        return t
 
-    def wdw(self, name, k):  # [k*k][C] -> [C, 1, k, k]
-        w = self.p[name]
-        return w.t().reshape(-1, 1, k, k)
+    def w1x1(self, name, out, cin, init):  # [out][in] -> [out, in, 1, 1]
+        return self.w(name, (out, cin), init)[:, :, None, None]
+
+    def wdw(self, name, k, C, init):  # [k*k][C] -> [C, 1, k, k]
+        return self.w(name, (k * k, C), init).t().reshape(C, 1, k, k)
 
     def bn(self, x, name, training, st):
-        return batch_norm(x, self.p, name, training, self.eps, st)
+        """Keras BatchNormalization (momentum 0.99, eps 1e-3) on NCHW x."""
+        C = x.shape[1]
+        g = self.w(name + "/gamma", (C,), ("const", 1.0))
+        b = self.w(name + "/beta", (C,), ("const", 0.0))
+        if self.recording is not None:
+            self.recording.setdefault("__bn__", []).append(name)
+        if training:
+            mean = x.mean(dim=(0, 2, 3))
+            var = ((x - mean[None, :, None, None]) ** 2).mean(dim=(0, 2, 3))
+            if st is not None:
+                st.batch[name] = (mean.detach(), var.detach(), x.shape[0] * x.shape[2] * x.shape[3])
+        elif self.recording is not None:
+            mean = var = torch.zeros(C, dtype=self.dtype, device="meta")
+        else:
+            mean, var = self.p[name + "/moving_mean"], self.p[name + "/moving_variance"]
+        inv = 1.0 / torch.sqrt(var + self.eps)
+        return (x - mean[None, :, None, None]) * (inv * g)[None, :, None, None] + b[None, :, None, None]
 
     # ---- layers
     def stem(self, x, training, st):
-        """layers/stem.py:37-38."""
-        bb = self.m.bb
-        w = self.p[f"{bb}/stem/conv2d/kernel"].permute(3, 2, 0, 1)  # HWIO -> OIHW
-        return swish(self.bn(conv_same(x, w, 2), f"{bb}/stem/tpu_batch_normalization", training, st))
+        """layers/stem.py:37-38 (conv 3x3 s2 SAME, no bias -> BN -> swish)."""
+        cs = self.stem_filters  # round_filters(blocks_args[0].input_filters) (stem.py:15-16)
+        w = self.w(f"{self.bb}/stem/conv2d/kernel", (3, 3, 3, cs), _cki(3, 3, cs)).permute(3, 2, 0, 1)
+        return swish(self.bn(conv_same(x, w, 2), f"{self.bb}/stem/tpu_batch_normalization", training, st))
 
     def mbconv(self, x, i, training, st):
         """layers/mb_conv_block.py:127-160 (no skip, no drop-connect)."""
-        sp = self.m.specs[i]
-        b = self.m.block_bns[i]
-        pre = f"{self.m.bb}/blocks_{i}"
-        if sp.expand_ratio != 1:
-            x = swish(self.bn(Fn.conv2d(x, self.w1x1(b["expand_w"])), b["bn0"].name, training, st))
-        k = sp.kernel_size
-        x = conv_same(x, self.wdw(f"{pre}/depthwise_conv2d/depthwise_kernel", k), sp.stride, groups=x.shape[1])
-        x = swish(self.bn(x, b["bn1"].name, training, st))
-        # SE (layers/se.py:35-39)
+        b = self.blocks[i]
+        pre = f"{self.bb}/blocks_{i}"
+        bn_name = _keras_counter_names("tpu_batch_normalization")
+        conv_name = _keras_counter_names("conv2d")
+        cin, e = b["cin"], b["cin"] * b["e"]
+        if b["e"] != 1:
+            n = conv_name()
+            x = Fn.conv2d(x, self.w1x1(f"{pre}/{n}/kernel", e, cin, _cki(1, 1, e)))
+            x = swish(self.bn(x, f"{pre}/{bn_name()}", training, st))
+        k = b["k"]
+        x = conv_same(x, self.wdw(f"{pre}/depthwise_conv2d/depthwise_kernel", k, e, _cki(k, k, 1)), b["s"], groups=e)
+        x = swish(self.bn(x, f"{pre}/{bn_name()}", training, st))
+        # SE (layers/se.py:35-39), width mb_conv_block.py:98-101
+        R = max(1, int(cin * b["se"]))
         s = x.mean(dim=(2, 3), keepdim=True)
-        s = Fn.conv2d(s, self.w1x1(f"{pre}/se/conv2d/kernel"), self.p[f"{pre}/se/conv2d/bias"])
-        s = Fn.conv2d(swish(s), self.w1x1(f"{pre}/se/conv2d_1/kernel"), self.p[f"{pre}/se/conv2d_1/bias"])
+        s = Fn.conv2d(s, self.w1x1(f"{pre}/se/conv2d/kernel", R, e, _cki(1, 1, R)),
+                      self.w(f"{pre}/se/conv2d/bias", (R,), ("const", 0.0)))
+        s = Fn.conv2d(swish(s), self.w1x1(f"{pre}/se/conv2d_1/kernel", e, R, _cki(1, 1, e)),
+                      self.w(f"{pre}/se/conv2d_1/bias", (e,), ("const", 0.0)))
         x = torch.sigmoid(s) * x
-        return self.bn(Fn.conv2d(x, self.w1x1(b["project_w"])), b["bn2"].name, training, st)
+        n = conv_name()
+        x = Fn.conv2d(x, self.w1x1(f"{pre}/{n}/kernel", b["cout"], e, _cki(1, 1, b["cout"])))
+        return self.bn(x, f"{pre}/{bn_name()}", training, st)
 
-    def resample(self, x, rr, H, training, st):
-        """ResampleFeatureMap.call (resample_feature_map.py:43-52)."""
-        if rr is not None and rr["conv"] is not None:
-            pre = rr["conv"]
-            x = Fn.conv2d(x, self.w1x1(f"{pre}/conv2d/kernel"), self.p[f"{pre}/conv2d/bias"])
-            x = self.bn(x, rr["bn"].name, training, st)
-        if x.shape[2] > H:
+    def resample(self, x, prefix, level_size, training, st):
+        """ResampleFeatureMap (resample_feature_map.py:14-52): decisions from the arriving
+        tensor's channels and height, as its lazy build() makes them."""
+        F = self.F
+        C = x.shape[1]
+        if C != F:
+            x = Fn.conv2d(x, self.w1x1(f"{prefix}/conv2d/kernel", F, C, ("glorot", C, F)),
+                          self.w(f"{prefix}/conv2d/bias", (F,), ("const", 0.0)))
+            x = self.bn(x, f"{prefix}/bn", training, st)
+        if x.shape[2] > level_size:
             x = maxpool_same(x)
-        elif x.shape[2] < H:
-            x = resize_nearest(x, H, H)
+        elif x.shape[2] < level_size:
+            x = resize_nearest(x, level_size, level_size)
         return x
 
-    def sepconv(self, x, pre, dwname, pwname, bname):
-        x = conv_same(x, self.wdw(f"{pre}/{dwname}", 3), 1, groups=x.shape[1])
-        return Fn.conv2d(x, self.w1x1(f"{pre}/{pwname}"), self.p[f"{pre}/{bname}"])
+    def sepconv(self, x, pre, dwname, pwname, bname, nout, dw_init, pw_init, b_init):
+        C = x.shape[1]
+        x = conv_same(x, self.wdw(f"{pre}/{dwname}", 3, C, dw_init), 1, groups=C)
+        return Fn.conv2d(x, self.w1x1(f"{pre}/{pwname}", nout, C, pw_init), self.w(f"{pre}/{bname}", (nout,), b_init))
+
+    # bifpn.py:108-116: (level, input node ids); ids 0..4 = P3..P7 inputs, 5.. = nodes
+    BIFPN_NODES = [(6, [3, 4]), (5, [2, 5]), (4, [1, 6]), (3, [0, 7]), (4, [1, 7, 8]), (5, [2, 6, 9]), (6, [3, 5, 10]),
+                   (7, [4, 11])]
 
     def bifpn_cell(self, c, feats, training, st):
-        """BiFPNNode.call / BiFPN.call (bifpn.py:59-67, 89-117)."""
+        """BiFPN.call / BiFPNNode.call / OpAfterCombine.call (bifpn.py:24-29, 59-67, 89-117)."""
+        assert len(feats) == 5, "bifpn.py:105 unpacks exactly P3..P7"
         nodes = list(feats)
-        nl = len(self.m.levels)
-        outs = {}
-        for j, node in enumerate(self.m.cells[c]):
-            lvl = node["level"]
-            H = self.m.level_hw[lvl][0]
-            pre = node["prefix"]
-            w = self.p[f"{pre}/WSM"]
+        F = self.F
+        for j, (lvl, ins) in enumerate(self.BIFPN_NODES):
+            pre = f"fpn_cell_{c}/node_{j}"
+            size = self.levels_size[lvl]
+            w = self.w(f"{pre}/WSM", (len(ins),), ("const", 1.0))
             wsum = w.sum()
             acc = None
-            for k, src in enumerate(node["inputs"]):
-                r = self.resample(nodes[src], node["resample"][k], H, training, st) * w[k] / (wsum + 0.0001)
+            for k, src in enumerate(ins):
+                r = self.resample(nodes[src], f"{pre}/resample_{k}", size, training, st) * w[k] / (wsum + 0.0001)
                 acc = r if acc is None else acc + r
             op = f"{pre}/op_after_combine"
             y = self.sepconv(swish(acc), op, "separable_conv2d/depthwise_kernel", "separable_conv2d/pointwise_kernel",
-                             "separable_conv2d/bias")
-            y = self.bn(y, node["bn"].name, training, st)
+                             "separable_conv2d/bias", F, ("glorot", 9 * F, 9), ("glorot", F, F), ("const", 0.0))
+            y = self.bn(y, f"{op}/batch_normalization", training, st)
             nodes.append(y)
-            if j >= nl - 2:
-                outs[lvl] = y
-        return [outs[l] for l in self.m.levels]
+        return nodes[-5:]  # (p3_2, p4_2, p5_2, p6_2, p7_2)
 
     def head(self, net, feats, training, st, masks=None):
         """ClassNet.call / BoxNet.call (class_net.py:79-103, box_net.py:81-102)."""
-        h = self.m.heads[net]
+        tag = "class" if net == "class_net" else "box"
+        last = self.NC if net == "class_net" else 4
+        nout = self.A * last
+        bias0 = -math.log((1 - 0.01) / 0.01) if net == "class_net" else 0.0  # class_net.py:74
+        F = self.F
         surv = self.cfg.survival_prob
+        vs = lambda fan: ("vs_fan_in", fan)  # noqa: E731
         out = []
-        for li, lvl in enumerate(self.m.levels):
+        for li, lvl in enumerate(self.levels):
             image = feats[li]
-            for i, pre in enumerate(h["convs"]):
+            for i in range(self.cfg.box_class_repeats):
                 orig = image
-                image = self.sepconv(image, pre, "depthwise_kernel", "pointwise_kernel", "bias")
-                image = swish(self.bn(image, h["bns"][i][li].name, training, st))
+                pre = f"{net}/{tag}-{i}"
+                image = self.sepconv(image, pre, "depthwise_kernel", "pointwise_kernel", "bias", F, vs(9 * F), vs(F),
+                                     ("const", 0.0))
+                image = swish(self.bn(image, f"{net}/{tag}-{i}-bn-{lvl}", training, st))
                 if i > 0 and surv:
                     if training:
                         m = masks[net][i - 1][li] if masks is not None else None
                         if m is not None:
                             image = image * torch.as_tensor(m, dtype=self.dtype)[:, None, None, None]
                     image = image + orig
-            pre = h["predict"]
-            c = self.sepconv(image, pre, "depthwise_kernel", "pointwise_kernel", "bias")
+            pre = f"{net}/{tag}-predict"
+            c = self.sepconv(image, pre, "depthwise_kernel", "pointwise_kernel", "bias", nout, vs(9 * F), vs(F),
+                             ("const", bias0))
             B, _, H, W = c.shape
-            last = h["nout"] // self.m.A
-            out.append(c.permute(0, 2, 3, 1).reshape(B, H, W, self.m.A, last))
+            out.append(c.permute(0, 2, 3, 1).reshape(B, H, W, self.A, last))
         return out
+
+    def _input(self, x_nhwc):
+        if isinstance(x_nhwc, torch.Tensor) and x_nhwc.device.type == "meta":
+            return x_nhwc.permute(0, 3, 1, 2)
+        return torch.as_tensor(np.asarray(x_nhwc), dtype=self.dtype).permute(0, 3, 1, 2)
+
+    def _backbone(self, x, training, st):
+        x = self.stem(x, training, st)
+        reds = []
+        for i in range(len(self.blocks)):
+            x = self.mbconv(x, i, training, st)
+            if i in self.red_idx:
+                reds.append(x)
+        return [x] + reds
 
     def backbone(self, x_nhwc, training, st: Optional[BNState] = None):
         """BackboneModel.call (backbone_model.py:96-148): [features, reduction_1..5], NHWC."""
-        x = torch.as_tensor(np.asarray(x_nhwc), dtype=self.dtype).permute(0, 3, 1, 2)
-        x = self.stem(x, training, st)
-        reds = []
-        for i in range(len(self.m.specs)):
-            x = self.mbconv(x, i, training, st)
-            if i in self.m.red_idx:
-                reds.append(x)
-        return [t.permute(0, 2, 3, 1) for t in [x] + reds]
+        return [t.permute(0, 2, 3, 1) for t in self._backbone(self._input(x_nhwc), training, st)]
 
     def forward(self, x_nhwc, training, masks=None, st: Optional[BNState] = None):
-        """EfficientDetNet.call: returns (boxes list, classes list) NHWC [B,H,W,A,*]."""
-        x = torch.as_tensor(np.asarray(x_nhwc), dtype=self.dtype).permute(0, 3, 1, 2)
-        x = self.stem(x, training, st)
-        reds = []
-        for i in range(len(self.m.specs)):
-            x = self.mbconv(x, i, training, st)
-            if i in self.m.red_idx:
-                reds.append(x)
-        all_feats = [x] + reds
-        feats = [all_feats[l] for l in self.m.levels if l < len(all_feats)]
-        for l in self.m.levels:
-            if l < len(all_feats):
-                continue
-            feats.append(self.resample(feats[-1], self.m.resample_extra[l], self.m.level_hw[l][0], training, st))
+        """EfficientDetNet.call (efficientdet_net.py:76-95): (boxes list, classes list), NHWC
+        [B, H, W, A, *]."""
+        all_feats = self._backbone(self._input(x_nhwc), training, st)
+        feats = all_feats[self.cfg.min_level:self.cfg.max_level + 1]
+        for level in range(6, self.cfg.max_level + 1):  # efficientdet_net.py:28-35, 84-85
+            feats.append(self.resample(feats[-1], f"resample_p{level}", self.levels_size[level], training, st))
         for c in range(self.cfg.fpn_cell_repeats):
             feats = self.bifpn_cell(c, feats, training, st)
         self.fpn_out = feats
@@ -267,10 +396,24 @@ class RefEfficientDet:
         return loss, parts
 
 
+def param_specs(cfg, blocks_args=None) -> "OrderedDict[str, tuple]":
+    """Every variable the reference model creates for ``cfg``, in creation order:
+    name -> (shape, initialiser record).  BN moving statistics are listed by ``bn_names``."""
+    r = RefEfficientDet(cfg, None, torch.float32, blocks_args)
+    r.recording = OrderedDict()
+    S = cfg.image_size
+    r.forward(torch.zeros((1, S, S, 3), dtype=torch.float32, device="meta"), True)
+    rec = r.recording
+    bns = rec.pop("__bn__")
+    out = OrderedDict((k, v) for k, v in rec.items())
+    out.bn_names = list(OrderedDict.fromkeys(bns))  # type: ignore[attr-defined]
+    return out
+
+
 def ref_train_step(ref: RefEfficientDet, x, y_box, y_cls, y_mask, masks=None, lr=0.01, momentum=0.9, clip=10.0,
                    ema_decay=0.9998, mom_state=None, ema_state=None, bn_momentum=0.99):
     """train_step_normal (efficientdet_net_train.py:112-132) + SGD momentum + EMA + BN moving
-    update.  Returns (loss, gnorm, new_params dict, grads dict, bnstate)."""
+    update.  Returns (loss, gnorm, new_params dict, grads dict, bnstate, parts)."""
     for v in ref.p.values():
         v.requires_grad_(False)
     train_keys = [k for k in ref.p if not (k.endswith("/moving_mean") or k.endswith("/moving_variance"))]
@@ -295,4 +438,6 @@ def ref_train_step(ref: RefEfficientDet, x, y_box, y_cls, y_mask, masks=None, lr
         mm, mv = ref.p[name + "/moving_mean"], ref.p[name + "/moving_variance"]
         new[name + "/moving_mean"] = mm - (mm - mean) * (1 - bn_momentum)
         new[name + "/moving_variance"] = mv - (mv - unb) * (1 - bn_momentum)
+    for p in ref.p.values():
+        p.requires_grad_(False)
     return loss.detach(), gnorm.detach(), new, {k: g.detach() for k, g in grads.items()}, st, parts

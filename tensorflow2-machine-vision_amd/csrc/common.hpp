@@ -109,14 +109,8 @@ __device__ __forceinline__ float dswishf_(float x) {
   return s * (1.f + x * (1.f - s));
 }
 
-// fp64 statistics accumulation.  EDET_EXP_NOATOM drops it: a timing experiment only (the
-// statistics are then wrong), used to price same-address atomic serialisation.
-__device__ __forceinline__ void stat_add(double* p, double v) {
-#ifdef EDET_EXP_NOATOM
-  if (v == 1234.5)
-#endif
-    atomicAdd(p, v);
-}
+// fp64 statistics accumulation (one atomic per channel per block; DESIGN.md "Reproducibility")
+__device__ __forceinline__ void stat_add(double* p, double v) { atomicAdd(p, v); }
 
 // Sum over the four 16-lane rows of a wave (lane bits 4 and 5), result in every lane: the
 // MFMA epilogues reduce a column's 4 row groups this way.  gfx950's v_permlane16/32_swap are

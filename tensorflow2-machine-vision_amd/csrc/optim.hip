@@ -20,8 +20,12 @@ __device__ float sched_lr(const edet_sched& s, int step) {
   return 0.5f * s.adjusted_lr * (1.f + cosf(3.14159265358979323846f * fs / decay));
 }
 
+// Norm pass.  Exactly EDET_OPT_NORM_BLOCKS blocks, each writing its two partial sums to its
+// own slots (fp64, no atomics): the apply pass folds the slots in one fixed order, so every
+// data-parallel replica holding the same all-reduced gradient computes the same gnorm bit for
+// bit and the clip factor -- and hence the parameters -- never drift between replicas.
 __global__ __launch_bounds__(256) void k_opt_norm(const float* w, const float* g, int64_t n, int64_t n_l2,
-                                                  edet_sched sc, float* scalars, int32_t* step) {
+                                                  edet_sched sc, float* scalars, double* partials, int32_t* step) {
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float gs = 0.f, ws = 0.f;
@@ -39,8 +43,8 @@ __global__ __launch_bounds__(256) void k_opt_norm(const float* w, const float* g
   if (lane == 0) { red[0][wave] = gs; red[1][wave] = ws; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    atomicAdd(scalars + 1, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
-    atomicAdd(scalars + 2, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+    partials[blockIdx.x] = (double)red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    partials[EDET_OPT_NORM_BLOCKS + blockIdx.x] = (double)red[1][0] + red[1][1] + red[1][2] + red[1][3];
     if (blockIdx.x == 0) {
       const int s = *step;
       scalars[4] = sched_lr(sc, s);
@@ -49,10 +53,30 @@ __global__ __launch_bounds__(256) void k_opt_norm(const float* w, const float* g
   }
 }
 
+__device__ __forceinline__ double wave_sum64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// sum of the norm partials, fixed order (thread t owns slot t; wave trees; waves 0..3)
+__device__ double2 fold_partials(const double* partials) {
+  static_assert(EDET_OPT_NORM_BLOCKS == 256, "one slot per thread");
+  __shared__ double red[2][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const double a = wave_sum64(partials[threadIdx.x]);
+  const double b = wave_sum64(partials[EDET_OPT_NORM_BLOCKS + threadIdx.x]);
+  if (lane == 0) { red[0][wave] = a; red[1][wave] = b; }
+  __syncthreads();
+  return make_double2(((red[0][0] + red[0][1]) + red[0][2]) + red[0][3], ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3]);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_opt_apply(float* w, const float* g, float* v, float* ema, int64_t n,
-                                                   int64_t n_l2, edet_sched sc, float* scalars, T* wc) {
-  const float gnorm = sqrtf(scalars[1]);
+                                                   int64_t n_l2, edet_sched sc, float* scalars,
+                                                   const double* partials, T* wc) {
+  const double2 sums = fold_partials(partials);
+  const float gnorm = (float)sqrt(sums.x);
   const float clip = sc.clip_norm / fmaxf(gnorm, sc.clip_norm);
   const float lr = scalars[4];
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
@@ -68,8 +92,10 @@ __global__ __launch_bounds__(256) void k_opt_apply(float* w, const float* g, flo
     if (wc) wc[i] = from_f<T>(wv);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
+    scalars[1] = (float)sums.x;
+    scalars[2] = (float)sums.y;
     scalars[3] = gnorm;
-    scalars[0] += sc.l2_weight * 0.5f * scalars[2];
+    scalars[0] += (float)((double)sc.l2_weight * 0.5 * sums.y);
   }
 }
 
@@ -135,24 +161,21 @@ using namespace edet;
 extern "C" {
 
 int edet_opt_norm(const float* w, const float* g, int64_t n, int64_t n_l2,
-                  const edet_sched* sched, float* scalars, int32_t* step,
+                  const edet_sched* sched, float* scalars, double* partials, int32_t* step,
                   edet_stream_t stream) {
-  EDET_REQUIRE(w && g && sched && scalars && step && n_l2 <= n, "opt_norm: bad argument");
-  // 256 blocks: every block ends in two same-address float atomics, and 2048 of them
-  // serialised in L2 for ~40 us
-  const int nb = std::min(grid_for(n), 256);
-  hipLaunchKernelGGL(k_opt_norm, dim3(nb), dim3(256), 0, (hipStream_t)stream, w, g, n, n_l2, *sched,
-                     scalars, step);
+  EDET_REQUIRE(w && g && sched && scalars && partials && step && n_l2 <= n, "opt_norm: bad argument");
+  hipLaunchKernelGGL(k_opt_norm, dim3(EDET_OPT_NORM_BLOCKS), dim3(256), 0, (hipStream_t)stream, w, g, n, n_l2,
+                     *sched, scalars, partials, step);
   return check_launch("edet opt_norm");
 }
 
 int edet_opt_apply(float* w, const float* g, float* v, float* ema, int64_t n, int64_t n_l2,
-                   const edet_sched* sched, float* scalars, int dtype, void* wcompute,
+                   const edet_sched* sched, float* scalars, const double* partials, int dtype, void* wcompute,
                    edet_stream_t stream) {
-  EDET_REQUIRE(w && g && v && sched && scalars && n_l2 <= n, "opt_apply: bad argument");
+  EDET_REQUIRE(w && g && v && sched && scalars && partials && n_l2 <= n, "opt_apply: bad argument");
   EDET_DTYPE_DISPATCH(dtype, T, {
     hipLaunchKernelGGL(k_opt_apply<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, w, g, v, ema, n,
-                       n_l2, *sched, scalars, (T*)wcompute);
+                       n_l2, *sched, scalars, partials, (T*)wcompute);
     return check_launch("edet opt_apply");
   });
 }

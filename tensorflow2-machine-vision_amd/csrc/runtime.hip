@@ -70,7 +70,7 @@ extern "C" {
 
 const char* edet_last_error(void) { return edet::g_err; }
 
-int edet_abi_version(void) { return 3; }  // 3: edet_fuse_input.pool_arg
+int edet_abi_version(void) { return 4; }  // 3: edet_fuse_input.pool_arg; 4: opt norm partials
 
 int edet_set_workspace(void* ptr, size_t bytes) {
   edet::g_ws = ptr;

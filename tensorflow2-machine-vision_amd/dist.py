@@ -111,6 +111,40 @@ def timed(ctx: DPContext, fn: Callable[[], None], steps: int, sync: Callable[[],
     return time.perf_counter() - t0
 
 
+def graphed_train_step(model, data, allreduce: Optional[Callable[[torch.Tensor], None]] = None) -> Callable[[], None]:
+    """Capture ``model.train_step(data)`` in HIP graphs and return the replay callable.
+
+    One replica: the whole step is one graph.  Data parallel: three graphs -- prepare
+    (targets, this replica's N+) | compute (forward, fused loss, backward) | optimizer -- with
+    the N+ all-reduce and the flat gradient all-reduce issued between them on the same
+    stream, so the collectives stay outside the captured work (RCCL/gloo calls are not
+    captured).  ``data``'s tensors must stay alive and in place while the graphs are used."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    if allreduce is None:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            model.train_step(data)
+        return g.replay
+    g0, g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g0):
+        t_pyr = model.prepare_step(data)
+    with torch.cuda.graph(g1):
+        model.compute_step(data, *t_pyr)
+    with torch.cuda.graph(g2):
+        model.apply_gradients()
+
+    def step():
+        g0.replay()
+        allreduce(model.scalars[5:6])
+        g1.replay()
+        allreduce(model.P.g)
+        g2.replay()
+
+    step.graphs = (g0, g1, g2)  # keep the graphs alive with the callable
+    return step
+
+
 def shutdown(ctx: DPContext) -> None:
     if ctx.distributed and tdist.is_initialized():
         tdist.barrier()

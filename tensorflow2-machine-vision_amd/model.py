@@ -435,7 +435,7 @@ class EfficientDetNetTrain(EfficientDetNet):
     def __init__(self, blocks_args=None, global_params: Optional[Config] = None, anchors: Optional[Anchors] = None,
                  name: str = "", min_lr: float = 1e-6, dtype: str = "bf16", device="cuda", seed: int = 0,
                  lr_schedule: Optional[Dict] = None, world_size: int = 1, grad_allreduce=None,
-                 npos_allreduce=None, drop_seed: int = 1234):
+                 npos_allreduce=None, drop_seed: int = 1234, rank: int = 0):
         super().__init__(blocks_args, global_params, name, dtype, device, seed)
         cfg = self.cfg
         self.anchors = anchors
@@ -443,9 +443,13 @@ class EfficientDetNetTrain(EfficientDetNet):
         self.world_size = world_size
         self.grad_allreduce = grad_allreduce
         self.npos_allreduce = npos_allreduce
-        self.drop_seed = drop_seed
+        # each data-parallel replica draws its own drop-connect masks (MirroredStrategy replicas
+        # draw tf.random.uniform independently, drop_connect.py:13): fold the rank into the seed
+        self.rank = rank
+        self.drop_seed = drop_seed ^ (0x9E3779B97F4A7C15 * rank & 0xFFFFFFFFFFFFFFFF) if rank else drop_seed
         dev = self.eng.device
         self.scalars = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.norm_partials = torch.zeros(2 * L.OPT_NORM_BLOCKS, dtype=torch.float64, device=dev)
         self.level_parts = torch.zeros(2 * L.MAX_SEG, dtype=torch.float32, device=dev)
         self.step_counter = torch.zeros(1, dtype=torch.int32, device=dev)
         s = lr_schedule or {}
@@ -549,13 +553,21 @@ class EfficientDetNetTrain(EfficientDetNet):
         P = self.P
         s = stream()
         L.call("edet_opt_norm", vp(P.w), vp(P.g), P.numel, P.n_l2, self.sched, vp(self.scalars),
-               vp(self.step_counter), s)
+               vp(self.norm_partials), vp(self.step_counter), s)
         L.call("edet_opt_apply", vp(P.w), vp(P.g), vp(P.v), vp(P.ema), P.numel, P.n_l2, self.sched, vp(self.scalars),
-               self.eng.dt, vp(P.wc) if P.wc is not P.w else None, s)
+               vp(self.norm_partials), self.eng.dt, vp(P.wc) if P.wc is not P.w else None, s)
         P.refresh_compute_copy(cast=False)  # transposed 1x1 copies for the next dgrad
         cfg = self.cfg
         L.call("edet_bn_update_moving", P.n_bn, vp(P.bn_tstats[0]), vp(P.bn_tstats[1]), vp(P.bn_count),
                float(cfg.batch_norm_momentum), vp(P.bn_mm), vp(P.bn_mv), s)
+
+    def load_state_dict(self, sd):
+        """Weights (and BN moving statistics) from a checkpoint, with fresh optimizer state:
+        zero momentum, EMA = the loaded weights, step counter 0 -- the reference restarts the
+        same way from its weights-only h5 (train.py:127-129, 150)."""
+        super().load_state_dict(sd)
+        memset0(self.P.v)
+        memset0(self.step_counter)
 
     def test_step(self, data):
         """test_step (efficientdet_net_train.py:135-169): inference-mode forward, the same loss

@@ -71,7 +71,7 @@ def _flat_grads(ref, loss):
 
 def _ref(m):
     from oracle.ref_model import RefEfficientDet
-    ref = RefEfficientDet(m, m.state_dict())
+    ref = RefEfficientDet(m.cfg, m.state_dict())
     for k, v in ref.p.items():
         v.requires_grad_(not (k.endswith("/moving_mean") or k.endswith("/moving_variance")))
     return ref

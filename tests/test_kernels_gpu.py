@@ -437,11 +437,16 @@ def test_stem(dt, shape, workspace_mode):
 
 # ----------------------------------------------------------------- loss
 @pytest.mark.parametrize("dt", DTS)
-def test_detection_loss(dt):
-    rng = np.random.default_rng(21)
-    A, NC = 9, 5
-    pyr = Pyr(2, [(4, 4), (2, 2)])
-    ldc, ldb = 48, 40
+@pytest.mark.parametrize("NC,ldc,sizes", [(5, 48, [(4, 4), (2, 2)]),
+                                          # the D0 headline geometry: 81 classes, 729 logits in
+                                          # rows of 736 (the NC >= 8 stepping path of k_loss)
+                                          (81, 736, [(8, 8), (4, 4), (2, 2), (1, 1), (1, 1)]),
+                                          (8, 72, [(6, 5), (3, 3)])])
+def test_detection_loss(dt, NC, ldc, sizes):
+    rng = np.random.default_rng(21 + NC)
+    A = 9
+    pyr = Pyr(2, sizes)
+    ldb = 40
     cls = torch.zeros(pyr.rows, ldc)
     cls[:, : A * NC] = rnd(rng, pyr.rows, A * NC, scale=3.0)
     box = torch.zeros(pyr.rows, ldb)
@@ -450,9 +455,10 @@ def test_detection_loss(dt):
     ct = torch.tensor(rng.integers(0, NC, (pyr.rows, A)), dtype=torch.int32)
     bt = rnd(rng, pyr.rows, A, 4, scale=0.2)
     bt[rng.random((pyr.rows, A, 4)) < 0.5] = 0.0
-    pad = slice(pyr.seg_rows(0), pyr.row_off[1])  # padding rows between the levels: never read
-    ct[pad] = 0
-    bt[pad] = 0.0
+    for s in range(pyr.nseg - 1):  # padding rows between the levels: never read
+        pad = slice(pyr.row_off[s] + pyr.seg_rows(s), pyr.row_off[s + 1])
+        ct[pad] = 0
+        bt[pad] = 0.0
     mask = (ct > 0).to(torch.uint8)
     npos = zeros(1)
     mask_g = mask.to(DEV)
@@ -494,38 +500,77 @@ def test_detection_loss(dt):
 
 
 # ----------------------------------------------------------------- optimizer
-def test_optimizer_step():
-    rng = np.random.default_rng(2)
+def _sched_lr(step, adj=0.08, init=0.008, warm=10, total=100):
+    """CosineLrSchedule.__call__ (efficientnet/train.py:55-63)."""
+    if step < warm:
+        return init + step / warm * (adj - init)
+    return 0.5 * adj * (1 + np.cos(np.pi * step / (total - warm)))
+
+
+@pytest.mark.parametrize("steps,start,clip", [(1, 3, 10.0), (4, 8, 10.0), (3, 57, 10.0), (2, 20, 50.0)])
+def test_optimizer_step(steps, start, clip):
+    """L2 + clip_by_global_norm + SGD momentum + EMA over several consecutive steps, through
+    the warm-up -> cosine switch (start 8, 4 steps) and deep in the cosine phase."""
+    rng = np.random.default_rng(2 + start)
     n, n_l2 = 10000, 6000
     w = g(rnd(rng, n))
-    gr = g(rnd(rng, n) * 3)
     v = g(rnd(rng, n) * 0.1)
     ema = g(rnd(rng, n))
     sc = L.Sched()
     sc.adjusted_lr, sc.warmup_init, sc.warmup_steps, sc.total_steps = 0.08, 0.008, 10, 100
-    sc.momentum, sc.ema_decay, sc.clip_norm, sc.l2_weight = 0.9, 0.9998, 10.0, 4e-5
+    sc.momentum, sc.ema_decay, sc.clip_norm, sc.l2_weight = 0.9, 0.9998, clip, 4e-5
     scal = zeros(8)
-    step = torch.tensor([3], dtype=torch.int32, device=DEV)
-    W0, G0, V0, E0 = (t.double().cpu() for t in (w, gr, v, ema))
+    parts = torch.zeros(2 * L.OPT_NORM_BLOCKS, dtype=torch.float64, device=DEV)
+    step = torch.tensor([start], dtype=torch.int32, device=DEV)
+    W, V, E = (t.double().cpu() for t in (w, v, ema))
     wc = torch.empty(n, dtype=torch.bfloat16, device=DEV)
-    L.call("edet_opt_norm", vp(w), vp(gr), n, n_l2, sc, vp(scal), vp(step), stream())
-    L.call("edet_opt_apply", vp(w), vp(gr), vp(v), vp(ema), n, n_l2, sc, vp(scal), L.BF16, vp(wc), stream())
-    gg = G0.clone()
-    gg[:n_l2] += 4e-5 * W0[:n_l2]
-    gn = gg.norm()
-    lr = 0.008 + 3 / 10 * (0.08 - 0.008)
-    gg *= 10.0 / max(float(gn), 10.0)
-    V1 = 0.9 * V0 - lr * gg
-    W1 = W0 + V1
-    E1 = E0 - (1 - 0.9998) * (E0 - W1)
-    close(scal[3], gn, "f32", rtol=1e-5)
-    close(scal[4], torch.tensor(lr), "f32", rtol=1e-6)
-    close(scal[0], 4e-5 * (W0[:n_l2] ** 2).sum() / 2, "f32", rtol=1e-5)
-    close(w, W1, "f32", rtol=1e-5, atol=1e-6)
-    close(v, V1, "f32", rtol=1e-5, atol=1e-6)
-    close(ema, E1, "f32", rtol=1e-5, atol=1e-6)
-    close(wc, W1, "bf16")
-    assert int(step.item()) == 4
+    for i in range(steps):
+        gr = g(rnd(rng, n) * 3)
+        G0 = gr.double().cpu()
+        W0 = W.clone()
+        L.call("edet_opt_norm", vp(w), vp(gr), n, n_l2, sc, vp(scal), vp(parts), vp(step), stream())
+        L.call("edet_opt_apply", vp(w), vp(gr), vp(v), vp(ema), n, n_l2, sc, vp(scal), vp(parts), L.BF16, vp(wc),
+               stream())
+        gg = G0.clone()
+        gg[:n_l2] += 4e-5 * W0[:n_l2]
+        gn = gg.norm()
+        lr = _sched_lr(start + i)
+        gg *= clip / max(float(gn), clip)
+        V = 0.9 * V - lr * gg
+        W = W0 + V
+        E = E - (1 - 0.9998) * (E - W)
+        close(scal[3], gn, "f32", rtol=1e-5)
+        close(scal[4], torch.tensor(lr), "f32", rtol=2e-6, atol=1e-9)
+    close(w, W, "f32", rtol=1e-5, atol=1e-6)
+    close(v, V, "f32", rtol=1e-5, atol=1e-6)
+    close(ema, E, "f32", rtol=1e-5, atol=1e-6)
+    close(wc, W, "bf16")
+    assert int(step.item()) == start + steps
+
+
+def test_optimizer_norm_is_bit_reproducible():
+    """The clip factor depends on gnorm; data-parallel replicas apply it to the same
+    all-reduced gradient and must get the same bits: repeated norm passes over one
+    gradient give identical gnorm and identical updated weights, with clipping active."""
+    rng = np.random.default_rng(5)
+    n, n_l2 = 3_000_000, 2_000_000
+    gr = g(rnd(rng, n) * 30)
+    w0 = g(rnd(rng, n))
+    sc = L.Sched()
+    sc.fixed_lr, sc.momentum, sc.ema_decay, sc.clip_norm, sc.l2_weight = 0.01, 0.9, 0.9998, 1.0, 4e-5
+    outs = []
+    for _ in range(3):
+        w, v, ema = w0.clone(), torch.zeros_like(w0), w0.clone()
+        scal = zeros(8)
+        parts = torch.zeros(2 * L.OPT_NORM_BLOCKS, dtype=torch.float64, device=DEV)
+        step = torch.zeros(1, dtype=torch.int32, device=DEV)
+        L.call("edet_opt_norm", vp(w), vp(gr), n, n_l2, sc, vp(scal), vp(parts), vp(step), stream())
+        L.call("edet_opt_apply", vp(w), vp(gr), vp(v), vp(ema), n, n_l2, sc, vp(scal), vp(parts), L.F32, None,
+               stream())
+        outs.append((scal.clone(), w))
+    assert float(outs[0][0][3]) > 10 * sc.clip_norm  # clipping active
+    for s, w in outs[1:]:
+        assert torch.equal(s[3], outs[0][0][3]) and torch.equal(w, outs[0][1])
 
 
 def test_bn_moving_update_and_inference_stats():

@@ -94,7 +94,7 @@ def test_forward_parity_fp32(training):
     fm = fixed_masks(m)
     masks = {"class_net": torch.tensor(fm[0]).cuda(), "box_net": torch.tensor(fm[1]).cuda()}
     boxes, classes = m.call(torch.tensor(x).cuda(), training=training, masks=masks if training else None)
-    ref = RefEfficientDet(m, m.state_dict())
+    ref = RefEfficientDet(m.cfg, m.state_dict())
     rmasks = {"class_net": fm[0], "box_net": fm[1]}
     rb, rc = ref.forward(x, training, rmasks if training else None)
     for l in range(5):
@@ -118,7 +118,7 @@ def test_train_step_parity_fp32():
     fm = fixed_masks(m)
     m.fixed_masks = {"class_net": torch.tensor(fm[0]).cuda(), "box_net": torch.tensor(fm[1]).cuda()}
     sd0 = m.state_dict()
-    ref = RefEfficientDet(m, sd0)
+    ref = RefEfficientDet(m.cfg, sd0)
     loss_r, gn_r, new_r, grads_r, st, parts = ref_train_step(ref, x, yb, yc, ym, {"class_net": fm[0], "box_net": fm[1]},
                                                              lr=0.01)
     out = m.train_step((torch.tensor(x).cuda(), t))
@@ -285,7 +285,7 @@ def test_test_step_loss_and_map():
     data = (torch.tensor(x).cuda(), torch.tensor(boxes), torch.tensor(cls),
             [torch.tensor(v) for v in yb], [torch.tensor(v) for v in yc], [torch.tensor(v) for v in ym])
     out = m.test_step(data)
-    ref = RefEfficientDet(m, m.state_dict())
+    ref = RefEfficientDet(m.cfg, m.state_dict())
     with torch.no_grad():
         rb, rc = ref.forward(x, False)
         rloss, _ = ref.detection_loss(rb, rc, yb, yc, ym)
@@ -311,7 +311,7 @@ def test_backbone_b0_224_parity_fp32(training):
     m = EfficientDetNet(efficientnet_b0_blocks(), c, dtype="f32", seed=5)
     x = np.random.default_rng(5).random((2, 224, 224, 3), dtype=np.float32)
     outs = m.backbone(torch.tensor(x).cuda(), training=training)
-    ref = RefEfficientDet(m, m.state_dict()).backbone(x, training)
+    ref = RefEfficientDet(m.cfg, m.state_dict()).backbone(x, training)
     assert [tuple(o.shape) for o in outs] == [(2, 7, 7, 320), (2, 112, 112, 16), (2, 56, 56, 24), (2, 28, 28, 40),
                                                (2, 14, 14, 112), (2, 7, 7, 320)]
     for o, r in zip(outs, ref):
@@ -326,7 +326,7 @@ def test_d4_topology_forward_parity_fp32():
     assert len(m.specs) == 32 and m.F == 224 and len(m.cells) == 7
     x = np.random.default_rng(6).random((1, 256, 256, 3), dtype=np.float32)
     boxes, classes = m.call(torch.tensor(x).cuda(), training=False)
-    rb, rc = RefEfficientDet(m, m.state_dict()).forward(x, False)
+    rb, rc = RefEfficientDet(m.cfg, m.state_dict()).forward(x, False)
     for l in range(5):
         assert rel_err(boxes[l].cpu(), rb[l].detach()) < 1e-3, l
         assert rel_err(classes[l].cpu(), rc[l].detach()) < 1e-3, l
