@@ -129,12 +129,29 @@ class BNState:
         self.batch = {}  # name -> (mean, var_biased, count)
 
 
-def maxpool_same(x):
-    """MaxPooling2D 3x3 s2 'SAME' (resample_feature_map.py:35-38): padded cells ignored."""
+def maxpool_same(x, route=None, stats=None):
+    """MaxPooling2D 3x3 s2 'SAME' (resample_feature_map.py:35-38): padded cells ignored.
+
+    ``route`` (optional, same shape as x): choose each window's argmax on these values instead
+    of x's own (first maximum in row-major order, like TF's MaxPoolGrad and torch) and take x
+    at that position.  Parity tests pass the product's own fp32 values here so that windows
+    whose top two entries lie within fp32 rounding of each other -- where fp32 and fp64
+    legitimately pick different winners and the gradient is routed to a different pixel --
+    are decided the same way on both sides; ``stats['rerouted']`` counts the windows whose
+    decision that changed.  The forward value changes by at most that near-tie gap."""
     pt, pb = same_pad(x.shape[2], 3, 2)
     pl, pr = same_pad(x.shape[3], 3, 2)
-    x = Fn.pad(x, (pl, pr, pt, pb), value=-math.inf)
-    return Fn.max_pool2d(x, 3, 2)
+    xp = Fn.pad(x, (pl, pr, pt, pb), value=-math.inf)
+    if route is None:
+        return Fn.max_pool2d(xp, 3, 2)
+    rp = Fn.pad(torch.as_tensor(route, dtype=x.dtype), (pl, pr, pt, pb), value=-math.inf)
+    _, idx = Fn.max_pool2d(rp, 3, 2, return_indices=True)
+    N, C, Ho, Wo = idx.shape
+    if stats is not None:
+        _, own = Fn.max_pool2d(xp.detach(), 3, 2, return_indices=True)
+        stats["rerouted"] = stats.get("rerouted", 0) + int((own != idx).sum())
+        stats["windows"] = stats.get("windows", 0) + idx.numel()
+    return xp.reshape(N, C, -1).gather(2, idx.reshape(N, C, -1)).reshape(N, C, Ho, Wo)
 
 
 def resize_nearest(x, H, W):
@@ -177,9 +194,38 @@ class RefEfficientDet:
         n = len(self.blocks)
         self.red_idx = [i for i in range(n) if i == n - 1 or self.blocks[i + 1]["s"] > 1]
         self.recording = None
+        self.trace = None  # debug: name -> intermediate tensor (the product's activation names)
+        self.routes = None  # name -> values deciding max-pool winners (see maxpool_same)
+        self.route_stats = {}
+        self.store = None  # storage rounding of every tensor the product keeps in HBM (bf16 emulation)
+        self._names = {}
         self.p = {}
         if params is not None:
             self.p = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in params.items()}
+
+    def _t(self, name, x):
+        """Name an intermediate with the product's activation name (tracing / pool routing)."""
+        if self.recording is None:
+            if self.trace is not None:
+                if x.requires_grad:
+                    x.retain_grad()
+                self.trace[name] = x
+            if self.routes is not None:
+                self._names[id(x)] = name
+        return x
+
+    def _st(self, x):
+        """A tensor the product stores (conv outputs, SE output, fusion sums, residual sums,
+        pooled values): rounded by ``store`` when emulating a storage precision."""
+        return x if self.store is None or self.recording is not None else self.store(x)
+
+    def _pool(self, x, stored):
+        route = None
+        if self.routes is not None:
+            route = self.routes.get(self._names.get(id(x)))
+        y = maxpool_same(x, route, self.route_stats)
+        # resample_p6/p7 are stored; a BiFPN input is pooled inside the fusion kernel
+        return self._st(y) if stored else y
 
     # ---- parameters, created on first use (Keras lazy build)
     def w(self, name, shape, init):
@@ -223,7 +269,8 @@ class RefEfficientDet:
         """layers/stem.py:37-38 (conv 3x3 s2 SAME, no bias -> BN -> swish)."""
         cs = self.stem_filters  # round_filters(blocks_args[0].input_filters) (stem.py:15-16)
         w = self.w(f"{self.bb}/stem/conv2d/kernel", (3, 3, 3, cs), _cki(3, 3, cs)).permute(3, 2, 0, 1)
-        return swish(self.bn(conv_same(x, w, 2), f"{self.bb}/stem/tpu_batch_normalization", training, st))
+        return self._t("stem", swish(self.bn(self._st(conv_same(x, w, 2)), f"{self.bb}/stem/tpu_batch_normalization",
+                                             training, st)))
 
     def mbconv(self, x, i, training, st):
         """layers/mb_conv_block.py:127-160 (no skip, no drop-connect)."""
@@ -234,10 +281,11 @@ class RefEfficientDet:
         cin, e = b["cin"], b["cin"] * b["e"]
         if b["e"] != 1:
             n = conv_name()
-            x = Fn.conv2d(x, self.w1x1(f"{pre}/{n}/kernel", e, cin, _cki(1, 1, e)))
-            x = swish(self.bn(x, f"{pre}/{bn_name()}", training, st))
+            x = self._st(Fn.conv2d(x, self.w1x1(f"{pre}/{n}/kernel", e, cin, _cki(1, 1, e))))
+            x = self._t(f"{pre}/expand", swish(self.bn(x, f"{pre}/{bn_name()}", training, st)))
         k = b["k"]
-        x = conv_same(x, self.wdw(f"{pre}/depthwise_conv2d/depthwise_kernel", k, e, _cki(k, k, 1)), b["s"], groups=e)
+        x = self._st(conv_same(x, self.wdw(f"{pre}/depthwise_conv2d/depthwise_kernel", k, e, _cki(k, k, 1)), b["s"],
+                               groups=e))
         x = swish(self.bn(x, f"{pre}/{bn_name()}", training, st))
         # SE (layers/se.py:35-39), width mb_conv_block.py:98-101
         R = max(1, int(cin * b["se"]))
@@ -246,10 +294,10 @@ class RefEfficientDet:
                       self.w(f"{pre}/se/conv2d/bias", (R,), ("const", 0.0)))
         s = Fn.conv2d(swish(s), self.w1x1(f"{pre}/se/conv2d_1/kernel", e, R, _cki(1, 1, e)),
                       self.w(f"{pre}/se/conv2d_1/bias", (e,), ("const", 0.0)))
-        x = torch.sigmoid(s) * x
+        x = self._t(f"{pre}/se_out", self._st(torch.sigmoid(s) * x))
         n = conv_name()
-        x = Fn.conv2d(x, self.w1x1(f"{pre}/{n}/kernel", b["cout"], e, _cki(1, 1, b["cout"])))
-        return self.bn(x, f"{pre}/{bn_name()}", training, st)
+        x = self._st(Fn.conv2d(x, self.w1x1(f"{pre}/{n}/kernel", b["cout"], e, _cki(1, 1, b["cout"]))))
+        return self._t(f"{pre}/project", self.bn(x, f"{pre}/{bn_name()}", training, st))
 
     def resample(self, x, prefix, level_size, training, st):
         """ResampleFeatureMap (resample_feature_map.py:14-52): decisions from the arriving
@@ -257,19 +305,20 @@ class RefEfficientDet:
         F = self.F
         C = x.shape[1]
         if C != F:
-            x = Fn.conv2d(x, self.w1x1(f"{prefix}/conv2d/kernel", F, C, ("glorot", C, F)),
-                          self.w(f"{prefix}/conv2d/bias", (F,), ("const", 0.0)))
-            x = self.bn(x, f"{prefix}/bn", training, st)
+            x = self._st(Fn.conv2d(x, self.w1x1(f"{prefix}/conv2d/kernel", F, C, ("glorot", C, F)),
+                                   self.w(f"{prefix}/conv2d/bias", (F,), ("const", 0.0))))
+            x = self._t(prefix, self.bn(x, f"{prefix}/bn", training, st))
         if x.shape[2] > level_size:
-            x = maxpool_same(x)
+            x = self._t(prefix + "/pool", self._pool(x, stored=prefix.startswith("resample_p")))
         elif x.shape[2] < level_size:
             x = resize_nearest(x, level_size, level_size)
         return x
 
     def sepconv(self, x, pre, dwname, pwname, bname, nout, dw_init, pw_init, b_init):
         C = x.shape[1]
-        x = conv_same(x, self.wdw(f"{pre}/{dwname}", 3, C, dw_init), 1, groups=C)
-        return Fn.conv2d(x, self.w1x1(f"{pre}/{pwname}", nout, C, pw_init), self.w(f"{pre}/{bname}", (nout,), b_init))
+        x = self._st(conv_same(x, self.wdw(f"{pre}/{dwname}", 3, C, dw_init), 1, groups=C))
+        return self._st(Fn.conv2d(x, self.w1x1(f"{pre}/{pwname}", nout, C, pw_init),
+                                  self.w(f"{pre}/{bname}", (nout,), b_init)))
 
     # bifpn.py:108-116: (level, input node ids); ids 0..4 = P3..P7 inputs, 5.. = nodes
     BIFPN_NODES = [(6, [3, 4]), (5, [2, 5]), (4, [1, 6]), (3, [0, 7]), (4, [1, 7, 8]), (5, [2, 6, 9]), (6, [3, 5, 10]),
@@ -290,9 +339,10 @@ class RefEfficientDet:
                 r = self.resample(nodes[src], f"{pre}/resample_{k}", size, training, st) * w[k] / (wsum + 0.0001)
                 acc = r if acc is None else acc + r
             op = f"{pre}/op_after_combine"
-            y = self.sepconv(swish(acc), op, "separable_conv2d/depthwise_kernel", "separable_conv2d/pointwise_kernel",
-                             "separable_conv2d/bias", F, ("glorot", 9 * F, 9), ("glorot", F, F), ("const", 0.0))
-            y = self.bn(y, f"{op}/batch_normalization", training, st)
+            y = self.sepconv(self._t(f"{pre}/fuse", swish(self._st(acc))), op, "separable_conv2d/depthwise_kernel",
+                             "separable_conv2d/pointwise_kernel", "separable_conv2d/bias", F, ("glorot", 9 * F, 9),
+                             ("glorot", F, F), ("const", 0.0))
+            y = self._t(f"{pre}/pw", self.bn(y, f"{op}/batch_normalization", training, st))
             nodes.append(y)
         return nodes[-5:]  # (p3_2, p4_2, p5_2, p6_2, p7_2)
 
@@ -319,7 +369,7 @@ class RefEfficientDet:
                         m = masks[net][i - 1][li] if masks is not None else None
                         if m is not None:
                             image = image * torch.as_tensor(m, dtype=self.dtype)[:, None, None, None]
-                    image = image + orig
+                    image = self._st(image + orig)
             pre = f"{net}/{tag}-predict"
             c = self.sepconv(image, pre, "depthwise_kernel", "pointwise_kernel", "bias", nout, vs(9 * F), vs(F),
                              ("const", bias0))
@@ -348,6 +398,7 @@ class RefEfficientDet:
     def forward(self, x_nhwc, training, masks=None, st: Optional[BNState] = None):
         """EfficientDetNet.call (efficientdet_net.py:76-95): (boxes list, classes list), NHWC
         [B, H, W, A, *]."""
+        self._names = {}
         all_feats = self._backbone(self._input(x_nhwc), training, st)
         feats = all_feats[self.cfg.min_level:self.cfg.max_level + 1]
         for level in range(6, self.cfg.max_level + 1):  # efficientdet_net.py:28-35, 84-85

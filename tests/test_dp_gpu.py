@@ -50,7 +50,7 @@ def _worker(rank, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
                       LOCAL_RANK=str(rank))
     torch.cuda.set_device(0)
-    from tests.test_headline_gpu import perturb
+    from tests.test_headline_gpu import ActCapture, perturb
     from tf2mv_amd import dist as dp
     from tf2mv_amd.anchors import Anchors
     from tf2mv_amd.config import efficientnet_b0_blocks
@@ -74,13 +74,17 @@ def _worker(rank, port, outdir):
     fm = _masks()
     m.fixed_masks = {"class_net": torch.tensor(fm[0][..., sl]).cuda(), "box_net": torch.tensor(fm[1][..., sl]).cuda()}
     data = (xs, t)
+    with ActCapture() as cap:  # this replica's max-pool decisions (oracle routing, see test_headline_gpu)
+        m.call(xs, training=True, masks=m.fixed_masks)
+    routes = cap.pool_routes(m)
+    del cap
     m.train_step(data)  # eager warm-up: allocates the persistent buffers before capture
     torch.cuda.synchronize()
     m.load_state_dict(sd0)  # back to the initial weights, fresh momentum / step counter
     step = dp.graphed_train_step(m, data, ar)
     step()
     torch.cuda.synchronize()
-    out = {"g": m.P.g.cpu(), "w": m.P.w.cpu(), "scal": m.scalars.cpu(), "own_masks": own, "sd0_w": torch.tensor(0)}
+    out = {"g": m.P.g.cpu(), "w": m.P.w.cpu(), "scal": m.scalars.cpu(), "own_masks": own, "routes": routes}
     torch.save(out, os.path.join(outdir, f"r{rank}.pt"))
     if rank == 0:
         torch.save({k: torch.tensor(v) for k, v in sd0.items()}, os.path.join(outdir, "sd0.pt"))
@@ -124,6 +128,7 @@ def test_dp_two_ranks_distinct_shards_graphed_step():
         sl = slice(k * BL, (k + 1) * BL)
         t = anchors.generate_targets_batched(torch.tensor(boxes[sl]), torch.tensor(cls[sl]), torch.tensor(n[sl]))
         yb, yc, ym = ref_targets(_M, t, BL, NC)
+        ref.routes = r[k]["routes"]
         rb, rc = ref.forward(x[sl], True, {"class_net": fm[0][..., sl], "box_net": fm[1][..., sl]})
         lk, _ = ref.detection_loss(rb, rc, yb, yc, ym, with_l2=False, npos_sum=npos, count_scale=WORLD)
         total = lk if total is None else total + lk

@@ -496,7 +496,8 @@ def test_detection_loss(dt, NC, ldc, sizes):
         sl = pyr.seg_slice(s)
         close(cls_g[sl, : A * NC], xs.grad[sl], dt, scale=1e-3)
         close(box_g[sl, : A * 4], bs.grad[sl], dt, scale=1e-1)
-        assert float(cls_g[sl, A * NC:].abs().max()) == 0.0
+        if ldc > A * NC:
+            assert float(cls_g[sl, A * NC:].abs().max()) == 0.0
 
 
 # ----------------------------------------------------------------- optimizer
