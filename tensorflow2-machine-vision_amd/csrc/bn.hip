@@ -41,12 +41,11 @@ static RowGeom row_geom(int C, int passes = 0) {
   r.TPR = NV <= 256 ? NV : 256;
   r.VPT = cdiv(NV, r.TPR);
   r.R = 256 / r.TPR;
-  static const int force = getenv("EDET_ROW_PASSES") ? atoi(getenv("EDET_ROW_PASSES")) : 0;  // A/B only
   if (passes <= 0) {
-    passes = force > 0 ? force : 16384 / (r.R * C);
+    passes = 16384 / (r.R * C);
     // C >= 1024 runs one row per block pass: shorter chunks give more blocks in flight
     // (M = 8192, C = 1152 apply: 38 -> 31 us, scripts/row_probe.py)
-    if (force <= 0 && C >= 1024 && passes > 8) passes = 8;
+    if (C >= 1024 && passes > 8) passes = 8;
   }
   if (passes < 1) passes = 1;
   if (passes > 32) passes = 32;
@@ -734,7 +733,7 @@ int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, i
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 2 * C * sizeof(float2) + 2 * (size_t)g.geo.R * C * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    static const int rcap = getenv("EDET_REDUCE_GRID") ? atoi(getenv("EDET_REDUCE_GRID")) : 512;  // A/B only
+    constexpr int rcap = 512;  // persistent blocks (r01h sweep: 1.51 -> 1.43 ms/step against 1024)
     const int grid = nb < rcap ? nb : rcap;
     const int f = (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0);
     if (nb) launch_reduce<T>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
@@ -760,9 +759,8 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 3 * C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    // resident blocks per launch (0 = one block per chunk); A/B knob EDET_APPLY_GRID
-    static const int gcap = getenv("EDET_APPLY_GRID") ? atoi(getenv("EDET_APPLY_GRID")) : 2048;
-    const int grid = gcap > 0 && nb > gcap ? gcap : nb;
+    constexpr int gcap = 2048;  // resident blocks per launch
+    const int grid = nb > gcap ? gcap : nb;
     const int f = (x->bn.enabled ? AF_BN : 0) | (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0);
     if (nb) launch_apply<T>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
     return check_launch("edet lazy_bwd_apply");

@@ -974,29 +974,17 @@ static int launch_dw3(DwArgs g, hipStream_t s) {
 
 // Kernel forms: TILE = k_dw_fwd / k_dw_wgrad / k_dw_dgrad (8x8 LDS tiles), DW3 = k_dw3
 // (pipelined tiles), DIRECT = k_dw2_fwd / k_dw2_dgrad (one pixel per thread), DW4 =
-// k_dw4_dgrad (register-blocked patches).  EDET_DW_FWD / EDET_DW_WGRAD / EDET_DW_DGRAD
-// (0..3) force one form where it applies, for A/B timing (scripts/dw_probe.py).
+// k_dw4_dgrad (register-blocked patches).  The per-shape choice below was measured with
+// scripts/dw_probe.py.
 enum DwForm { DW_TILE = 0, DW_DW3 = 1, DW_DIRECT = 2, DW_DW4 = 3 };
 
-static int dw_env(const char* name) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : -1;
-}
-
-// block targets of the tile forms (EDET_DW_GRID_FWD / EDET_DW_GRID_WGRAD: A/B only)
-static int dw_env_grid(int which) {
-  static const int f = dw_env("EDET_DW_GRID_FWD"), w = dw_env("EDET_DW_GRID_WGRAD");
-  const int v = which == 0 ? f : w;
-  return v > 0 ? v : (which == 0 ? 2048 : 4096);  // kbench sweep 1024..8192: fwd 2048, wgrad 4096
-}
+// block targets of the tile forms (kbench sweep 1024..8192: fwd 2048, wgrad 4096)
+constexpr int DW_GRID_FWD = 2048, DW_GRID_WGRAD = 4096;
 
 static DwForm dw_form(int which, int K, int S, int C) {
-  static const int force[3] = {dw_env("EDET_DW_FWD"), dw_env("EDET_DW_DGRAD"), dw_env("EDET_DW_WGRAD")};
   const bool direct_ok = C <= 2048;
   const bool dw4_ok = C % 8 == 0;  // channel rows split over blockIdx.y past 256 vectors
-  int f = force[which];
   if (which == 0) {
-    if (f == DW_TILE || f == DW_DW3 || (f == DW_DIRECT && direct_ok)) return (DwForm)f;
     // per-shape winners of scripts/dw_probe.py over the D0 b32 layers: the tile form with its
     // loads all in flight beats the direct form (which re-evaluates the lazy transform per
     // tap) everywhere; the pipelined tiles win where the double-buffered LDS still leaves
@@ -1005,11 +993,9 @@ static DwForm dw_form(int which, int K, int S, int C) {
     return DW_TILE;
   }
   if (which == 1) {
-    if (f == DW_TILE || (f == DW_DIRECT && direct_ok) || (f == DW_DW4 && dw4_ok)) return (DwForm)f;
     if (dw4_ok) return DW_DW4;
     return direct_ok ? DW_DIRECT : DW_TILE;
   }
-  if (f == DW_TILE || f == DW_DW3) return (DwForm)f;
   return (S == 1 && (C <= 64 || (K == 5 && C == 240))) ? DW_DW3 : DW_TILE;
 }
 
@@ -1021,7 +1007,7 @@ static int launch_dw(int which, DwArgs g, hipStream_t s) {
     if (form == DW_DW3) return launch_dw3<T, K, S, false>(g, s);
     if (form == DW_TILE) {
       g.tiles_total = host_tiles(g.pout);
-      const int G = std::max(1, std::min(g.tiles_total, cdiv(dw_env_grid(0), g.ncb)));
+      const int G = std::max(1, std::min(g.tiles_total, cdiv(DW_GRID_FWD, g.ncb)));
       if (g.tiles_total) hipLaunchKernelGGL((k_dw_fwd<T, K, S>), dim3(G * g.ncb), dim3(256), 0, s, g);
       return check_launch("edet dwconv fwd");
     }
@@ -1037,7 +1023,7 @@ static int launch_dw(int which, DwArgs g, hipStream_t s) {
     g.tiles_total = host_tiles(g.pout);
     // ~4096 blocks: these loops are latency-bound (768 blocks measured 1.3-1.9x slower,
     // 4096 is 7 % faster than 2048)
-    int chunks = cdiv(dw_env_grid(2), g.ncb);
+    int chunks = cdiv(DW_GRID_WGRAD, g.ncb);
     if (chunks > g.tiles_total) chunks = g.tiles_total;
     if (chunks < 1) chunks = 1;
     g.tiles_per_wg = cdiv(g.tiles_total, chunks);

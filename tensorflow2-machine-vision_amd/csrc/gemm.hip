@@ -850,6 +850,219 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
   }
 }
 
+// ------------------------------------------------------------------ wave-streaming weight gradient
+// dW[n][k] = sum_m dY[m][n] * A[m][k] (+ db[n] = sum_m dY[m][n]) for a plain bf16 A.
+//
+// The product is a reduction over the very long m axis of two m-major operands.  Each wave
+// owns the whole 16FN x 16FK output tile of its block and streams its own 32-row groups: the
+// group's dY and A rows arrive as 16-byte vectors (one row of the tile = 2(FN+FK) vectors, the
+// wave's 64 lanes cover 32 rows x that), are written to the wave's private LDS image as they
+// are, and read back m-contiguous with gfx950's transposing ds_read_b64_tr_b16 as MFMA
+// fragments: FN x FK v_mfma_f32_16x16x32_bf16 per group, plus FN against an all-ones fragment
+// for the bias gradient.  No block barrier in the row loop; the next WS_PF groups' vectors are
+// in flight while a group is multiplied.  Each element of dY and A is read once per tile
+// (once overall when the tile covers N x K), the 4 waves' partial tiles are folded in LDS in a
+// fixed order and leave the block once, as plain stores into the caller's split-partials
+// workspace (one fixed-order sum pass after) or as fp32 atomics without a workspace.
+struct WgsArgs {
+  const uint16_t* a;
+  const uint16_t* dy;
+  float* dw;
+  float* db;
+  float* part;  // [split][N][K] then [split][N], or null: atomics into dw / db
+  edet_pyramid pyr;
+  int lda, lddy, M, K, N;
+  int ntk, splits, gpb, ngrp;
+};
+
+constexpr int WS_PF = 2;  // groups in flight ahead of the one being multiplied
+
+template <int FN, int FK>
+__global__ __launch_bounds__(256) void k_wgs(WgsArgs g) {
+  constexpr int CW = 2 * (FN + FK);        // 16-byte vectors per tile row
+  constexpr int VPL = FN + FK;             // vectors per lane per 32-row group (32 * CW / 64)
+  constexpr int LDM = 16 * (FN + FK) + 8;  // LDS image row (bf16), padded
+  extern __shared__ __attribute__((aligned(16))) uint16_t wsm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = lid / g.splits, split = lid - tile * g.splits;
+  const int tn = tile / g.ntk, tk = tile - tn * g.ntk;
+  const int n0 = tn * 16 * FN, k0 = tk * 16 * FK;
+  const bool do_db = g.db != nullptr && tk == 0;
+  uint16_t* img = wsm + wave * 32 * LDM;
+  const int gbeg = split * g.gpb, gend = min(g.ngrp, gbeg + g.gpb);
+
+  // this lane's vectors of a group: (row, vector-in-row) pairs are compile-time per slot
+  auto fetch = [&](int grp, uint4* v) {
+    int seg = 0;
+    for (int s = 1; s < g.pyr.nseg; ++s)
+      if (grp * 32 >= g.pyr.row_off[s]) seg = s;
+    const int rend = g.pyr.row_off[seg] + seg_rows(g.pyr, seg);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int e = lane + 64 * i, r = e / CW, c = e - r * CW;
+      const int row = grp * 32 + r;
+      const bool live = grp < gend && row < rend;
+      const uint16_t* p;
+      bool ok;
+      if (c < 2 * FN) {
+        const int col = n0 + 8 * c;
+        ok = live && col < g.lddy;
+        p = g.dy + (size_t)row * g.lddy + col;
+      } else {
+        const int col = k0 + 8 * (c - 2 * FN);
+        ok = live && col < g.K;
+        p = g.a + (size_t)row * g.lda + col;
+      }
+      // select-predicated address: the load is issued unconditionally (a load inside a
+      // divergent branch is waited on inside it)
+      const uint4 t = *reinterpret_cast<const uint4*>(ok ? p : g.dy);
+      v[i] = ok ? t : make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  floatx4 acc[FN][FK], accb[FN];
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    accb[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < FK; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bf16x8_t ones = __builtin_bit_cast(bf16x8_t, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
+
+  uint4 pre[WS_PF][VPL];
+#pragma unroll
+  for (int u = 0; u < WS_PF; ++u) fetch(gbeg + wave + 4 * u, pre[u]);
+  for (int grp = gbeg + wave; grp < gend; grp += 4) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int e = lane + 64 * i, r = e / CW, c = e - r * CW;
+      *reinterpret_cast<uint4*>(img + r * LDM + 8 * c) = pre[0][i];
+    }
+#pragma unroll
+    for (int u = 0; u + 1 < WS_PF; ++u)
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) pre[u][i] = pre[u + 1][i];
+    fetch(grp + 4 * WS_PF, pre[WS_PF - 1]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    bf16x8_t fa[FN], fb[FK];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) fa[i] = tr_frag(img, LDM, 0, 16 * i);
+#pragma unroll
+    for (int j = 0; j < FK; ++j) fb[j] = tr_frag(img, LDM, 0, 16 * (FN + j));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+#pragma unroll
+      for (int j = 0; j < FK; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      if (do_db) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], ones, accb[i], 0, 0, 0);
+    }
+  }
+
+  // fold the 4 waves' tiles in LDS (fixed order: ((w0 + w1) + (w2 + w3))), lane-major slots
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(wsm);  // [2][FN*FK+FN][4][64]
+  constexpr int NV = FN * FK + FN;
+  auto put = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+#pragma unroll
+      for (int j = 0; j < FK; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[((slot * NV + i * FK + j) * 4 + r) * 64 + lane] = acc[i][j][r];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[((slot * NV + FN * FK + i) * 4 + r) * 64 + lane] = accb[i][r];
+    }
+  };
+  auto add = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+#pragma unroll
+      for (int j = 0; j < FK; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += red[((slot * NV + i * FK + j) * 4 + r) * 64 + lane];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) accb[i][r] += red[((slot * NV + FN * FK + i) * 4 + r) * 64 + lane];
+    }
+  };
+  if (wave >= 2) put(wave - 2);
+  __syncthreads();
+  if (wave < 2) add(wave);
+  __syncthreads();
+  if (wave == 1) put(0);
+  __syncthreads();
+  if (wave != 0) return;
+  add(0);
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+#pragma unroll
+    for (int j = 0; j < FK; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + 16 * i + 4 * (lane >> 4) + r, k = k0 + 16 * j + (lane & 15);
+        if (n < g.N && k < g.K) {
+          if (g.part) g.part[((size_t)split * g.N + n) * g.K + k] = acc[i][j][r];
+          else atomicAdd(g.dw + (size_t)n * g.K + k, acc[i][j][r]);
+        }
+      }
+    if (do_db && (lane & 15) == 0)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + 16 * i + 4 * (lane >> 4) + r;
+        if (n < g.N) {
+          if (g.part) g.part[(size_t)g.splits * g.N * g.K + (size_t)split * g.N + n] = accb[i][r];
+          else atomicAdd(g.db + n, accb[i][r]);
+        }
+      }
+  }
+}
+
+struct WgsShape {
+  int fn, fk;
+};
+// instantiated tiles (16FN x 16FK outputs per block)
+constexpr WgsShape WGS_SHAPES[] = {{1, 2}, {2, 2}, {2, 3}, {3, 2}, {6, 1}};
+
+template <int FN, int FK>
+static int launch_wgs(WgsArgs g, int grid, hipStream_t s) {
+  constexpr int LDM = 16 * (FN + FK) + 8;
+  const size_t stage = 4 * 32 * LDM * sizeof(uint16_t);
+  const size_t red = 2 * (FN * FK + FN) * 4 * 64 * sizeof(float);
+  const size_t lds = stage > red ? stage : red;
+  hipLaunchKernelGGL((k_wgs<FN, FK>), dim3(grid), dim3(256), lds, s, g);
+  return check_launch("edet wgrad");
+}
+
+static int dispatch_wgs(WgsArgs g, int fn, int fk, int grid, hipStream_t s) {
+#define EDET_WGS_CASE(A, B) \
+  if (fn == A && fk == B) return launch_wgs<A, B>(g, grid, s);
+  EDET_WGS_CASE(1, 2) EDET_WGS_CASE(2, 2) EDET_WGS_CASE(2, 3) EDET_WGS_CASE(3, 2) EDET_WGS_CASE(6, 1)
+#undef EDET_WGS_CASE
+  set_error("wgrad: no tile %dx%d", fn, fk);
+  return EDET_EUNSUPPORTED;
+}
+
+// the tile that moves the fewest bytes: each tile re-reads dY for every K tile and A for every
+// N tile (N rounded to the tile's 16-column fragments), plus a small charge per fragment for
+// the MFMA and LDS work of zero-padded columns
+static WgsShape pick_wgs(int N, int K) {
+  const int FNt = cdiv(N, 16), FKt = cdiv(K, 16);
+  WgsShape best{0, 0};
+  double bc = 1e300;
+  for (const WgsShape& t : WGS_SHAPES) {
+    const int ntn = cdiv(FNt, t.fn), ntk = cdiv(FKt, t.fk);
+    const double bytes = (double)ntk * 16 * t.fn * ntn + (double)ntn * 16 * t.fk * ntk;
+    const double frags = (double)ntn * ntk * t.fn * t.fk;
+    const double cost = bytes + 6.0 * frags;
+    if (cost < bc) { bc = cost; best = t; }
+  }
+  return best;
+}
+
 // ------------------------------------------------------------------ B-resident GEMM
 // Persistent kernel for the memory-bound 1x1 convs.  Each block loads its column group of the
 // weight B [NG][KP] into LDS ONCE, then streams A through the chip in chunks of R rows x KC
@@ -1398,10 +1611,9 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
 
 template <typename T, bool LAZY, int NF, int KS>
 static int launch_gemm_s(const GemmArgs& g, hipStream_t s) {
-  static const int blk_env = getenv("EDET_GS_BLOCKS") ? atoi(getenv("EDET_GS_BLOCKS")) : 0;  // A/B only
   const int ngroups = (g.M + 15) / 16;
   // 512 blocks (2 per CU): measured best over 512..2048 in the D0 step (scripts/kbench.py)
-  const int grid = std::max(1, std::min(cdiv(ngroups, 4), blk_env > 0 ? blk_env : 512));
+  const int grid = std::max(1, std::min(cdiv(ngroups, 4), 512));
   hipLaunchKernelGGL((k_gemm_s<T, NF, KS, LAZY>), dim3(grid), dim3(256), 0, s, g);
   return check_launch("edet gemm_s");
 }
@@ -1428,8 +1640,7 @@ static int launch_gemm_s_n(const GemmArgs& g, hipStream_t s) {
 template <typename T, bool LAZY>
 static int dispatch_gemm_s(const GemmArgs& g, hipStream_t s, bool& done) {
   done = false;
-  static const int off = getenv("EDET_NO_GEMM_S") ? atoi(getenv("EDET_NO_GEMM_S")) : 0;  // A/B only
-  if (off || sizeof(T) != 2 || g.K % 8 || g.N % 8 || g.accumulate || g.ldc % 8 || g.lda % 8 || g.ldb % 8) return EDET_OK;
+  if (sizeof(T) != 2 || g.K % 8 || g.N % 8 || g.accumulate || g.ldc % 8 || g.lda % 8 || g.ldb % 8) return EDET_OK;
   const bool plain = !LAZY && !g.has_stats;
   if (g.K <= 32 && g.N <= 160 && (g.pyr.nseg == 1 || plain)) {
     done = true;
@@ -1525,9 +1736,6 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
   const int KP = cdiv(g.K, 32) * 32;
   const int LDCf = cdiv(g.N, 8) * 8;
   constexpr size_t BUDGET = 96 * 1024;
-  // EDET_GEMM_FORM=1 forces the K-streaming form (A/B timing, scripts/gemm_probe.py)
-  static const int force = getenv("EDET_GEMM_FORM") ? atoi(getenv("EDET_GEMM_FORM")) : 0;
-  if (force == 1) return dispatch_gemm_kloop<T, LAZY>(g, s);
   // lazy A with K >= 112 into N > 320 (the stage 5-7 expand convs): the A-resident form walks
   // its column chunks one dependent B load at a time with 2 blocks per CU; the pipelined
   // K loop over 128-column tiles measured 1.3-1.4x faster (8192x192x1152, 32768x112x672)
@@ -1602,32 +1810,39 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
   const int tiles = g.ntn * g.ntk;
   hipStream_t s = (hipStream_t)stream;
   const bool plain = lazy_is_plain(a);
+  // narrow outputs over very long M (the stage 0-1 convs: 2M x 16 -> 96, 2M x 32 -> 16): every
+  // wave streams its own rows against the whole N x K tile (k_wgs), each operand read once.
+  // Wider tiles need too many accumulators for the occupancy this stream wants (measured
+  // slower than the 64x64 cooperative tiles below on every other D0 shape, scripts/wg_probe.py)
+  if (dtype == EDET_BF16 && plain && K % 8 == 0 && cdiv(N, 16) * cdiv(K, 16) <= 6 && g.M >= (1 << 18)) {
+    const WgsShape t = pick_wgs(N, K);
+    WgsArgs w{};
+    w.a = (const uint16_t*)a->x; w.dy = (const uint16_t*)dy; w.dw = dwt; w.db = dbias; w.pyr = *rows;
+    w.lda = a->ld; w.lddy = lddy; w.M = g.M; w.K = K; w.N = N;
+    w.ntk = cdiv(cdiv(K, 16), t.fk);
+    const int wtiles = cdiv(cdiv(N, 16), t.fn) * w.ntk;
+    w.ngrp = cdiv(g.M, 32);
+    // 512 blocks of 4 waves, at least 16 row groups per wave; the block's folded tile goes out
+    // as fp32 atomics (N*K per block: 1.5K floats at 96 x 16)
+    int splits = std::max(1, std::min(cdiv(512, wtiles), w.ngrp / 64));
+    w.gpb = cdiv(w.ngrp, splits);
+    w.splits = cdiv(w.ngrp, w.gpb);
+    w.part = nullptr;
+    return dispatch_wgs(w, t.fn, t.fk, wtiles * w.splits, s);
+  }
   if (dtype == EDET_BF16) {
-    // stages never straddle a segment: segments start on 128-row boundaries
-    static const int blk_env = getenv("EDET_WG_BLOCKS") ? atoi(getenv("EDET_WG_BLOCKS")) : 0;  // A/B only
-    static const int stg_env = getenv("EDET_WG_STAGES") ? atoi(getenv("EDET_WG_STAGES")) : 0;  // A/B only
-    // ~2048 blocks of at least 8 stages each (scripts/kbench.py sweep over the D0 step:
-    // 2.37 -> 2.23 ms against 1024 blocks x 4 stages)
-    int split = cdiv(blk_env > 0 ? blk_env : 2048, tiles);
-    const int max_split = std::max(1, cdiv(g.M, WT_BM * (stg_env > 0 ? stg_env : 8)));
+    // lazy A (BN / act / gate applied while staging): 64x64 tiles with transposing LDS reads.
+    // Stages never straddle a segment: segments start on 128-row boundaries.  ~2048 blocks of
+    // at least 8 stages each, fp32 atomics into dW.
+    int split = cdiv(2048, tiles);
+    const int max_split = std::max(1, cdiv(g.M, WT_BM * 8));
     if (split > max_split) split = max_split;
-    // fp32 atomics into dW (distinct addresses, split-way contention) measured faster than
-    // per-split partials + a fixed-order sum pass for every D0 shape (-95 us/step, class head
-    // 152 -> 118 us); EDET_WG_PART=1 restores the partials for N*K >= 16K (A/B)
-    static const int part_env = getenv("EDET_WG_PART") ? atoi(getenv("EDET_WG_PART")) : 0;  // A/B only
-    const bool use_part = part_env == 1 && (long)N * K >= 16384 && workspace_f32(0) != nullptr;
-    if (use_part && split > 128) split = 128;
     g.rows_per = cdiv(cdiv(g.M, split), WT_BM) * WT_BM;
     split = std::max(1, cdiv(g.M, g.rows_per));
-    const size_t nw = (size_t)split * N * K, nb = dbias ? (size_t)split * N : 0;
-    g.part = (use_part && split > 1) ? workspace_f32(nw + nb) : nullptr;
+    g.part = nullptr;
     if (plain) hipLaunchKernelGGL((k_wgrad_tr<false>), dim3(tiles * split), dim3(256), 0, s, g);
     else hipLaunchKernelGGL((k_wgrad_tr<true>), dim3(tiles * split), dim3(256), 0, s, g);
-    int rc = check_launch("edet wgrad");
-    if (rc || !g.part) return rc;
-    rc = sum_partials(g.part, split, (long)N * K, dwt, s);
-    if (!rc && dbias) rc = sum_partials(g.part + nw, split, N, dbias, s);
-    return rc;
+    return check_launch("edet wgrad");
   }
   int split = cdiv(2048, tiles);
   const int max_split = cdiv(g.M, 32 * 4);  // at least 4 row-chunks per block

@@ -18,7 +18,6 @@ from __future__ import annotations
 
 from typing import List, Optional, Sequence, Tuple
 
-import os
 
 import torch
 
@@ -112,8 +111,8 @@ def stem(eng: Engine, P: ParamStore, x: torch.Tensor, wname: str, bn: BNParam) -
 
 # --------------------------------------------------------------------------- 1x1 conv
 # output width from which the weight gradient reads a materialized copy of a lazy A operand
-# (scripts/kbench.py; EDET_WGRAD_MATERIALIZE_N overrides for A/B timing)
-WGRAD_MATERIALIZE_N = int(os.environ.get("EDET_WGRAD_MATERIALIZE_N", "64"))
+# (scripts/kbench.py)
+WGRAD_MATERIALIZE_N = 64
 
 
 def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optional[str] = None,
