@@ -10,11 +10,17 @@ synthetic 512x512 batch of 32 images per GPU (weak scaling).  Inputs and targets
 in HBM before the timed region.  The step is captured once in a HIP graph and replayed.
 
 Prints ONE JSON line on rank 0 with value = images/s over all ranks, plus
-  roofline     : dominant kernel's algorithmic bytes / its average launch duration (HIP
-                 events around each launch of an instrumented eager step) vs 8 TB/s HBM
-  cpu_baseline : BASELINE config 1 (D0 forward, one 512x512 image) through the oracle (fp32
-                 torch-CPU restatement of the reference semantics, not TF) on the host cores,
-                 median of 5 after 2 warm-ups, plus the oracle train step; rank 0 at N=1 only
+  roofline       : the device kernel with the most time in the step (by base name; the
+                   library reports which kernel each call launched): its algorithmic bytes per
+                   launch / its average launch duration, timed by wall-clock probes around its
+                   launches inside the captured step graph, vs 8 TB/s HBM; `traffic` = PMC
+                   HBM bytes per launch from profiles/pmc_traffic.json
+  roofline_table : every kernel above 2 % of the step's kernel time (instrumented eager step,
+                   HIP events per call): calls, ms, avg us, bytes/launch, GB/s, fraction, PMC ratio
+  roofline_step  : all launches' algorithmic bytes / the timed step time
+  cpu_baseline   : BASELINE config 1 (D0 forward, one 512x512 image) through the oracle (fp32
+                   torch-CPU restatement of the reference semantics, not TF) on the host cores,
+                   median of 10 after 2 warm-ups, plus the oracle train step; rank 0 at N=1 only
 """
 import argparse
 import json
@@ -56,12 +62,16 @@ def synthetic_batch(anchors, B, size, seed, device, dtype):
 
 # ---------------------------------------------------------------- per-kernel instrumentation
 def algorithmic_bytes(name, args, es):
-    """Minimum HBM bytes of one launch: every operand read once, every output written once."""
+    """Minimum HBM bytes of one launch: every operand read once, every output written once
+    (activations in the storage dtype, fp32 statistics / parameters / gradients at 4 B)."""
     from tf2mv_amd import _lib as L
 
     def rows(p):
         p = getattr(p, "_obj", p)
         return sum(p.batch * p.H[i] * p.W[i] for i in range(p.nseg))
+
+    def obj(x):
+        return getattr(x, "_obj", x)
 
     if name == "edet_conv1x1_fwd":
         p, K, N = args[2], args[3], args[5]
@@ -90,12 +100,35 @@ def algorithmic_bytes(name, args, es):
     if name == "edet_detection_loss":
         p, A, NC = args[5], args[6], args[7]
         return rows(p) * A * (2 * NC * es + 2 * 4 * es + 4 + 16)
-    if name == "edet_stem_fwd":
+    if name in ("edet_stem_fwd", "edet_stem_wgrad"):
         B, H, W, Co = args[2], args[3], args[4], args[6]
         return B * H * W * 3 * es + B * ((H + 1) // 2) * ((W + 1) // 2) * Co * es
-    if name == "edet_stem_wgrad":
-        B, H, W, Co = args[2], args[3], args[4], args[6]
-        return B * H * W * 3 * es + B * ((H + 1) // 2) * ((W + 1) // 2) * Co * es
+    if name == "edet_se_squeeze":  # (dtype, lz, B, HW, C, svec, s)
+        return args[2] * args[3] * args[4] * es
+    if name in ("edet_gate_bn_reduce", "edet_gate_grad"):  # x and dv
+        return 2 * args[2] * args[3] * args[4] * es
+    if name == "edet_residual_fwd":  # (dtype, lzx, lzres, pyr, C, scale, y, s)
+        return 3 * rows(args[3]) * args[4] * es
+    if name == "edet_maxpool_fwd":  # (dtype, lz, B, H, W, C, y, s)
+        B, H, W, C = args[2], args[3], args[4], args[5]
+        return B * (H * W + ((H + 1) // 2) * ((W + 1) // 2)) * C * es
+    if name == "edet_maxpool_bwd":  # (dtype, lz, B, H, W, C, dy, dx, acc, s)
+        B, H, W, C, acc = args[2], args[3], args[4], args[5], args[8]
+        return B * (H * W * (2 + acc) + ((H + 1) // 2) * ((W + 1) // 2)) * C * es
+    if name in ("edet_bifpn_fuse_fwd", "edet_bifpn_fuse_bwd"):  # (dtype, n, fi, w, B, H, W, C, ...)
+        n, fi, B, H, W, C = args[1], obj(args[2]), args[4], args[5], args[6], args[7]
+        ins = sum(B * fi[i].H * fi[i].W for i in range(n)) * C * es
+        out = B * H * W * C * es
+        if name == "edet_bifpn_fuse_fwd":
+            return ins + out
+        dx = sum(B * fi[i].H * fi[i].W * (1 + fi[i].accumulate) for i in range(n)) * C * es
+        return ins + 2 * out + dx  # inputs (weight gradient), y and dF, dx
+    if name == "edet_opt_norm":
+        return 8 * args[2]
+    if name == "edet_opt_apply":  # w, v, ema read+write, g read, compute copy write
+        return 7 * 4 * args[4] + es * args[4]
+    if name == "edet_count_positives":
+        return args[1]
     return None
 
 
@@ -143,10 +176,13 @@ class KernelTimer:
             if name in ("edet_memset_async", "edet_memcpy_async"):
                 return self.orig(name, *args)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            L.launched_kernels()
             s.record()
             r = self.orig(name, *args)
             e.record()
-            self.rec.append((name, s, e, algorithmic_bytes(name, args, self.es), shape_tag(name, args)))
+            ks = L.launched_kernels()
+            self.rec.append((name, s, e, algorithmic_bytes(name, args, self.es), shape_tag(name, args),
+                             ks[0] if ks else name))
             return r
 
         L.call = timed
@@ -162,7 +198,7 @@ class KernelTimer:
         """Per-call table (slowest first): name, shape, us, achieved GB/s."""
         torch.cuda.synchronize()
         rows = []
-        for name, s, e, b, tag in self.rec:
+        for name, s, e, b, tag, _ in self.rec:
             ms = s.elapsed_time(e)
             rows.append((ms, name, tag, (b / (ms * 1e6)) if (b and ms > 0) else None, b or 0))
         rows.sort(reverse=True)
@@ -171,14 +207,17 @@ class KernelTimer:
                 g = "" if gbs is None else f"{gbs:8.1f} GB/s"
                 f.write(f"{ms * 1e3:9.1f} us  {name:24s} {tag:40s} {g:14s} {b:12d} B\n")
 
-    def summary(self):
+    def summary(self, by="entry"):
+        """Per entry point (by="entry") or per device kernel (by="kernel", the first kernel a
+        call launched): [calls, ms, algorithmic bytes, all bytes known, entry points]."""
         torch.cuda.synchronize()
         agg = {}
-        for name, s, e, b, _ in self.rec:
+        for name, s, e, b, _, kern in self.rec:
             ms = s.elapsed_time(e)
-            a = agg.setdefault(name, [0, 0.0, 0.0, True])
+            a = agg.setdefault(name if by == "entry" else kern, [0, 0.0, 0.0, True, set()])
             a[0] += 1
             a[1] += ms
+            a[4].add(name)
             if b is None:
                 a[3] = False
             else:
@@ -186,24 +225,19 @@ class KernelTimer:
         return agg
 
 
-# C-ABI entry points that launch exactly one device kernel: their probe-measured launch
-# durations are directly comparable with the rocprofv3 summary of that kernel
-ONE_TO_ONE = {"edet_lazy_bwd_apply": "k_lazy_bwd_apply", "edet_lazy_bwd_reduce": "k_lazy_bwd_reduce",
-              "edet_detection_loss": "k_loss", "edet_stem_fwd": "k_stem_fwd", "edet_stem_wgrad": "k_stem_wgrad"}
-
-
 class ProbeTimer:
-    """Wraps every launch of one C-ABI function with edet_probe begin/end on its stream.  The
-    probes are ordinary kernels, so they can be captured into the step's HIP graph (timing
-    events cannot): replaying K captured steps accumulates each launch's duration on the GPU's
-    constant-rate wall clock."""
+    """Wraps every launch of the C-ABI functions ``funcs`` with edet_probe begin/end on its
+    stream.  The probes are ordinary kernels, so they can be captured into the step's HIP graph
+    (timing events cannot): replaying K captured steps accumulates each launch's duration on the
+    GPU's constant-rate wall clock.  Only calls that launched exactly the device kernel
+    ``kernel`` count in the result (an entry point may pick different kernels per shape)."""
 
-    def __init__(self, func, es, max_calls=1024):
+    def __init__(self, funcs, kernel, es, max_calls=1024):
         from tf2mv_amd import _lib as L
-        self.L, self.func, self.es = L, func, es
+        self.L, self.funcs, self.kernel, self.es = L, set(funcs), kernel, es
         self.slots = torch.zeros(max_calls * 3, dtype=torch.int64, device="cuda")
         self.max_calls = max_calls
-        self.bytes = []
+        self.bytes, self.match = [], []
         self.orig = L.call
 
     def __enter__(self):
@@ -211,16 +245,19 @@ class ProbeTimer:
         L = self.L
 
         def probed(name, *args):
-            if name != self.func:
+            if name not in self.funcs:
                 return self.orig(name, *args)
             i = len(self.bytes)
             assert i < self.max_calls
             slot = ctypes.c_void_p(self.slots.data_ptr() + 24 * i)
             st = args[-1]  # every entry point takes its stream last
             self.orig("edet_probe", slot, 0, st)
+            L.launched_kernels()
             r = self.orig(name, *args)
+            ks = L.launched_kernels()
             self.orig("edet_probe", slot, 1, st)
             self.bytes.append(algorithmic_bytes(name, args, self.es))
+            self.match.append(ks == [self.kernel])
             return r
 
         L.call = probed
@@ -239,18 +276,20 @@ class ProbeTimer:
         self.orig("edet_wall_clock_khz", ctypes.byref(khz))
         n = len(self.bytes)
         sl = self.slots.view(-1, 3)[:n].cpu()
-        launches = int(sl[:, 2].sum())
-        ticks = int(sl[:, 1].sum())
+        sel = [i for i in range(n) if self.match[i] and self.bytes[i] is not None]
+        launches = int(sum(int(sl[i, 2]) for i in sel))
+        ticks = int(sum(int(sl[i, 1]) for i in sel))
         avg_us = ticks / max(launches, 1) / (khz.value / 1000.0)
-        bpl = sum(self.bytes) / max(n, 1)
-        return {"launches": launches, "avg_launch_us": avg_us, "bytes_per_launch": bpl,
+        bpl = sum(self.bytes[i] for i in sel) / max(len(sel), 1)
+        return {"launches": launches, "calls_per_step": len(sel), "avg_launch_us": avg_us, "bytes_per_launch": bpl,
                 "achieved_GBps": bpl / avg_us * 1e-3 if avg_us > 0 else None, "clock_khz": khz.value}
 
 
-def probe_roofline(model, data, func, steps, es):
-    """Average launch duration of ``func`` over ``steps`` replays of a captured step graph that
-    carries the probes, and the algorithmic bytes per launch."""
-    pt = ProbeTimer(func, es)
+def probe_roofline(model, data, funcs, kernel, steps, es):
+    """Average launch duration of ``kernel`` (launched from the entry points ``funcs``) over
+    ``steps`` replays of a captured step graph that carries the probes, and its algorithmic
+    bytes per launch."""
+    pt = ProbeTimer(funcs, kernel, es)
     with pt:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -494,6 +533,8 @@ def main():
 
     roofline = None
     kernels = None
+    table = None
+    step_level = None
     if args.kernel_timing and rank == 0:
         es = 2 if args.dtype == "bf16" else 4
         # the instrumented steps below run on rank 0 alone: snapshot the optimizer-visible
@@ -508,6 +549,7 @@ def main():
             model.train_step(data)
         model.eng.overlap = bool(args.overlap)
         agg = kt.summary()
+        kag = kt.summary("kernel")
         if os.environ.get("EDET_KERNEL_DETAIL"):
             kt.detail(os.environ["EDET_KERNEL_DETAIL"])
         total_ms = sum(a[1] for a in agg.values())
@@ -518,24 +560,46 @@ def main():
         for k, a in top[:12]:
             log(f"   {k:28s} calls={a[0]:4d} ms={a[1]:8.3f} share={a[1] / total_ms * 100:5.1f}%"
                 + (f" {a[2] / (a[1] * 1e6):8.1f} GB/s" if a[3] else ""))
-        # dominant single-kernel entry point (1:1 with a device kernel, so the probe average
-        # is comparable with the rocprofv3 summary of the same command)
-        dom = next((kv for kv in top if kv[0] in ONE_TO_ONE and kv[1][3]), None)
+        # per device kernel (base name: a kernel's compile-time cases are one kernel, as rocprof
+        # rows are summed in profiles/): every kernel above 2 % of the step's kernel time
+        ktop = sorted(kag.items(), key=lambda kv: -kv[1][1])
+        table = []
+        for k, a in ktop:
+            if a[1] < 0.02 * total_ms:
+                continue
+            gbs = a[2] / (a[1] * 1e6) if a[3] and a[1] > 0 else None
+            tr = pmc_traffic(k)
+            table.append({"kernel": k, "calls": a[0], "ms": round(a[1], 4), "share": round(a[1] / total_ms, 4),
+                          "avg_us": round(a[1] * 1e3 / a[0], 2),
+                          "bytes_per_launch": round(a[2] / a[0]) if a[3] else None,
+                          "achieved_GBps": None if gbs is None else round(gbs, 1),
+                          "frac": None if gbs is None else round(gbs / HBM_PEAK_GBS, 4),
+                          "pmc_traffic_ratio": (round(tr / (a[2] / a[0]), 3) if (tr and a[3] and a[2]) else None),
+                          "entry_points": sorted(a[4])})
+        known = sum(a[2] for a in kag.values() if a[3])
+        step_level = {"algorithmic_bytes": round(known), "ms_per_step": round(el / args.steps * 1e3, 3),
+                      "achieved_GBps": round(known / (el / args.steps) * 1e-9, 1),
+                      "frac": round(known / (el / args.steps) * 1e-9 / HBM_PEAK_GBS, 4),
+                      "note": "sum of every launch's algorithmic bytes (launches with a formula: "
+                              f"{sum(a[0] for a in kag.values() if a[3])} of {sum(a[0] for a in kag.values())}) "
+                              "over the timed step"}
+        # headline roofline: the kernel with the most time in the step, its launches timed by
+        # wall-clock probes inside the captured step graph
+        dom = next(((k, a) for k, a in ktop if a[3]), None)
         if dom is not None and args.graph:
-            name = dom[0]
-            pr = probe_roofline(model, data, name, args.steps, es)
-            kname = ONE_TO_ONE[name]
+            kname, a = dom
+            pr = probe_roofline(model, data, a[4], kname, args.steps, es)
             ach = pr["achieved_GBps"]
             traffic = pmc_traffic(kname)
-            roofline = {"bound": "hbm", "kernel": kname, "entry_point": name, "achieved": round(ach, 1),
+            roofline = {"bound": "hbm", "kernel": kname, "entry_points": sorted(a[4]), "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                         "traffic": None if traffic is None else round(traffic),
                         "bytes_per_launch": round(pr["bytes_per_launch"]), "avg_launch_us": round(pr["avg_launch_us"], 2),
-                        "launches": pr["launches"], "timing": "wall-clock probes in the captured step graph, "
+                        "launches": pr["launches"], "share_of_kernel_time": round(a[1] / total_ms, 4),
+                        "timing": "wall-clock probes in the captured step graph, "
                         f"{args.steps} replays ({pr['ms_per_step']:.2f} ms/step with probes)"}
             log(f"[bench] roofline {kname}: {pr['launches']} launches, avg {pr['avg_launch_us']:.2f} us, "
                 f"{pr['bytes_per_launch'] / 1e6:.2f} MB/launch -> {ach:.1f} GB/s")
-
         for t, c in saved:
             t.copy_(c)
         P.refresh_compute_copy()
@@ -567,6 +631,8 @@ def main():
             "loss": round(loss, 5),  # global-batch loss of the last timed step
             "gnorm": round(gnorm, 5),
             "roofline": roofline,
+            "roofline_table": table,
+            "roofline_step": step_level,
             "cpu_baseline": cpu,
             "kernels": kernels,
         }

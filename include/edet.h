@@ -136,6 +136,10 @@ int edet_set_workspace(void* ptr, size_t bytes);
  * (now - slot[0]) to slot[1] and 1 to slot[2].  Capturable in HIP graphs. */
 int edet_probe(uint64_t* slot, int end, edet_stream_t stream);
 int edet_wall_clock_khz(int* khz);
+/* measurement: the kernels this thread launched through the library since the previous call,
+ * comma-separated base names (e.g. "k_wgrad_tr,k_sum_partials") into buf; returns the number
+ * of launches (not a status). */
+int edet_launched_kernels(char* buf, size_t size);
 
 /* ---- pointwise (1x1) convolution: y[m][n] = sum_k v(a)[m][k] * wt[n][k] + bias[n] ----
  * wt is [N][K] in `dtype`.  `stats` (nullable) receives per-segment column sums of y. */

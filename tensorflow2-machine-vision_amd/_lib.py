@@ -81,6 +81,7 @@ SIGNATURES = {
     "edet_set_workspace": [P, c_size_t],
     "edet_probe": [P, c_int, P],
     "edet_wall_clock_khz": [P],
+    "edet_launched_kernels": [c_char_p, c_size_t],
     "edet_conv1x1_fwd": [c_int, PLazy, PPyr, c_int, P, c_int, P, P, c_int, c_int, PStat, P],
     "edet_conv1x1_dgrad": [c_int, P, c_int, PPyr, c_int, P, c_int, P, c_int, c_int, P],
     "edet_conv1x1_wgrad": [c_int, PLazy, PPyr, c_int, P, c_int, c_int, P, P, P],
@@ -164,3 +165,10 @@ def lib() -> _Lib:
 
 def call(name: str, *args):
     return lib().call(name, *args)
+
+
+def launched_kernels() -> list:
+    """Base names of the kernels launched since the previous query (measurement)."""
+    buf = ctypes.create_string_buffer(512)
+    lib().fns["edet_launched_kernels"](buf, 512)
+    return [k for k in buf.value.decode().split(",") if k]

@@ -258,7 +258,7 @@ int edet_detect_nms(int dtype, const float* boxes, const void* cls, int ldc, con
   float* key = (float*)scratch;
   int32_t* cid = (int32_t*)(key + (size_t)p->batch * N);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(k_nms<T>, dim3(p->batch), dim3(1024), 0, (hipStream_t)stream, boxes, (const T*)cls, ldc, *p,
+    EDET_LAUNCH(k_nms<T>, dim3(p->batch), dim3(1024), 0, (hipStream_t)stream, boxes, (const T*)cls, ldc, *p,
                        A, NC, N, max_out, iou_thr, score_thr, key, cid, out_boxes, out_cls, out_scores, out_count);
     return check_launch("edet detect_nms");
   });
@@ -269,7 +269,7 @@ int edet_anchor_boxes(int fh, int fw, float start_y, float delta_y, float start_
                       edet_stream_t stream) {
   EDET_REQUIRE(half_yx && out && fh > 0 && fw > 0 && A > 0, "anchor_boxes: bad argument");
   const int n = fh * fw * A;
-  hipLaunchKernelGGL(k_anchor_boxes, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, fh, fw, start_y,
+  EDET_LAUNCH(k_anchor_boxes, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, fh, fw, start_y,
                      delta_y, start_x, delta_x, A, half_yx, out);
   return check_launch("edet anchor_boxes");
 }
@@ -283,7 +283,7 @@ int edet_generate_targets(const float* anchors, const edet_pyramid* p, int A,
   int64_t total = 0;
   for (int s = 0; s < p->nseg; ++s) total += (int64_t)p->batch * p->H[s] * p->W[s] * A;
   if (total == 0) return EDET_OK;
-  hipLaunchKernelGGL(k_targets, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  EDET_LAUNCH(k_targets, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      anchors, *p, A, gt, gt_cls, n_gt, max_gt, iou_thr, box_t, cls_t, mask, total);
   return check_launch("edet generate_targets");
 }
@@ -295,7 +295,7 @@ int edet_decode_boxes(int dtype, const float* anchors, const edet_pyramid* p, in
   for (int s = 0; s < p->nseg; ++s) total += (int64_t)p->batch * p->H[s] * p->W[s] * A;
   if (total == 0) return EDET_OK;
   EDET_DTYPE_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(k_decode<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+    EDET_LAUNCH(k_decode<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        anchors, *p, A, (const T*)rel, ld, out, total);
     return check_launch("edet decode_boxes");
   });

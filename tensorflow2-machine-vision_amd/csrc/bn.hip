@@ -695,14 +695,14 @@ static int lazy_checks(const edet_lazy* x, const edet_pyramid* p, int C) {
 template <typename T, int F = 0>
 static void launch_reduce(int f, dim3 grid, dim3 block, size_t lds, hipStream_t s, const LArgs& g, int nb) {
   if constexpr (F < 16) {
-    if (f == F) hipLaunchKernelGGL((k_lazy_bwd_reduce<T, F>), grid, block, lds, s, g, nb);
+    if (f == F) EDET_LAUNCH((k_lazy_bwd_reduce<T, F>), grid, block, lds, s, g, nb);
     else launch_reduce<T, F + 2>(f, grid, block, lds, s, g, nb);
   }
 }
 template <typename T, int F = 0>
 static void launch_apply(int f, dim3 grid, dim3 block, size_t lds, hipStream_t s, const LArgs& g, int nb) {
   if constexpr (F < 16) {
-    if (f == F) hipLaunchKernelGGL((k_lazy_bwd_apply<T, F>), grid, block, lds, s, g, nb);
+    if (f == F) EDET_LAUNCH((k_lazy_bwd_apply<T, F>), grid, block, lds, s, g, nb);
     else launch_apply<T, F + 1>(f, grid, block, lds, s, g, nb);
   }
 }
@@ -780,10 +780,10 @@ static int img_reduce(int dtype, bool gategrad, const edet_lazy* x, int B, int H
   const int nb = B * g.chunks_per_img;
   const size_t lds = C * sizeof(float2) + (size_t)g.geo.R * C * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (gategrad && x->act) hipLaunchKernelGGL((k_img_reduce<T, true, true>), dim3(nb), row_block(g.geo), lds, s, g);
-    else if (gategrad) hipLaunchKernelGGL((k_img_reduce<T, true, false>), dim3(nb), row_block(g.geo), lds, s, g);
-    else if (x->act) hipLaunchKernelGGL((k_img_reduce<T, false, true>), dim3(nb), row_block(g.geo), lds, s, g);
-    else hipLaunchKernelGGL((k_img_reduce<T, false, false>), dim3(nb), row_block(g.geo), lds, s, g);
+    if (gategrad && x->act) EDET_LAUNCH((k_img_reduce<T, true, true>), dim3(nb), row_block(g.geo), lds, s, g);
+    else if (gategrad) EDET_LAUNCH((k_img_reduce<T, true, false>), dim3(nb), row_block(g.geo), lds, s, g);
+    else if (x->act) EDET_LAUNCH((k_img_reduce<T, false, true>), dim3(nb), row_block(g.geo), lds, s, g);
+    else EDET_LAUNCH((k_img_reduce<T, false, false>), dim3(nb), row_block(g.geo), lds, s, g);
     return check_launch("edet se reduce");
   });
 }
@@ -814,7 +814,7 @@ int edet_gate_bn_reduce(int dtype, const edet_lazy* x, int B, int HW, int C, con
   const int nb = B * g.chunks_per_img;
   const size_t lds = 2 * C * sizeof(float2) + (size_t)g.geo.R * C * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(k_gate_bn_reduce<T>, dim3(nb), row_block(g.geo), lds, (hipStream_t)stream, g);
+    EDET_LAUNCH(k_gate_bn_reduce<T>, dim3(nb), row_block(g.geo), lds, (hipStream_t)stream, g);
     return check_launch("edet gate_bn_reduce");
   });
 }
@@ -822,7 +822,7 @@ int edet_gate_bn_reduce(int dtype, const edet_lazy* x, int B, int HW, int C, con
 int edet_se_bn_combine(int B, int C, const float* gate, const float* dsq, const double* sums5,
                        const edet_bngrad64* acc, edet_stream_t stream) {
   EDET_REQUIRE(gate && dsq && sums5 && acc && acc->dgamma[0] && acc->dbeta[0], "se_bn_combine: null argument");
-  hipLaunchKernelGGL(k_se_bn_combine, dim3(cdiv(C, 8)), dim3(256), 0, (hipStream_t)stream, B, C, gate, dsq, sums5,
+  EDET_LAUNCH(k_se_bn_combine, dim3(cdiv(C, 8)), dim3(256), 0, (hipStream_t)stream, B, C, gate, dsq, sums5,
                      acc->dgamma[0], acc->dbeta[0]);
   return check_launch("edet se_bn_combine");
 }
@@ -832,8 +832,8 @@ int edet_se_fwd(int B, int C, int R, const double* s, const float* w1, const flo
   EDET_REQUIRE(s && w1 && b1 && w2 && b2 && z1 && gate && B > 0 && C > 0 && R > 0,
                "se_fwd: bad argument");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_se_reduce_c, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, s, w1, b1, z1);
-  hipLaunchKernelGGL(k_se_excite, dim3(cdiv(B * C, 256)), dim3(256), 0, st, B, C, R, z1, w2, b2, gate);
+  EDET_LAUNCH(k_se_reduce_c, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, s, w1, b1, z1);
+  EDET_LAUNCH(k_se_excite, dim3(cdiv(B * C, 256)), dim3(256), 0, st, B, C, R, z1, w2, b2, gate);
   return check_launch("edet se_fwd");
 }
 
@@ -844,9 +844,9 @@ int edet_se_bwd(int B, int C, int R, int HW, const double* s, const float* z1,
   EDET_REQUIRE(s && z1 && gate && dgate && w1 && w2 && dw1 && db1 && dw2 && db2 && dsq && dz1,
                "se_bwd: null argument");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_se_dz1, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, z1, gate, dgate, w2, dz1);
+  EDET_LAUNCH(k_se_dz1, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, z1, gate, dgate, w2, dz1);
   const int nA = cdiv(C * R, 8), nB = cdiv(std::max(B * C, std::max(C, R)), 256);
-  hipLaunchKernelGGL(k_se_wgrad, dim3(nA + nB), dim3(256), 0, st, B, C, R, HW, nA, s, z1, gate, dgate, dz1, w1,
+  EDET_LAUNCH(k_se_wgrad, dim3(nA + nB), dim3(256), 0, st, B, C, R, HW, nA, s, z1, gate, dgate, dz1, w1,
                      dw1, db1, dw2, db2, dsq);
   return check_launch("edet se_bwd");
 }
@@ -865,7 +865,7 @@ int edet_residual_fwd(int dtype, const edet_lazy* x, const edet_lazy* res,
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 2 * C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_residual<T>, dim3(nb), row_block(g.geo), lds, (hipStream_t)stream, g);
+    if (nb) EDET_LAUNCH(k_residual<T>, dim3(nb), row_block(g.geo), lds, (hipStream_t)stream, g);
     return check_launch("edet residual");
   });
 }
@@ -882,10 +882,10 @@ int edet_lazy_materialize(int dtype, const edet_lazy* x, const edet_pyramid* p, 
   const size_t lds = C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {
     const hipStream_t st = (hipStream_t)stream;
-    if (nb && x->act && x->gate) hipLaunchKernelGGL((k_materialize<T, true, true>), dim3(nb), row_block(g.geo), lds, st, g);
-    else if (nb && x->act) hipLaunchKernelGGL((k_materialize<T, true, false>), dim3(nb), row_block(g.geo), lds, st, g);
-    else if (nb && x->gate) hipLaunchKernelGGL((k_materialize<T, false, true>), dim3(nb), row_block(g.geo), lds, st, g);
-    else if (nb) hipLaunchKernelGGL((k_materialize<T, false, false>), dim3(nb), row_block(g.geo), lds, st, g);
+    if (nb && x->act && x->gate) EDET_LAUNCH((k_materialize<T, true, true>), dim3(nb), row_block(g.geo), lds, st, g);
+    else if (nb && x->act) EDET_LAUNCH((k_materialize<T, true, false>), dim3(nb), row_block(g.geo), lds, st, g);
+    else if (nb && x->gate) EDET_LAUNCH((k_materialize<T, false, true>), dim3(nb), row_block(g.geo), lds, st, g);
+    else if (nb) EDET_LAUNCH((k_materialize<T, false, false>), dim3(nb), row_block(g.geo), lds, st, g);
     return check_launch("edet lazy_materialize");
   });
 }
@@ -894,7 +894,7 @@ int edet_bn_inference_stats(int64_t n, const float* mmean, const float* mvar, co
                             double* sum, double* sq, edet_stream_t stream) {
   EDET_REQUIRE(mmean && mvar && count && sum && sq, "bn_inference_stats: null argument");
   if (n <= 0) return EDET_OK;
-  hipLaunchKernelGGL(k_bn_infer_stats, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n,
+  EDET_LAUNCH(k_bn_infer_stats, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n,
                      mmean, mvar, count, sum, sq);
   return check_launch("edet bn_inference_stats");
 }
@@ -903,7 +903,7 @@ int edet_bn_update_moving(int64_t n, const double* sum, const double* sq, const 
                           float momentum, float* mmean, float* mvar, edet_stream_t stream) {
   EDET_REQUIRE(sum && sq && count && mmean && mvar, "bn_update_moving: null argument");
   if (n <= 0) return EDET_OK;
-  hipLaunchKernelGGL(k_bn_update, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  EDET_LAUNCH(k_bn_update, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      n, sum, sq, count, momentum, mmean, mvar);
   return check_launch("edet bn_update_moving");
 }

@@ -14,6 +14,13 @@ namespace edet {
 // ------------------------------------------------------------------ error reporting
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// measurement: remember the kernel each launch site starts (edet_launched_kernels)
+void note_kernel(const char* site);
+#define EDET_LAUNCH(K, ...)                 \
+  do {                                      \
+    ::edet::note_kernel(#K);                \
+    hipLaunchKernelGGL(K, __VA_ARGS__);     \
+  } while (0)
 // registered scratch (edet_set_workspace) if it holds n floats, else nullptr
 float* workspace_f32(size_t n_floats);
 // out[i] += sum_s part[s*n + i], fixed order

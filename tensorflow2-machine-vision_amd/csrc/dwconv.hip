@@ -956,7 +956,7 @@ static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s) {
     patches += (long)g.pin.batch * cdiv(g.pin.H[i] + pt, 2) * cdiv(g.pin.W[i] + pl, 2);
   }
   const int grid = (int)std::max<long>(1, std::min<long>(4096, (patches + geo.R - 1) / geo.R));
-  if (patches) hipLaunchKernelGGL((k_dw4_dgrad<T, K, S, CPT, 2, 2>), dim3(grid, ncs), dim3(geo.TPR * geo.R), 0, s, g, geo);
+  if (patches) EDET_LAUNCH((k_dw4_dgrad<T, K, S, CPT, 2, 2>), dim3(grid, ncs), dim3(geo.TPR * geo.R), 0, s, g, geo);
   return check_launch("edet dwconv dgrad");
 }
 
@@ -968,7 +968,7 @@ static int launch_dw3(DwArgs g, hipStream_t s) {
   g.tiles_total = host_tiles(g.pout);
   if (!g.tiles_total) return EDET_OK;
   const int G = std::max(1, std::min(g.tiles_total, cdiv(256 * per_cu, g.ncb)));
-  hipLaunchKernelGGL((k_dw3<T, K, S, WG>), dim3(G * g.ncb), dim3(256), 0, s, g);
+  EDET_LAUNCH((k_dw3<T, K, S, WG>), dim3(G * g.ncb), dim3(256), 0, s, g);
   return check_launch("edet dwconv3");
 }
 
@@ -1008,14 +1008,14 @@ static int launch_dw(int which, DwArgs g, hipStream_t s) {
     if (form == DW_TILE) {
       g.tiles_total = host_tiles(g.pout);
       const int G = std::max(1, std::min(g.tiles_total, cdiv(DW_GRID_FWD, g.ncb)));
-      if (g.tiles_total) hipLaunchKernelGGL((k_dw_fwd<T, K, S>), dim3(G * g.ncb), dim3(256), 0, s, g);
+      if (g.tiles_total) EDET_LAUNCH((k_dw_fwd<T, K, S>), dim3(G * g.ncb), dim3(256), 0, s, g);
       return check_launch("edet dwconv fwd");
     }
   } else if (which == 1) {
     if (form == DW_DW4) return launch_dw4_dgrad<T, K, S>(g, s);
     if (form == DW_TILE) {
       g.tiles_total = host_tiles(g.pin);
-      if (g.tiles_total) hipLaunchKernelGGL((k_dw_dgrad<T, K, S>), dim3(g.tiles_total * g.ncb), dim3(256), 0, s, g);
+      if (g.tiles_total) EDET_LAUNCH((k_dw_dgrad<T, K, S>), dim3(g.tiles_total * g.ncb), dim3(256), 0, s, g);
       return check_launch("edet dwconv dgrad");
     }
   } else {
@@ -1029,7 +1029,7 @@ static int launch_dw(int which, DwArgs g, hipStream_t s) {
     g.tiles_per_wg = cdiv(g.tiles_total, chunks);
     chunks = cdiv(g.tiles_total, g.tiles_per_wg);
     g.part = nullptr;  // K*K*C is small: atomics measured faster than a 2048-way partial sum
-    if (g.tiles_total) hipLaunchKernelGGL((k_dw_wgrad<T, K, S>), dim3(chunks * g.ncb), dim3(256), 0, s, g);
+    if (g.tiles_total) EDET_LAUNCH((k_dw_wgrad<T, K, S>), dim3(chunks * g.ncb), dim3(256), 0, s, g);
     return check_launch("edet dwconv wgrad");
   }
   // DW_DIRECT (fwd / dgrad)
@@ -1040,9 +1040,9 @@ static int launch_dw(int which, DwArgs g, hipStream_t s) {
   const int grid = (int)std::max<long>(1, std::min<long>(4096, (px + geo.R - 1) / geo.R));
   if (which == 0) {
     const size_t lds = g.has_stats ? 2 * (size_t)geo.R * g.C * sizeof(float) : 0;
-    if (px) hipLaunchKernelGGL((k_dw2_fwd<T, K, S>), dim3(grid), dim3(geo.TPR * geo.R), lds, s, g, geo);
+    if (px) EDET_LAUNCH((k_dw2_fwd<T, K, S>), dim3(grid), dim3(geo.TPR * geo.R), lds, s, g, geo);
   } else {
-    if (px) hipLaunchKernelGGL((k_dw2_dgrad<T, K, S>), dim3(grid), dim3(geo.TPR * geo.R), 0, s, g, geo);
+    if (px) EDET_LAUNCH((k_dw2_dgrad<T, K, S>), dim3(grid), dim3(geo.TPR * geo.R), 0, s, g, geo);
   }
   return check_launch("edet dwconv");
 }

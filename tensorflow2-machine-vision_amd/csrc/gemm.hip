@@ -1033,7 +1033,7 @@ static int launch_wgs(WgsArgs g, int grid, hipStream_t s) {
   const size_t stage = 4 * 32 * LDM * sizeof(uint16_t);
   const size_t red = 2 * (FN * FK + FN) * 4 * 64 * sizeof(float);
   const size_t lds = stage > red ? stage : red;
-  hipLaunchKernelGGL((k_wgs<FN, FK>), dim3(grid), dim3(256), lds, s, g);
+  EDET_LAUNCH((k_wgs<FN, FK>), dim3(grid), dim3(256), lds, s, g);
   return check_launch("edet wgrad");
 }
 
@@ -1420,7 +1420,7 @@ static int launch_pwb(const GemmArgs& g, const PwPlan& p, hipStream_t s) {
   const long want = (long)256 * per_cu;
   long rows = std::min<long>(p.nrg, std::max<long>(1, want / p.ngroups));
   const int grid = (int)(rows * p.ngroups);
-  hipLaunchKernelGGL((k_pwb<T, FN, KS, LAZY>), dim3(grid), dim3(256), lds, s, g, p);
+  EDET_LAUNCH((k_pwb<T, FN, KS, LAZY>), dim3(grid), dim3(256), lds, s, g, p);
   return check_launch("edet pwb");
 }
 
@@ -1614,7 +1614,7 @@ static int launch_gemm_s(const GemmArgs& g, hipStream_t s) {
   const int ngroups = (g.M + 15) / 16;
   // 512 blocks (2 per CU): measured best over 512..2048 in the D0 step (scripts/kbench.py)
   const int grid = std::max(1, std::min(cdiv(ngroups, 4), 512));
-  hipLaunchKernelGGL((k_gemm_s<T, NF, KS, LAZY>), dim3(grid), dim3(256), 0, s, g);
+  EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY>), dim3(grid), dim3(256), 0, s, g);
   return check_launch("edet gemm_s");
 }
 
@@ -1661,7 +1661,7 @@ static int launch_gemm(GemmArgs g, hipStream_t s) {
   const int nwg = g.ntm * g.ntn;
   if (nwg == 0) return EDET_OK;
   const size_t dyn = LAZY ? (size_t)g.K * (sizeof(float2) + 2 * sizeof(float)) : 0;
-  hipLaunchKernelGGL((k_gemm<T, BM, BN, KC, LAZY>), dim3(nwg), dim3(256), dyn, s, g);
+  EDET_LAUNCH((k_gemm<T, BM, BN, KC, LAZY>), dim3(nwg), dim3(256), dyn, s, g);
   return check_launch("edet gemm");
 }
 
@@ -1690,7 +1690,7 @@ static int launch_gemm_r(GemmArgs g, hipStream_t s) {
   // resident blocks per CU from the LDS image; the row-tile workers per split fill that once
   const int per_cu = max(1, min(8, (int)((160 * 1024) / lds)));
   const int G = min(ntm, max(1, cdiv(256 * per_cu, nsplit)));
-  hipLaunchKernelGGL((k_gemm_r<T, BM, LAZY>), dim3(G * nsplit), dim3(256), lds, s, g, KP, nsplit, cps, LDC);
+  EDET_LAUNCH((k_gemm_r<T, BM, LAZY>), dim3(G * nsplit), dim3(256), lds, s, g, KP, nsplit, cps, LDC);
   return check_launch("edet gemm_r");
 }
 
@@ -1840,8 +1840,8 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
     g.rows_per = cdiv(cdiv(g.M, split), WT_BM) * WT_BM;
     split = std::max(1, cdiv(g.M, g.rows_per));
     g.part = nullptr;
-    if (plain) hipLaunchKernelGGL((k_wgrad_tr<false>), dim3(tiles * split), dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((k_wgrad_tr<true>), dim3(tiles * split), dim3(256), 0, s, g);
+    if (plain) EDET_LAUNCH((k_wgrad_tr<false>), dim3(tiles * split), dim3(256), 0, s, g);
+    else EDET_LAUNCH((k_wgrad_tr<true>), dim3(tiles * split), dim3(256), 0, s, g);
     return check_launch("edet wgrad");
   }
   int split = cdiv(2048, tiles);
@@ -1852,8 +1852,8 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
   split = cdiv(g.M, g.rows_per);
   if (split < 1) split = 1;
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (plain) hipLaunchKernelGGL((k_wgrad<T, false>), dim3(tiles * split), dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((k_wgrad<T, true>), dim3(tiles * split), dim3(256), 0, s, g);
+    if (plain) EDET_LAUNCH((k_wgrad<T, false>), dim3(tiles * split), dim3(256), 0, s, g);
+    else EDET_LAUNCH((k_wgrad<T, true>), dim3(tiles * split), dim3(256), 0, s, g);
     return check_launch("edet wgrad");
   });
 }

@@ -258,7 +258,7 @@ int edet_detection_loss(int dtype, const void* cls, int ldc, const void* box, in
   g.nb_cls = total_chunks(*p, LCLS_ROWS);
   const int nb = g.nb_cls + total_chunks(*p, LBOX_ROWS);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_loss<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, g);
+    if (nb) EDET_LAUNCH(k_loss<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, g);
     return check_launch("edet detection_loss");
   });
 }
@@ -270,7 +270,7 @@ int edet_count_positives(const uint8_t* mask, int64_t n, float* out, edet_stream
   int nb = (int)((n / 16 + 255) / 256);
   if (nb > 64) nb = 64;
   if (nb < 1) nb = 1;
-  hipLaunchKernelGGL(k_count_pos, dim3(nb), dim3(256), 0, (hipStream_t)stream, mask, n, out);
+  EDET_LAUNCH(k_count_pos, dim3(nb), dim3(256), 0, (hipStream_t)stream, mask, n, out);
   return check_launch("edet count_positives");
 }
 
@@ -278,7 +278,7 @@ int edet_onehot_to_index(const float* onehot, int64_t n, int NC, int32_t* out,
                          edet_stream_t stream) {
   EDET_REQUIRE(onehot && out && NC > 0, "onehot_to_index: bad argument");
   if (n <= 0) return EDET_OK;
-  hipLaunchKernelGGL(k_onehot_index, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  EDET_LAUNCH(k_onehot_index, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      onehot, n, NC, out);
   return check_launch("edet onehot_to_index");
 }

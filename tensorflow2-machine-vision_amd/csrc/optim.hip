@@ -164,7 +164,7 @@ int edet_opt_norm(const float* w, const float* g, int64_t n, int64_t n_l2,
                   const edet_sched* sched, float* scalars, double* partials, int32_t* step,
                   edet_stream_t stream) {
   EDET_REQUIRE(w && g && sched && scalars && partials && step && n_l2 <= n, "opt_norm: bad argument");
-  hipLaunchKernelGGL(k_opt_norm, dim3(EDET_OPT_NORM_BLOCKS), dim3(256), 0, (hipStream_t)stream, w, g, n, n_l2,
+  EDET_LAUNCH(k_opt_norm, dim3(EDET_OPT_NORM_BLOCKS), dim3(256), 0, (hipStream_t)stream, w, g, n, n_l2,
                      *sched, scalars, partials, step);
   return check_launch("edet opt_norm");
 }
@@ -174,7 +174,7 @@ int edet_opt_apply(float* w, const float* g, float* v, float* ema, int64_t n, in
                    edet_stream_t stream) {
   EDET_REQUIRE(w && g && v && sched && scalars && partials && n_l2 <= n, "opt_apply: bad argument");
   EDET_DTYPE_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(k_opt_apply<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, w, g, v, ema, n,
+    EDET_LAUNCH(k_opt_apply<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, w, g, v, ema, n,
                        n_l2, *sched, scalars, partials, (T*)wcompute);
     return check_launch("edet opt_apply");
   });
@@ -184,7 +184,7 @@ int edet_cast_f32(int dtype, const float* src, void* dst, int64_t n, edet_stream
   EDET_REQUIRE(src && dst, "cast_f32: null argument");
   if (n <= 0) return EDET_OK;
   EDET_DTYPE_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(k_cast<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, src, (T*)dst, n);
+    EDET_LAUNCH(k_cast<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, src, (T*)dst, n);
     return check_launch("edet cast");
   });
 }
@@ -194,7 +194,7 @@ int edet_transpose_cast(int dtype, const float* src, void* dst, const int64_t* t
   EDET_REQUIRE(src && dst && table && n_entries >= 0 && max_tiles >= 0, "transpose_cast: bad argument");
   if (n_entries == 0 || max_tiles == 0) return EDET_OK;
   EDET_DTYPE_DISPATCH(dtype, T, {
-    hipLaunchKernelGGL(k_transpose_cast<T>, dim3(max_tiles, n_entries), dim3(256), 0, (hipStream_t)stream, src,
+    EDET_LAUNCH(k_transpose_cast<T>, dim3(max_tiles, n_entries), dim3(256), 0, (hipStream_t)stream, src,
                        (T*)dst, table);
     return check_launch("edet transpose_cast");
   });
@@ -204,7 +204,7 @@ int edet_dropmask(float* out, int n, float survival, uint64_t seed, const int32_
                   edet_stream_t stream) {
   EDET_REQUIRE(out && step && survival > 0.f, "dropmask: bad argument");
   if (n <= 0) return EDET_OK;
-  hipLaunchKernelGGL(k_dropmask, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, n, survival, seed,
+  EDET_LAUNCH(k_dropmask, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, n, survival, seed,
                      step);
   return check_launch("edet dropmask");
 }

@@ -710,15 +710,15 @@ int edet_stem_fwd(int dtype, const void* x, int B, int H, int W, const void* w, 
     uint16_t* yb = (uint16_t*)y;
     hipStream_t st = (hipStream_t)stream;
     switch (Cout / 16) {
-      case 1: hipLaunchKernelGGL(k_stem2_fwd<1>, dim3(grid), dim3(256), lds, st, xb, B, H, W, wb, Cout, yb, sum, sq, R); break;
-      case 2: hipLaunchKernelGGL(k_stem2_fwd<2>, dim3(grid), dim3(256), lds, st, xb, B, H, W, wb, Cout, yb, sum, sq, R); break;
-      case 3: hipLaunchKernelGGL(k_stem2_fwd<3>, dim3(grid), dim3(256), lds, st, xb, B, H, W, wb, Cout, yb, sum, sq, R); break;
-      default: hipLaunchKernelGGL(k_stem2_fwd<4>, dim3(grid), dim3(256), lds, st, xb, B, H, W, wb, Cout, yb, sum, sq, R); break;
+      case 1: EDET_LAUNCH(k_stem2_fwd<1>, dim3(grid), dim3(256), lds, st, xb, B, H, W, wb, Cout, yb, sum, sq, R); break;
+      case 2: EDET_LAUNCH(k_stem2_fwd<2>, dim3(grid), dim3(256), lds, st, xb, B, H, W, wb, Cout, yb, sum, sq, R); break;
+      case 3: EDET_LAUNCH(k_stem2_fwd<3>, dim3(grid), dim3(256), lds, st, xb, B, H, W, wb, Cout, yb, sum, sq, R); break;
+      default: EDET_LAUNCH(k_stem2_fwd<4>, dim3(grid), dim3(256), lds, st, xb, B, H, W, wb, Cout, yb, sum, sq, R); break;
     }
     return check_launch("edet stem2_fwd");
   }
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_stem_fwd<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const T*)x, B, H, W,
+    if (nb) EDET_LAUNCH(k_stem_fwd<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const T*)x, B, H, W,
                                (const T*)w, Cout, (T*)y, sum, sq);
     return check_launch("edet stem_fwd");
   });
@@ -741,10 +741,10 @@ int edet_stem_wgrad(int dtype, const void* x, int B, int H, int W, const void* d
       const uint16_t* db = (const uint16_t*)dy;
       hipStream_t st = (hipStream_t)stream;
       switch (Cout / 16) {
-        case 1: hipLaunchKernelGGL(k_stem2_wgrad<1>, dim3(grid), dim3(256), lds, st, xb, B, H, W, db, Cout, part, R); break;
-        case 2: hipLaunchKernelGGL(k_stem2_wgrad<2>, dim3(grid), dim3(256), lds, st, xb, B, H, W, db, Cout, part, R); break;
-        case 3: hipLaunchKernelGGL(k_stem2_wgrad<3>, dim3(grid), dim3(256), lds, st, xb, B, H, W, db, Cout, part, R); break;
-        default: hipLaunchKernelGGL(k_stem2_wgrad<4>, dim3(grid), dim3(256), lds, st, xb, B, H, W, db, Cout, part, R); break;
+        case 1: EDET_LAUNCH(k_stem2_wgrad<1>, dim3(grid), dim3(256), lds, st, xb, B, H, W, db, Cout, part, R); break;
+        case 2: EDET_LAUNCH(k_stem2_wgrad<2>, dim3(grid), dim3(256), lds, st, xb, B, H, W, db, Cout, part, R); break;
+        case 3: EDET_LAUNCH(k_stem2_wgrad<3>, dim3(grid), dim3(256), lds, st, xb, B, H, W, db, Cout, part, R); break;
+        default: EDET_LAUNCH(k_stem2_wgrad<4>, dim3(grid), dim3(256), lds, st, xb, B, H, W, db, Cout, part, R); break;
       }
       int rc = check_launch("edet stem2_wgrad");
       if (rc) return rc;
@@ -757,7 +757,7 @@ int edet_stem_wgrad(int dtype, const void* x, int B, int H, int W, const void* d
   const int nb = (int)((px + per - 1) / per);
   float* part = nullptr;  // 27*Cout weights over 2048 blocks: atomics measured faster
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_stem_wgrad<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const T*)x, B, H, W,
+    if (nb) EDET_LAUNCH(k_stem_wgrad<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const T*)x, B, H, W,
                                (const T*)dy, Cout, dw, per, part);
     int rc = check_launch("edet stem_wgrad");
     if (rc || !part || !nb) return rc;
@@ -772,7 +772,7 @@ int edet_maxpool_fwd(int dtype, const edet_lazy* x, int B, int H, int W, int C, 
   const long n = (long)B * cdiv(H, 2) * cdiv(W, 2) * (C / 8);
   const int nb = (int)((n + 255) / 256);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_maxpool_fwd<T>, dim3(nb), dim3(256), C * sizeof(float2), (hipStream_t)stream, *x, B, H, W, C, (T*)y);
+    if (nb) EDET_LAUNCH(k_maxpool_fwd<T>, dim3(nb), dim3(256), C * sizeof(float2), (hipStream_t)stream, *x, B, H, W, C, (T*)y);
     return check_launch("edet maxpool_fwd");
   });
 }
@@ -784,7 +784,7 @@ int edet_maxpool_bwd(int dtype, const edet_lazy* x, int B, int H, int W, int C,
   const long n = (long)B * H * W * (C / 8);
   const int nb = (int)((n + 255) / 256);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_maxpool_bwd<T>, dim3(nb), dim3(256), C * sizeof(float2), (hipStream_t)stream, *x, B, H, W, C,
+    if (nb) EDET_LAUNCH(k_maxpool_bwd<T>, dim3(nb), dim3(256), C * sizeof(float2), (hipStream_t)stream, *x, B, H, W, C,
                                (const T*)dy, (T*)dx, accumulate);
     return check_launch("edet maxpool_bwd");
   });
@@ -819,7 +819,7 @@ int edet_bifpn_fuse_fwd(int dtype, int n_in, const edet_fuse_input* ins, const f
   const long n = (long)B * H * W * (C / 8);
   const int nb = (int)((n + 255) / 256);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_fuse_fwd<T>, dim3(nb), dim3(256), n_in * C * sizeof(float2), (hipStream_t)stream, g);
+    if (nb) EDET_LAUNCH(k_fuse_fwd<T>, dim3(nb), dim3(256), n_in * C * sizeof(float2), (hipStream_t)stream, g);
     return check_launch("edet bifpn_fuse_fwd");
   });
 }
@@ -840,7 +840,7 @@ int edet_bifpn_fuse_bwd(int dtype, int n_in, const edet_fuse_input* ins, const f
     nb += g.nb_in[i];
   }
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) hipLaunchKernelGGL(k_fuse_bwd<T>, dim3(nb), dim3(256), n_in * C * sizeof(float2), (hipStream_t)stream, g);
+    if (nb) EDET_LAUNCH(k_fuse_bwd<T>, dim3(nb), dim3(256), n_in * C * sizeof(float2), (hipStream_t)stream, g);
     return check_launch("edet bifpn_fuse_bwd");
   });
 }

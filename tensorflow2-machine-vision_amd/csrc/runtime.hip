@@ -7,6 +7,14 @@ namespace edet {
 
 static thread_local char g_err[512] = "";
 
+// kernels launched by this thread since the last edet_launched_kernels() (base names)
+static thread_local const char* g_launched[8];
+static thread_local int g_nlaunched = 0;
+void note_kernel(const char* site) {
+  if (g_nlaunched < 8) g_launched[g_nlaunched] = site;
+  ++g_nlaunched;
+}
+
 void set_error(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
@@ -47,7 +55,7 @@ __global__ __launch_bounds__(256) void k_sum_partials(const float* part, int S, 
 
 int sum_partials(const float* part, int S, long n, float* out, hipStream_t st) {
   if (n <= 0) return EDET_OK;
-  hipLaunchKernelGGL(k_sum_partials, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, S, n, out);
+  EDET_LAUNCH(k_sum_partials, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, S, n, out);
   return check_launch("edet sum_partials");
 }
 
@@ -71,6 +79,22 @@ extern "C" {
 const char* edet_last_error(void) { return edet::g_err; }
 
 int edet_abi_version(void) { return 4; }  // 3: edet_fuse_input.pool_arg; 4: opt norm partials
+
+int edet_launched_kernels(char* buf, size_t size) {
+  EDET_REQUIRE(buf && size > 0, "launched_kernels: null buffer");
+  size_t o = 0;
+  const int n = edet::g_nlaunched < 8 ? edet::g_nlaunched : 8;
+  for (int i = 0; i < n; ++i) {
+    const char* p = edet::g_launched[i];
+    while (*p == '(' || *p == ' ') ++p;  // launch sites spell templates as (k_x<T, F>)
+    if (i && o + 1 < size) buf[o++] = ',';
+    for (; *p && *p != '<' && *p != ')' && o + 1 < size; ++p) buf[o++] = *p;
+  }
+  buf[o] = 0;
+  const int total = edet::g_nlaunched;
+  edet::g_nlaunched = 0;
+  return total;
+}
 
 int edet_set_workspace(void* ptr, size_t bytes) {
   edet::g_ws = ptr;
