@@ -1,6 +1,9 @@
 set -u
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -m pytest -q -x tests/test_kernels_gpu.py -k "dwconv" > gpurun_out/dw_test.txt 2>&1 || { tail -30 gpurun_out/dw_test.txt; exit 1; }
-for sh in "32 32 32 672 5 1" "32 128 128 144 3 1" "32 64 64 240 5 1" "32 16 16 1152 5 1" "32 128 128 144 5 2" "32 256 256 32 3 1" "32 256 256 96 3 2"; do
-  timeout -k 10 60 python scripts/dw_probe.py $sh >> gpurun_out/dw_probe.txt 2>&1 || exit 1
+P=$PWD/tensorflow2-machine-vision_amd
+EDET_LIB=$P/lib_d3/libedet.so timeout -k 10 300 python -m pytest -q -x tests/test_kernels_gpu.py tests/test_kernels_large_gpu.py -k "dw" > gpurun_out/dw_test.txt 2>&1 || { tail -30 gpurun_out/dw_test.txt; exit 1; }
+: > gpurun_out/dw_sweep.txt
+for v in lib lib_d1 lib_d2 lib_d3 lib_d3t1k lib_d1t1k; do
+  echo "== $v" >> gpurun_out/dw_sweep.txt
+  EDET_LIB=$P/$v/libedet.so timeout -k 10 120 python scripts/dw_sweep.py fwd >> gpurun_out/dw_sweep.txt 2>&1 || exit 1
 done

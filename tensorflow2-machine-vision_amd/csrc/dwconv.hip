@@ -938,12 +938,9 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo) {
 
 template <typename T, int K, int S>
 static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s) {
-#ifndef EDET_DW4_K5_CPT
-#define EDET_DW4_K5_CPT 4
-#endif
   // k5: 4 channels per thread (25 fp32 weights each in registers); 2 channels measured
-  // faster only at C = 1152 (EDET_DW4_K5_CPT, A/B)
-  constexpr int CPT = K == 3 ? 8 : EDET_DW4_K5_CPT;
+  // faster only at C = 1152
+  constexpr int CPT = K == 3 ? 8 : 4;
   DwGeom geo;
   // channel vectors per pixel row split over blockIdx.y until a row fits a block
   int ncs = 1;
@@ -972,11 +969,250 @@ static int launch_dw3(DwArgs g, hipStream_t s) {
   return check_launch("edet dwconv3");
 }
 
+// ------------------------------------------------------------------ row-streaming forward
+// One workgroup = one image x 32 channels x a strip of TW = 8*CPG output columns x up to TH
+// output rows.  It walks down its rows keeping the last K+S transformed input rows of the
+// strip in an LDS ring, so every input element of the strip is loaded and transformed once
+// (halo: (TW-1)*S+K columns per TW*S, K-S rows per block) against 2.25x in the 8x8 tiles for
+// k5; the S input rows of step i+1 are fetched into registers during step i-1, transformed
+// into the ring during step i, and each output row leaves through a double-buffered LDS stage
+// as 16-byte stores.  One barrier per output row.
+// steps of input rows in flight ahead of their commit, and the block count the rows per block
+// are chosen for (scripts/dw_sweep.py over the D0 b32 shapes: 1 step and 1024 blocks were
+// best or within 3 % of best everywhere; 2-4 steps gain nothing, 3072 blocks lose 10-20 %)
+constexpr int DWS_PREFETCH = 1, DWS_BLOCKS = 1024;
+struct DwsPlan {
+  int TH;                      // output rows per block
+  int strips[EDET_MAX_SEG];    // column strips per segment
+  int rowblk[EDET_MAX_SEG];    // row blocks per segment
+  int nblk[EDET_MAX_SEG];      // blocks per segment (ncb * batch * rowblk * strips)
+};
+
+template <int N, int WORDS>
+struct DwRaw {  // raw input vectors of a fetch, in registers until their commit
+  static constexpr int NV = N;
+  uint4 v[N][WORDS];
+  uint32_t ok;
+};
+
+template <typename T, int K, int S, int CPG, int D = DWS_PREFETCH>
+__global__ __launch_bounds__(256) void k_dws_fwd(DwArgs g, DwsPlan pl) {
+  constexpr int TW = 8 * CPG, IWS = (TW - 1) * S + K, R = K + S;
+  constexpr int RV = IWS * (DCB / 8);             // 8-channel vectors per input row
+  constexpr int NVS = (S * RV + 255) / 256;       // per thread, S rows (one step)
+  constexpr int NVP = (K * RV + 255) / 256;       // per thread, K rows (block prologue)
+  constexpr int WORDS = sizeof(T) == 2 ? 1 : 2;
+  constexpr int WIN = (CPG - 1) * S + K;
+  __shared__ __attribute__((aligned(16))) float ring[R * IWS * DCB];
+  __shared__ __attribute__((aligned(16))) T ost[2][TW * DCB];
+  __shared__ float2 xf[DCB];
+  __shared__ float gt[DCB];
+  const int tid = threadIdx.x, c = tid & 31, gc = tid >> 5;
+
+  // ---- block -> (seg, cb, n, row block, strip); consecutive logical ids share an XCD
+  int id = xcd_remap(blockIdx.x, gridDim.x), seg = 0;
+  while (seg < g.pout.nseg - 1 && id >= pl.nblk[seg]) id -= pl.nblk[seg++];
+  const int strip = id % pl.strips[seg];
+  id /= pl.strips[seg];
+  const int rb = id % pl.rowblk[seg];
+  id /= pl.rowblk[seg];
+  const int n = id % g.pout.batch, cb = id / g.pout.batch;
+  const int c0 = cb * DCB, C = g.C;
+  const int OH = g.pout.H[seg], OW = g.pout.W[seg], H = g.pin.H[seg], W = g.pin.W[seg];
+  const int oy0 = rb * pl.TH, ox0 = strip * TW;
+  const int nsteps = min(pl.TH, OH - oy0);
+  const int iy0 = oy0 * S - same_pad(H, K, S), ix0 = ox0 * S - same_pad(W, K, S);
+  const T* X = (const T*)g.x + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * g.lz.ld + c0;
+  T* Y = (T*)g.y + ((size_t)g.pout.row_off[seg] + (size_t)n * OH * OW) * C + c0;
+  const bool cvalid = c0 + c < C;
+
+  float wr[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(((const T*)g.w)[(size_t)i * C + c0 + c]) : 0.f;
+  if (tid < DCB) {
+    const int cc = c0 + tid;
+    xf[tid] = cc < C ? bn_affine(g.lz.bn, seg, cc, 1.f / (float)seg_rows(g.pin, seg)) : make_float2(1.f, 0.f);
+    gt[tid] = (g.lz.gate && cc < C) ? g.lz.gate[(size_t)n * C + cc] : 1.f;
+  }
+
+  // input rows [r0, r0 + nr) of the block (relative to iy0) <-> registers <-> ring slots
+  auto fetch = [&](auto& rb, int r0, int nr) {
+    constexpr int NV = std::remove_reference_t<decltype(rb)>::NV;
+    rb.ok = 0;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int v = tid + u * 256;
+      const int row = v / RV, rem = v - row * RV, x = rem >> 2, cv = (rem & 3) * 8;
+      const int gy = iy0 + r0 + row, gx = ix0 + x;
+      const bool in = row < nr && gy >= 0 && gy < H && gx >= 0 && gx < W && c0 + cv < C;
+      const uint4* src = reinterpret_cast<const uint4*>(X + (in ? (size_t)(gy * W + gx) * g.lz.ld + cv : 0));
+      rb.v[u][0] = src[0];
+      if constexpr (WORDS == 2) rb.v[u][1] = src[1];
+      rb.ok |= (uint32_t)in << u;
+    }
+  };
+  auto commit = [&](const auto& rb, int r0, int nr) {
+    constexpr int NV = std::remove_reference_t<decltype(rb)>::NV;
+    const int cv0 = (tid & 3) * 8;  // the same 8 channels for every u (256 % 4 == 0)
+    float2 a8[8];
+    float g8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a8[j] = xf[cv0 + j]; g8[j] = gt[cv0 + j]; }
+    const int act = g.lz.act;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int v = tid + u * 256;
+      const int row = v / RV, rem = v - row * RV, x = rem >> 2;
+      if (row >= nr) break;
+      float vals[8];
+      if constexpr (WORDS == 1) {
+        const uint32_t w4[4] = {rb.v[u][0].x, rb.v[u][0].y, rb.v[u][0].z, rb.v[u][0].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          vals[2 * i] = __uint_as_float(w4[i] << 16);
+          vals[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+        }
+      } else {
+        const uint32_t w8[8] = {rb.v[u][0].x, rb.v[u][0].y, rb.v[u][0].z, rb.v[u][0].w,
+                                rb.v[u][1].x, rb.v[u][1].y, rb.v[u][1].z, rb.v[u][1].w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vals[i] = __uint_as_float(w8[i]);
+      }
+      // transform unconditionally and zero the padding by a multiply: a select lets the
+      // compiler branch around the transform per element, and its vmcnt(0) inside those
+      // branches drains every prefetch in flight (the raw vector of a padding slot is a real,
+      // finite input element, see fetch)
+      const float m = ((rb.ok >> u) & 1) ? 1.f : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vals[j] = lazy_apply(vals[j], a8[j], act) * (g8[j] * m);
+      int slot = (r0 % R) + row;
+      if (slot >= R) slot -= R;
+      float* d = ring + (slot * IWS + x) * DCB + cv0;
+      reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
+      reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+    }
+  };
+  auto rows_of = [&](int i) { return i * S + K - S; };  // first new input row of step i
+
+  // prologue: rows [0, K) for step 0; steps 1..D's new rows in flight (slot (i-1) % D)
+  {
+    DwRaw<NVP, WORDS> rp;
+    fetch(rp, 0, K);
+    __syncthreads();  // xf / gt
+    commit(rp, 0, K);
+  }
+  DwRaw<NVS, WORDS> rs[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) fetch(rs[j], rows_of(1 + j), S);
+  __syncthreads();
+
+  float s = 0.f, q = 0.f;
+  auto store_row = [&](int i) {  // output row i from stage buffer i & 1 (after a barrier)
+    const int oy = oy0 + i;
+    const int px = tid >> 2, cv = (tid & 3) * 8;
+    if (px < TW && ox0 + px < OW && c0 + cv < C) {
+      T* dst = Y + ((size_t)oy * OW + ox0 + px) * C + cv;
+      const T* src = &ost[i & 1][px * DCB + cv];
+      if constexpr (sizeof(T) == 2) {
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+      } else {
+        reinterpret_cast<float4*>(dst)[0] = reinterpret_cast<const float4*>(src)[0];
+        reinterpret_cast<float4*>(dst)[1] = reinterpret_cast<const float4*>(src)[1];
+      }
+    }
+  };
+  for (int i0 = 0; i0 < nsteps; i0 += D) {
+#pragma unroll
+  for (int j = 0; j < D; ++j) {
+    const int i = i0 + j;
+    if (i >= nsteps) break;
+    if (i > 0) store_row(i - 1);
+    if (i + 1 < nsteps) commit(rs[j], rows_of(i + 1), S);  // rows of step i+1 (not read by step i)
+    // unconditional: a conditional refill joins old and new values in a copy, and the copy
+    // waits for the load (rows past the block are real or predicated-off elements)
+    fetch(rs[j], rows_of(i + 1 + D), S);
+    float acc[CPG];
+#pragma unroll
+    for (int j = 0; j < CPG; ++j) acc[j] = 0.f;
+    int slot = (i * S) % R;
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh) {
+      const float* rp = ring + (slot * IWS + gc * CPG * S) * DCB + c;
+      float win[WIN];
+#pragma unroll
+      for (int x = 0; x < WIN; ++x) win[x] = rp[x * DCB];
+#pragma unroll
+      for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+        for (int j = 0; j < CPG; ++j) acc[j] += win[j * S + kw] * wr[kh * K + kw];
+      slot = slot + 1 == R ? 0 : slot + 1;
+    }
+#pragma unroll
+    for (int j = 0; j < CPG; ++j) {
+      ost[i & 1][(gc * CPG + j) * DCB + c] = from_f<T>(acc[j]);
+      if (cvalid && ox0 + gc * CPG + j < OW) { s += acc[j]; q += acc[j] * acc[j]; }
+    }
+    __syncthreads();
+  }
+  }
+  store_row(nsteps - 1);
+  if (g.has_stats) {  // the ring is free after the last barrier
+    float* red = ring;
+    red[gc * DCB + c] = s;
+    red[(8 + gc) * DCB + c] = q;
+    __syncthreads();
+    if (tid < DCB && c0 + tid < C) {
+      float ss = 0.f, qq = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { ss += red[k * DCB + tid]; qq += red[(8 + k) * DCB + tid]; }
+      stat_add(g.stats.sum[seg] + c0 + tid, (double)ss);
+      stat_add(g.stats.sq[seg] + c0 + tid, (double)qq);
+    }
+  }
+}
+
+template <typename T, int K, int S, int CPG>
+static int launch_dws_fwd(DwArgs g, hipStream_t s) {
+  constexpr int TW = 8 * CPG;
+  int ohmax = 0;
+  for (int i = 0; i < g.pout.nseg; ++i) ohmax = std::max(ohmax, g.pout.H[i]);
+  DwsPlan pl{};
+  long total = 0;
+  // rows per block: the most that still leaves >= DWS_BLOCKS blocks, at least 2
+  for (int TH = 256; TH >= 2; TH /= 2) {
+    if (TH > 2 * ohmax && TH > 2) continue;
+    total = 0;
+    for (int i = 0; i < g.pout.nseg; ++i) {
+      pl.strips[i] = cdiv(g.pout.W[i], TW);
+      pl.rowblk[i] = cdiv(g.pout.H[i], TH);
+      pl.nblk[i] = g.ncb * g.pout.batch * pl.rowblk[i] * pl.strips[i];
+      total += pl.nblk[i];
+    }
+    pl.TH = TH;
+    if (total >= DWS_BLOCKS) break;
+  }
+  if (total == 0) return EDET_OK;
+  EDET_REQUIRE(total < (1L << 31), "dwconv fwd: grid too large");
+  EDET_LAUNCH((k_dws_fwd<T, K, S, CPG>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
+  return check_launch("edet dwconv fwd (rows)");
+}
+
+// strip width from the widest output segment: 32 columns where it fills them (16 at stride 2,
+// whose input window is twice as wide)
+template <typename T, int K, int S>
+static int dispatch_dws_fwd(const DwArgs& g, hipStream_t s) {
+  int owmax = 0;
+  for (int i = 0; i < g.pout.nseg; ++i) owmax = std::max(owmax, g.pout.W[i]);
+  if (S == 1 && owmax >= 32) return launch_dws_fwd<T, K, S, 4>(g, s);
+  if (owmax >= 16) return launch_dws_fwd<T, K, S, 2>(g, s);
+  return launch_dws_fwd<T, K, S, 1>(g, s);
+}
+
 // Kernel forms: TILE = k_dw_fwd / k_dw_wgrad / k_dw_dgrad (8x8 LDS tiles), DW3 = k_dw3
 // (pipelined tiles), DIRECT = k_dw2_fwd / k_dw2_dgrad (one pixel per thread), DW4 =
-// k_dw4_dgrad (register-blocked patches).  The per-shape choice below was measured with
-// scripts/dw_probe.py.
-enum DwForm { DW_TILE = 0, DW_DW3 = 1, DW_DIRECT = 2, DW_DW4 = 3 };
+// k_dw4_dgrad (register-blocked patches), ROWS = k_dws_fwd (row-streaming strips).  The
+// per-shape choice below was measured with scripts/dw_probe.py / scripts/dw_sweep.py.
+enum DwForm { DW_TILE = 0, DW_DW3 = 1, DW_DIRECT = 2, DW_DW4 = 3, DW_ROWS = 4 };
 
 // block targets of the tile forms (kbench sweep 1024..8192: fwd 2048, wgrad 4096)
 constexpr int DW_GRID_FWD = 2048, DW_GRID_WGRAD = 4096;
@@ -989,6 +1225,10 @@ static DwForm dw_form(int which, int K, int S, int C) {
     // loads all in flight beats the direct form (which re-evaluates the lazy transform per
     // tap) everywhere; the pipelined tiles win where the double-buffered LDS still leaves
     // enough blocks per CU, and take C > 2048 (channel-blocked)
+    // the row-streaming form (k_dws_fwd) wins every k5 shape (1.0-1.37x) and the k3 shapes
+    // below; the 8x8 tiles keep k3 s2 at C = 96 (256^2 input: 194 vs 214 us) and k3 s1 at
+    // C >= 480 (even, or 23 vs 29 us at 16^2 x 1152)
+    if (C <= 2048 && (K == 5 || (S == 1 && C <= 144) || (S == 2 && C >= 192))) return DW_ROWS;
     if ((K == 3 && S == 2 && C >= 192) || (S == 1 && C == 240) || C > 2048) return DW_DW3;
     return DW_TILE;
   }
@@ -1004,6 +1244,7 @@ static int launch_dw(int which, DwArgs g, hipStream_t s) {
   g.ncb = cdiv(g.C, DCB);
   const DwForm form = dw_form(which, K, S, g.C);
   if (which == 0) {
+    if (form == DW_ROWS) return dispatch_dws_fwd<T, K, S>(g, s);
     if (form == DW_DW3) return launch_dw3<T, K, S, false>(g, s);
     if (form == DW_TILE) {
       g.tiles_total = host_tiles(g.pout);

@@ -168,6 +168,25 @@ def test_dwconv_fwd_bwd(dt, k, s, H, W, C, lazy, nseg, workspace_mode):
     close(dw, wr.grad, dt, scale=pout.rows ** 0.5 * 3)
 
 
+@pytest.mark.parametrize("k,s,B,H,C", [(5, 1, 16, 64, 240), (3, 1, 8, 100, 64), (5, 2, 16, 72, 144)])
+def test_dwconv_fwd_long_blocks(k, s, B, H, C):
+    """Forward at batch sizes where a row-streaming block walks many output rows (its LDS
+    ring of K+S input rows wraps several times) and strips end inside the image."""
+    rng = np.random.default_rng(k + H)
+    pin = Pyr(B, [(H, H)])
+    pout = pin.strided(s)
+    x = pyr_data(rng, pin, C, "bf16")
+    lz = LazyDesc(x, pin, C, bn=make_bn(x, pin, C, rng), act=1, gate=g(torch.rand(B, C), "f32"))
+    w = g(rnd(rng, k * k, C, scale=0.3), "bf16")
+    y = torch.empty(pout.rows, C, dtype=TDT["bf16"], device=DEV)
+    st = [(zeros64(C), zeros64(C))]
+    L.call("edet_dwconv_fwd", DT["bf16"], lz.c, pin.c, C, k, s, vp(w), vp(y), pout.c, stat_out(st), stream())
+    ref = dw_ref(lz.cpu_value(), pin, k, s, w.double().cpu())
+    close(y, ref, "bf16")
+    close(st[0][0], ref.sum(0), "bf16", scale=pout.rows ** 0.5 * 4)
+    close(st[0][1], (ref * ref).sum(0), "bf16", scale=pout.rows ** 0.5 * 4)
+
+
 # ----------------------------------------------------------------- lazy backward (BN train bwd)
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("C,act,gate,dsq,scale,nseg", [(40, 0, 0, 0, 0, 1), (96, 1, 1, 1, 0, 1), (64, 1, 0, 0, 1, 2),
