@@ -17,7 +17,9 @@ from gpu_util import LazyDesc, make_bn, stat_out, zeros64  # noqa: E402
 
 SHAPES = [(32, 256, 256, 32, 3, 1), (32, 256, 256, 96, 3, 2), (32, 128, 128, 144, 3, 1), (32, 128, 128, 144, 5, 2),
           (32, 64, 64, 240, 5, 1), (32, 64, 64, 240, 3, 2), (32, 32, 32, 480, 3, 1), (32, 32, 32, 480, 5, 1),
-          (32, 32, 32, 672, 5, 1), (32, 32, 32, 672, 5, 2), (32, 16, 16, 1152, 5, 1), (32, 16, 16, 1152, 3, 1)]
+          (32, 32, 32, 672, 5, 1), (32, 32, 32, 672, 5, 2), (32, 16, 16, 1152, 5, 1), (32, 16, 16, 1152, 3, 1),
+          (32, 0, 0, 64, 3, 1), (32, 64, 64, 64, 3, 1)]  # H = 0: the D0 P3-P7 pyramid
+D0_PYR = [(64, 64), (32, 32), (16, 16), (8, 8), (4, 4)]
 
 
 def timeit(fn, reps=20):
@@ -37,7 +39,7 @@ def main():
     s = stream()
     tot = 0.0
     for B, H, W, C, k, st in SHAPES:
-        pin = Pyr(B, [(H, W)])
+        pin = Pyr(B, D0_PYR if H == 0 else [(H, W)])
         pout = pin.strided(st)
         x = torch.randn(pin.rows, C, device="cuda").to(torch.bfloat16)
         lz = LazyDesc(x, pin, C, bn=make_bn(x, pin, C, rng), act=1)
@@ -46,7 +48,7 @@ def main():
         dy = torch.randn(pout.rows, C, device="cuda").to(torch.bfloat16)
         dx = torch.empty(pin.rows, C, device="cuda", dtype=torch.bfloat16)
         dw = torch.zeros(k * k, C, device="cuda")
-        so = stat_out([(zeros64(C), zeros64(C))])
+        so = stat_out([(zeros64(C), zeros64(C)) for _ in range(pin.nseg)])
         if which == "fwd":
             f = lambda: L.call("edet_dwconv_fwd", L.BF16, lz.c, pin.c, C, k, st, vp(w), vp(y), pout.c, so, s)
         elif which == "dgrad":

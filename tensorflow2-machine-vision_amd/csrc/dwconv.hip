@@ -969,18 +969,21 @@ static int launch_dw3(DwArgs g, hipStream_t s) {
   return check_launch("edet dwconv3");
 }
 
-// ------------------------------------------------------------------ row-streaming forward
+// ------------------------------------------------------------------ row-streaming forms
 // One workgroup = one image x 32 channels x a strip of TW = 8*CPG output columns x up to TH
 // output rows.  It walks down its rows keeping the last K+S transformed input rows of the
 // strip in an LDS ring, so every input element of the strip is loaded and transformed once
 // (halo: (TW-1)*S+K columns per TW*S, K-S rows per block) against 2.25x in the 8x8 tiles for
-// k5; the S input rows of step i+1 are fetched into registers during step i-1, transformed
-// into the ring during step i, and each output row leaves through a double-buffered LDS stage
-// as 16-byte stores.  One barrier per output row.
-// steps of input rows in flight ahead of their commit, and the block count the rows per block
-// are chosen for (scripts/dw_sweep.py over the D0 b32 shapes: 1 step and 1024 blocks were
-// best or within 3 % of best everywhere; 2-4 steps gain nothing, 3072 blocks lose 10-20 %)
-constexpr int DWS_PREFETCH = 1, DWS_BLOCKS = 1024;
+// k5.  The S input rows of step i+1 (and, for wgrad, its dy row) are fetched into registers
+// during step i-1 and committed to LDS during step i; one barrier per output row.
+//   forward: each output row leaves through a double-buffered LDS stage as 16-byte stores;
+//            BN statistics stay in registers until the block ends.
+//   wgrad:   thread (c, column group) accumulates its K*K taps over the block's rows; the
+//            column groups are reduced in LDS and added to dw once per block.
+// The block count the rows per block are chosen for: scripts/dw_sweep.py over the D0 b32
+// shapes, 1024 was best or within 3 % of best everywhere (3072 lost 10-20 %); prefetching 2-4
+// steps ahead instead of 1 gained nothing.
+constexpr int DWS_BLOCKS = 1024;
 struct DwsPlan {
   int TH;                      // output rows per block
   int strips[EDET_MAX_SEG];    // column strips per segment
@@ -995,16 +998,18 @@ struct DwRaw {  // raw input vectors of a fetch, in registers until their commit
   uint32_t ok;
 };
 
-template <typename T, int K, int S, int CPG, int D = DWS_PREFETCH>
-__global__ __launch_bounds__(256) void k_dws_fwd(DwArgs g, DwsPlan pl) {
+template <typename T, int K, int S, int CPG, bool WG>
+__global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
   constexpr int TW = 8 * CPG, IWS = (TW - 1) * S + K, R = K + S;
   constexpr int RV = IWS * (DCB / 8);             // 8-channel vectors per input row
   constexpr int NVS = (S * RV + 255) / 256;       // per thread, S rows (one step)
   constexpr int NVP = (K * RV + 255) / 256;       // per thread, K rows (block prologue)
   constexpr int WORDS = sizeof(T) == 2 ? 1 : 2;
   constexpr int WIN = (CPG - 1) * S + K;
+  static_assert(R * IWS >= 8 * K, "wgrad reduction scratch exceeds the ring");
   __shared__ __attribute__((aligned(16))) float ring[R * IWS * DCB];
-  __shared__ __attribute__((aligned(16))) T ost[2][TW * DCB];
+  __shared__ __attribute__((aligned(16))) T ost[WG ? 1 : 2][WG ? 8 : TW * DCB];  // fwd output stage
+  __shared__ __attribute__((aligned(16))) float dys[WG ? 2 : 1][WG ? TW * DCB : 4];  // wgrad dy rows
   __shared__ float2 xf[DCB];
   __shared__ float gt[DCB];
   const int tid = threadIdx.x, c = tid & 31, gc = tid >> 5;
@@ -1022,13 +1027,15 @@ __global__ __launch_bounds__(256) void k_dws_fwd(DwArgs g, DwsPlan pl) {
   const int oy0 = rb * pl.TH, ox0 = strip * TW;
   const int nsteps = min(pl.TH, OH - oy0);
   const int iy0 = oy0 * S - same_pad(H, K, S), ix0 = ox0 * S - same_pad(W, K, S);
+  const size_t obase = (size_t)g.pout.row_off[seg] + (size_t)n * OH * OW;
   const T* X = (const T*)g.x + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * g.lz.ld + c0;
-  T* Y = (T*)g.y + ((size_t)g.pout.row_off[seg] + (size_t)n * OH * OW) * C + c0;
   const bool cvalid = c0 + c < C;
 
-  float wr[K * K];
+  float wr[WG ? 1 : K * K];
+  if constexpr (!WG) {
 #pragma unroll
-  for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(((const T*)g.w)[(size_t)i * C + c0 + c]) : 0.f;
+    for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(((const T*)g.w)[(size_t)i * C + c0 + c]) : 0.f;
+  }
   if (tid < DCB) {
     const int cc = c0 + tid;
     xf[tid] = cc < C ? bn_affine(g.lz.bn, seg, cc, 1.f / (float)seg_rows(g.pin, seg)) : make_float2(1.f, 0.f);
@@ -1036,9 +1043,9 @@ __global__ __launch_bounds__(256) void k_dws_fwd(DwArgs g, DwsPlan pl) {
   }
 
   // input rows [r0, r0 + nr) of the block (relative to iy0) <-> registers <-> ring slots
-  auto fetch = [&](auto& rb, int r0, int nr) {
-    constexpr int NV = std::remove_reference_t<decltype(rb)>::NV;
-    rb.ok = 0;
+  auto fetch = [&](auto& rg, int r0, int nr) {
+    constexpr int NV = std::remove_reference_t<decltype(rg)>::NV;
+    rg.ok = 0;
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
       const int v = tid + u * 256;
@@ -1046,13 +1053,27 @@ __global__ __launch_bounds__(256) void k_dws_fwd(DwArgs g, DwsPlan pl) {
       const int gy = iy0 + r0 + row, gx = ix0 + x;
       const bool in = row < nr && gy >= 0 && gy < H && gx >= 0 && gx < W && c0 + cv < C;
       const uint4* src = reinterpret_cast<const uint4*>(X + (in ? (size_t)(gy * W + gx) * g.lz.ld + cv : 0));
-      rb.v[u][0] = src[0];
-      if constexpr (WORDS == 2) rb.v[u][1] = src[1];
-      rb.ok |= (uint32_t)in << u;
+      rg.v[u][0] = src[0];
+      if constexpr (WORDS == 2) rg.v[u][1] = src[1];
+      rg.ok |= (uint32_t)in << u;
     }
   };
-  auto commit = [&](const auto& rb, int r0, int nr) {
-    constexpr int NV = std::remove_reference_t<decltype(rb)>::NV;
+  auto unpack8 = [&](const uint4* q, float* o) {
+    if constexpr (WORDS == 1) {
+      const uint32_t w4[4] = {q[0].x, q[0].y, q[0].z, q[0].w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        o[2 * i] = __uint_as_float(w4[i] << 16);
+        o[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+      }
+    } else {
+      const uint32_t w8[8] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y, q[1].z, q[1].w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = __uint_as_float(w8[i]);
+    }
+  };
+  auto commit = [&](const auto& rg, int r0, int nr) {
+    constexpr int NV = std::remove_reference_t<decltype(rg)>::NV;
     const int cv0 = (tid & 3) * 8;  // the same 8 channels for every u (256 % 4 == 0)
     float2 a8[8];
     float g8[8];
@@ -1065,24 +1086,12 @@ __global__ __launch_bounds__(256) void k_dws_fwd(DwArgs g, DwsPlan pl) {
       const int row = v / RV, rem = v - row * RV, x = rem >> 2;
       if (row >= nr) break;
       float vals[8];
-      if constexpr (WORDS == 1) {
-        const uint32_t w4[4] = {rb.v[u][0].x, rb.v[u][0].y, rb.v[u][0].z, rb.v[u][0].w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          vals[2 * i] = __uint_as_float(w4[i] << 16);
-          vals[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
-        }
-      } else {
-        const uint32_t w8[8] = {rb.v[u][0].x, rb.v[u][0].y, rb.v[u][0].z, rb.v[u][0].w,
-                                rb.v[u][1].x, rb.v[u][1].y, rb.v[u][1].z, rb.v[u][1].w};
-#pragma unroll
-        for (int i = 0; i < 8; ++i) vals[i] = __uint_as_float(w8[i]);
-      }
+      unpack8(rg.v[u], vals);
       // transform unconditionally and zero the padding by a multiply: a select lets the
       // compiler branch around the transform per element, and its vmcnt(0) inside those
-      // branches drains every prefetch in flight (the raw vector of a padding slot is a real,
+      // branches drains the prefetch in flight (the raw vector of a padding slot is a real,
       // finite input element, see fetch)
-      const float m = ((rb.ok >> u) & 1) ? 1.f : 0.f;
+      const float m = ((rg.ok >> u) & 1) ? 1.f : 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) vals[j] = lazy_apply(vals[j], a8[j], act) * (g8[j] * m);
       int slot = (r0 % R) + row;
@@ -1092,27 +1101,58 @@ __global__ __launch_bounds__(256) void k_dws_fwd(DwArgs g, DwsPlan pl) {
       reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
     }
   };
+  // wgrad: dy row of step i, pixel tid/4 of the strip, channels (tid%4)*8 (zero outside)
+  uint4 dyr[WORDS];
+  auto fetch_dy = [&](int i) {
+    const int px = tid >> 2, cv = (tid & 3) * 8, oy = oy0 + i;
+    const bool in = px < TW && oy < OH && ox0 + px < OW && c0 + cv < C;
+    const uint4* src = reinterpret_cast<const uint4*>(
+        (const T*)g.dy + (in ? (obase + (size_t)oy * OW + ox0 + px) * C + c0 + cv : 0));
+    dyr[0] = src[0];
+    if constexpr (WORDS == 2) dyr[1] = src[1];
+    if (!in) {
+#pragma unroll
+      for (int w = 0; w < WORDS; ++w) dyr[w] = make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto commit_dy = [&](int i) {
+    const int px = tid >> 2, cv = (tid & 3) * 8;
+    if (px < TW) {
+      float vals[8];
+      unpack8(dyr, vals);
+      float* d = &dys[WG ? (i & 1) : 0][px * DCB + cv];
+      reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
+      reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+    }
+  };
   auto rows_of = [&](int i) { return i * S + K - S; };  // first new input row of step i
 
-  // prologue: rows [0, K) for step 0; steps 1..D's new rows in flight (slot (i-1) % D)
+  // prologue: rows [0, K) (+ dy row 0) for step 0; step 1's in flight
   {
     DwRaw<NVP, WORDS> rp;
     fetch(rp, 0, K);
+    if constexpr (WG) fetch_dy(0);
     __syncthreads();  // xf / gt
     commit(rp, 0, K);
+    if constexpr (WG) commit_dy(0);
   }
-  DwRaw<NVS, WORDS> rs[D];
-#pragma unroll
-  for (int j = 0; j < D; ++j) fetch(rs[j], rows_of(1 + j), S);
+  DwRaw<NVS, WORDS> rs;
+  fetch(rs, rows_of(1), S);
+  if constexpr (WG) fetch_dy(1);
   __syncthreads();
 
-  float s = 0.f, q = 0.f;
-  auto store_row = [&](int i) {  // output row i from stage buffer i & 1 (after a barrier)
+  float s = 0.f, q = 0.f;                 // fwd BN statistics of channel c
+  float acc[WG ? K * K : CPG];            // wgrad taps of channel c
+  if constexpr (WG) {
+#pragma unroll
+    for (int t = 0; t < K * K; ++t) acc[t] = 0.f;
+  }
+  auto store_row = [&](int i) {  // fwd output row i from stage buffer i & 1 (after a barrier)
     const int oy = oy0 + i;
     const int px = tid >> 2, cv = (tid & 3) * 8;
     if (px < TW && ox0 + px < OW && c0 + cv < C) {
-      T* dst = Y + ((size_t)oy * OW + ox0 + px) * C + cv;
-      const T* src = &ost[i & 1][px * DCB + cv];
+      T* dst = (T*)g.y + (obase + (size_t)oy * OW + ox0 + px) * C + c0 + cv;
+      const T* src = &ost[WG ? 0 : (i & 1)][px * DCB + cv];
       if constexpr (sizeof(T) == 2) {
         *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
       } else {
@@ -1121,58 +1161,101 @@ __global__ __launch_bounds__(256) void k_dws_fwd(DwArgs g, DwsPlan pl) {
       }
     }
   };
-  for (int i0 = 0; i0 < nsteps; i0 += D) {
-#pragma unroll
-  for (int j = 0; j < D; ++j) {
-    const int i = i0 + j;
-    if (i >= nsteps) break;
-    if (i > 0) store_row(i - 1);
-    if (i + 1 < nsteps) commit(rs[j], rows_of(i + 1), S);  // rows of step i+1 (not read by step i)
+  for (int i = 0; i < nsteps; ++i) {
+    if constexpr (!WG) {
+      if (i > 0) store_row(i - 1);
+    }
+    if (i + 1 < nsteps) {  // rows of step i+1: ring slots and dy buffer step i does not read
+      commit(rs, rows_of(i + 1), S);
+      if constexpr (WG) commit_dy(i + 1);
+    }
     // unconditional: a conditional refill joins old and new values in a copy, and the copy
     // waits for the load (rows past the block are real or predicated-off elements)
-    fetch(rs[j], rows_of(i + 1 + D), S);
-    float acc[CPG];
-#pragma unroll
-    for (int j = 0; j < CPG; ++j) acc[j] = 0.f;
+    fetch(rs, rows_of(i + 2), S);
+    if constexpr (WG) fetch_dy(i + 2);
     int slot = (i * S) % R;
+    if constexpr (!WG) {
+      float o[CPG];
+#pragma unroll
+      for (int j = 0; j < CPG; ++j) o[j] = 0.f;
+#pragma unroll
+      for (int kh = 0; kh < K; ++kh) {
+        const float* rp = ring + (slot * IWS + gc * CPG * S) * DCB + c;
+        float win[WIN];
+#pragma unroll
+        for (int x = 0; x < WIN; ++x) win[x] = rp[x * DCB];
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+          for (int j = 0; j < CPG; ++j) o[j] += win[j * S + kw] * wr[kh * K + kw];
+        slot = slot + 1 == R ? 0 : slot + 1;
+      }
+#pragma unroll
+      for (int j = 0; j < CPG; ++j) {
+        ost[i & 1][(gc * CPG + j) * DCB + c] = from_f<T>(o[j]);
+        if (cvalid && ox0 + gc * CPG + j < OW) { s += o[j]; q += o[j] * o[j]; }
+      }
+    } else {
+      float dv[CPG];
+#pragma unroll
+      for (int j = 0; j < CPG; ++j) dv[j] = dys[i & 1][(gc * CPG + j) * DCB + c];
+#pragma unroll
+      for (int kh = 0; kh < K; ++kh) {
+        const float* rp = ring + (slot * IWS + gc * CPG * S) * DCB + c;
+        float win[WIN];
+#pragma unroll
+        for (int x = 0; x < WIN; ++x) win[x] = rp[x * DCB];
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) {
+          float a = 0.f;
+#pragma unroll
+          for (int j = 0; j < CPG; ++j) a += win[j * S + kw] * dv[j];
+          acc[kh * K + kw] += a;
+        }
+        slot = slot + 1 == R ? 0 : slot + 1;
+      }
+    }
+    __syncthreads();
+  }
+  if constexpr (!WG) {
+    store_row(nsteps - 1);
+    if (g.has_stats) {  // the ring is free after the last barrier
+      float* red = ring;
+      red[gc * DCB + c] = s;
+      red[(8 + gc) * DCB + c] = q;
+      __syncthreads();
+      if (tid < DCB && c0 + tid < C) {
+        float ss = 0.f, qq = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { ss += red[k * DCB + tid]; qq += red[(8 + k) * DCB + tid]; }
+        stat_add(g.stats.sum[seg] + c0 + tid, (double)ss);
+        stat_add(g.stats.sq[seg] + c0 + tid, (double)qq);
+      }
+    }
+  } else {
+    // column groups reduced one filter row at a time through the (free) ring: [K][8][32]
+    float* red = ring;
 #pragma unroll
     for (int kh = 0; kh < K; ++kh) {
-      const float* rp = ring + (slot * IWS + gc * CPG * S) * DCB + c;
-      float win[WIN];
 #pragma unroll
-      for (int x = 0; x < WIN; ++x) win[x] = rp[x * DCB];
+      for (int kw = 0; kw < K; ++kw) red[(kw * 8 + gc) * DCB + c] = acc[kh * K + kw];
+      __syncthreads();
+      if (tid < K * DCB) {
+        const int kw = tid / DCB, cc = tid - kw * DCB;
+        if (c0 + cc < C) {
+          float sum = 0.f;
 #pragma unroll
-      for (int kw = 0; kw < K; ++kw)
-#pragma unroll
-        for (int j = 0; j < CPG; ++j) acc[j] += win[j * S + kw] * wr[kh * K + kw];
-      slot = slot + 1 == R ? 0 : slot + 1;
-    }
-#pragma unroll
-    for (int j = 0; j < CPG; ++j) {
-      ost[i & 1][(gc * CPG + j) * DCB + c] = from_f<T>(acc[j]);
-      if (cvalid && ox0 + gc * CPG + j < OW) { s += acc[j]; q += acc[j] * acc[j]; }
-    }
-    __syncthreads();
-  }
-  }
-  store_row(nsteps - 1);
-  if (g.has_stats) {  // the ring is free after the last barrier
-    float* red = ring;
-    red[gc * DCB + c] = s;
-    red[(8 + gc) * DCB + c] = q;
-    __syncthreads();
-    if (tid < DCB && c0 + tid < C) {
-      float ss = 0.f, qq = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { ss += red[k * DCB + tid]; qq += red[(8 + k) * DCB + tid]; }
-      stat_add(g.stats.sum[seg] + c0 + tid, (double)ss);
-      stat_add(g.stats.sq[seg] + c0 + tid, (double)qq);
+          for (int k = 0; k < 8; ++k) sum += red[(kw * 8 + k) * DCB + cc];
+          atomicAdd(g.dw + (size_t)(kh * K + kw) * C + c0 + cc, sum);
+        }
+      }
+      __syncthreads();
     }
   }
 }
 
-template <typename T, int K, int S, int CPG>
-static int launch_dws_fwd(DwArgs g, hipStream_t s) {
+template <typename T, int K, int S, int CPG, bool WG>
+static int launch_dws(DwArgs g, hipStream_t s) {
   constexpr int TW = 8 * CPG;
   int ohmax = 0;
   for (int i = 0; i < g.pout.nseg; ++i) ohmax = std::max(ohmax, g.pout.H[i]);
@@ -1192,20 +1275,23 @@ static int launch_dws_fwd(DwArgs g, hipStream_t s) {
     if (total >= DWS_BLOCKS) break;
   }
   if (total == 0) return EDET_OK;
-  EDET_REQUIRE(total < (1L << 31), "dwconv fwd: grid too large");
-  EDET_LAUNCH((k_dws_fwd<T, K, S, CPG>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
-  return check_launch("edet dwconv fwd (rows)");
+  EDET_REQUIRE(total < (1L << 31), "dwconv: grid too large");
+  EDET_LAUNCH((k_dws<T, K, S, CPG, WG>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
+  return check_launch("edet dwconv (rows)");
 }
 
 // strip width from the widest output segment: 32 columns where it fills them (16 at stride 2,
-// whose input window is twice as wide)
-template <typename T, int K, int S>
-static int dispatch_dws_fwd(const DwArgs& g, hipStream_t s) {
+// whose input window is twice as wide; 8 or 32 columns there measured slower, as did 16 at
+// stride 1)
+template <typename T, int K, int S, bool WG>
+static int dispatch_dws(const DwArgs& g, hipStream_t s) {
   int owmax = 0;
   for (int i = 0; i < g.pout.nseg; ++i) owmax = std::max(owmax, g.pout.W[i]);
-  if (S == 1 && owmax >= 32) return launch_dws_fwd<T, K, S, 4>(g, s);
-  if (owmax >= 16) return launch_dws_fwd<T, K, S, 2>(g, s);
-  return launch_dws_fwd<T, K, S, 1>(g, s);
+  if constexpr (S == 1) {
+    if (owmax >= 32) return launch_dws<T, K, S, 4, WG>(g, s);
+  }
+  if (owmax >= 16) return launch_dws<T, K, S, 2, WG>(g, s);
+  return launch_dws<T, K, S, 1, WG>(g, s);
 }
 
 // Kernel forms: TILE = k_dw_fwd / k_dw_wgrad / k_dw_dgrad (8x8 LDS tiles), DW3 = k_dw3
@@ -1217,7 +1303,7 @@ enum DwForm { DW_TILE = 0, DW_DW3 = 1, DW_DIRECT = 2, DW_DW4 = 3, DW_ROWS = 4 };
 // block targets of the tile forms (kbench sweep 1024..8192: fwd 2048, wgrad 4096)
 constexpr int DW_GRID_FWD = 2048, DW_GRID_WGRAD = 4096;
 
-static DwForm dw_form(int which, int K, int S, int C) {
+static DwForm dw_form(int which, int K, int S, int C, int nseg) {
   const bool direct_ok = C <= 2048;
   const bool dw4_ok = C % 8 == 0;  // channel rows split over blockIdx.y past 256 vectors
   if (which == 0) {
@@ -1236,15 +1322,19 @@ static DwForm dw_form(int which, int K, int S, int C) {
     if (dw4_ok) return DW_DW4;
     return direct_ok ? DW_DIRECT : DW_TILE;
   }
+  // wgrad: the row-streaming form wins 1.1-1.5x on single tensors up to C = 672 except k3 s2 at
+  // C = 96 (256^2 input); the BiFPN / head pyramids (C = 64, five levels) keep the pipelined
+  // tiles (30.4 vs 33.2 us), C = 1152 the 8x8 tiles (21.4 vs 25.6 us at k3)
+  if (nseg == 1 && C <= 672 && (K == 5 || S == 1 || C >= 192)) return DW_ROWS;
   return (S == 1 && (C <= 64 || (K == 5 && C == 240))) ? DW_DW3 : DW_TILE;
 }
 
 template <typename T, int K, int S>
 static int launch_dw(int which, DwArgs g, hipStream_t s) {
   g.ncb = cdiv(g.C, DCB);
-  const DwForm form = dw_form(which, K, S, g.C);
+  const DwForm form = dw_form(which, K, S, g.C, g.pin.nseg);
   if (which == 0) {
-    if (form == DW_ROWS) return dispatch_dws_fwd<T, K, S>(g, s);
+    if (form == DW_ROWS) return dispatch_dws<T, K, S, false>(g, s);
     if (form == DW_DW3) return launch_dw3<T, K, S, false>(g, s);
     if (form == DW_TILE) {
       g.tiles_total = host_tiles(g.pout);
@@ -1260,6 +1350,7 @@ static int launch_dw(int which, DwArgs g, hipStream_t s) {
       return check_launch("edet dwconv dgrad");
     }
   } else {
+    if (form == DW_ROWS) return dispatch_dws<T, K, S, true>(g, s);
     if (form == DW_DW3) return launch_dw3<T, K, S, true>(g, s);
     g.tiles_total = host_tiles(g.pout);
     // ~4096 blocks: these loops are latency-bound (768 blocks measured 1.3-1.9x slower,

@@ -169,9 +169,10 @@ def test_dwconv_fwd_bwd(dt, k, s, H, W, C, lazy, nseg, workspace_mode):
 
 
 @pytest.mark.parametrize("k,s,B,H,C", [(5, 1, 16, 64, 240), (3, 1, 8, 100, 64), (5, 2, 16, 72, 144)])
-def test_dwconv_fwd_long_blocks(k, s, B, H, C):
-    """Forward at batch sizes where a row-streaming block walks many output rows (its LDS
-    ring of K+S input rows wraps several times) and strips end inside the image."""
+def test_dwconv_long_blocks(k, s, B, H, C):
+    """Forward and weight gradient at batch sizes where a row-streaming block walks many
+    output rows (its LDS ring of K+S input rows wraps several times) and strips end inside
+    the image."""
     rng = np.random.default_rng(k + H)
     pin = Pyr(B, [(H, H)])
     pout = pin.strided(s)
@@ -185,6 +186,14 @@ def test_dwconv_fwd_long_blocks(k, s, B, H, C):
     close(y, ref, "bf16")
     close(st[0][0], ref.sum(0), "bf16", scale=pout.rows ** 0.5 * 4)
     close(st[0][1], (ref * ref).sum(0), "bf16", scale=pout.rows ** 0.5 * 4)
+    # weight gradient over the same blocks
+    v = lz.cpu_value()
+    wr = w.double().cpu().requires_grad_(True)
+    dy = pyr_data(rng, pout, C, "bf16")
+    (dw_ref(v, pin, k, s, wr) * dy.double().cpu()).sum().backward()
+    dw = zeros(k * k, C)
+    L.call("edet_dwconv_wgrad", DT["bf16"], lz.c, pin.c, C, k, s, vp(dy), pout.c, vp(dw), stream())
+    close(dw, wr.grad, "bf16", scale=pout.rows ** 0.5 * 3)
 
 
 # ----------------------------------------------------------------- lazy backward (BN train bwd)
