@@ -3,7 +3,12 @@ libedet vs the fp64 CPU oracle (oracle/ref_model.py) on identical parameters and
 
 Reduced size for oracle speed: D0 topology at 128x128, batch 2, 5 classes; drop-connect
 masks injected (the reference draws them randomly).  fp32 storage: outputs within 1e-3
-relative (north_star tolerance); bf16 storage: loss within 3 %, gradient cosine > 0.99.
+relative (north_star tolerance).  bf16 storage: measured against the fp32 path's own noise
+floor (the same step on bf16-rounded weights and input; the gradient at initialisation moves
+by cosine ~0.85 under that perturbation alone): gradient deviation within 3x that floor
++ 0.02, loss within 3x the floor's loss change or 0.2 %, predict-layer cosine > 0.95 (see
+test_train_step_bf16_within_fp32_noise_floor).  The headline geometry (512^2, NC=81) and the
+bf16 forward against a bf16-emulating oracle are in test_headline_gpu.py.
 """
 import numpy as np
 import pytest
@@ -330,3 +335,26 @@ def test_d4_topology_forward_parity_fp32():
     for l in range(5):
         assert rel_err(boxes[l].cpu(), rb[l].detach()) < 1e-3, l
         assert rel_err(classes[l].cpu(), rc[l].detach()) < 1e-3, l
+
+
+def test_keras_checkpoint_roundtrip_on_product():
+    """§8(f) row 4: the product's parameter table written in Keras names/layouts and loaded
+    back (checkpoint.py) reproduces every variable, BN moving statistics included, and the
+    forward output bit for bit."""
+    from tf2mv_amd import checkpoint as CK
+    m, _ = _train_model("f32", seed=3)
+    sd = m.state_dict()
+    kr = CK.keras_state_dict(sd)
+    assert kr["efficientnet-b0/blocks_1/conv2d/kernel:0"].shape[:2] == (1, 1)
+    x = torch.randn(1, SIZE, SIZE, 3).cuda()
+    b0, c0 = m.call(x, training=False)
+    b0 = [t.clone() for t in b0]
+    m2, _ = _train_model("f32", seed=4)
+    missing, unknown = CK.load_keras_state_dict(m2, kr)
+    assert not missing and not unknown
+    sd2 = m2.state_dict()
+    for k in sd:
+        np.testing.assert_array_equal(sd2[k], sd[k], err_msg=k)
+    b1, _ = m2.call(x, training=False)
+    for u, v in zip(b0, b1):
+        assert torch.equal(u, v)
