@@ -218,6 +218,12 @@ int edet_se_bwd(int B, int C, int R, int HW, const double* s, const float* z1,
                 const float* gate, const double* dgate, const float* w1, const float* w2,
                 float* dw1, float* db1, float* dw2, float* db2, float* dsq, float* dz1,
                 edet_stream_t stream); /* dz1: [B][R] scratch; weight grads accumulate (+=) */
+/* edet_se_bwd followed by edet_se_bn_combine(B, C, gate, dsq, sums5, acc) in the same two
+ * launches (the combine's sums over the images ride in the weight-gradient pass) */
+int edet_se_bwd_bn(int B, int C, int R, int HW, const double* s, const float* z1,
+                   const float* gate, const double* dgate, const float* w1, const float* w2,
+                   float* dw1, float* db1, float* dw2, float* db2, float* dsq, float* dz1,
+                   const double* sums5, const edet_bngrad64* acc, edet_stream_t stream);
 
 /* ---- out[rows][C] = v(x) = act(bn(x)) * gate: the SE-gated depthwise output written once for
  * the MBConv project conv (mb_conv_block.py:150-154), whose forward GEMM and weight gradient

@@ -20,10 +20,15 @@ from tf2mv_amd.runtime import Pyr, ensure_workspace, stream, vp  # noqa: E402
 from gpu_util import LazyDesc, make_bn, stat_out, zeros64  # noqa: E402
 
 
+KERN = {}
+
+
 def timeit(fn, reps=20):
     if os.environ.get("ONLY"):
         reps = 5
+    L.launched_kernels()
     fn()
+    KERN["last"] = ",".join(sorted(set(k.split("<")[0].replace("(", "") for k in L.launched_kernels())))
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(reps):
@@ -62,24 +67,31 @@ def main():
         s = stream()
         es = 2
         algo = (M * (K + N) + K * N) * es
-        res = {}
+        res, kern = {}, {}
         if (not only or only == "fwd plain"):
             res["fwd plain"] = timeit(lambda: L.call("edet_conv1x1_fwd", L.BF16, plain.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, None, s))
+            kern["fwd plain"] = KERN["last"]
         if (not only or only == "fwd +stats"):
             res["fwd +stats"] = timeit(lambda: L.call("edet_conv1x1_fwd", L.BF16, plain.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, so, s))
+            kern["fwd +stats"] = KERN["last"]
         if (not only or only == "fwd bn+sw"):
             res["fwd bn+sw"] = timeit(lambda: L.call("edet_conv1x1_fwd", L.BF16, lz_bs.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, so, s))
+            kern["fwd bn+sw"] = KERN["last"]
         if (not only or only == "fwd bn+sw+g"):
             res["fwd bn+sw+g"] = timeit(lambda: L.call("edet_conv1x1_fwd", L.BF16, lz_bsg.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, so, s))
+            kern["fwd bn+sw+g"] = KERN["last"]
         if (not only or only == "dgrad") and K % 8 == 0 and N % 8 == 0:
             res["dgrad"] = timeit(lambda: L.call("edet_conv1x1_dgrad", L.BF16, vp(dy), N, pyr.c, N, vp(wt), K, vp(dx), K, 0, s))
+            kern["dgrad"] = KERN["last"]
         if (not only or only == "wgrad plain") and N % 8 == 0:
             res["wgrad plain"] = timeit(lambda: L.call("edet_conv1x1_wgrad", L.BF16, plain.c, pyr.c, K, vp(dy), N, N, vp(dw), vp(db), s))
+            kern["wgrad plain"] = KERN["last"]
         if (not only or only == "wgrad bn+sw+g") and N % 8 == 0:
             res["wgrad bn+sw+g"] = timeit(lambda: L.call("edet_conv1x1_wgrad", L.BF16, lz_bsg.c, pyr.c, K, vp(dy), N, N, vp(dw), vp(db), s))
+            kern["wgrad bn+sw+g"] = KERN["last"]
         print(f"M={M} K={K} N={N}  algorithmic {algo / 1e6:.1f} MB")
         for k, us in res.items():
-            print(f"  {k:14s} {us:8.1f} us  {algo / (us * 1e3):8.1f} GB/s")
+            print(f"  {k:14s} {us:8.1f} us  {algo / (us * 1e3):8.1f} GB/s  {kern.get(k, '')}")
 
 
 if __name__ == "__main__":

@@ -98,6 +98,7 @@ SIGNATURES = {
     "edet_gate_bn_reduce": [c_int, PLazy, c_int, c_int, c_int, P, P, P],
     "edet_se_bn_combine": [c_int, c_int, P, P, P, PBnG, P],
     "edet_se_bwd": [c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "edet_se_bwd_bn": [c_int, c_int, c_int, c_int, P, P, P, P, P, P, P, P, P, P, P, P, P, PBnG, P],
     "edet_residual_fwd": [c_int, PLazy, PLazy, PPyr, c_int, P, P, P],
     "edet_lazy_materialize": [c_int, PLazy, PPyr, c_int, P, P],
     "edet_maxpool_fwd": [c_int, PLazy, c_int, c_int, c_int, c_int, P, P],

@@ -425,16 +425,28 @@ __global__ __launch_bounds__(256) void k_gate_bn_reduce(LArgs g) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_se_bn_combine(int B, int C, const float* gate, const float* dsq,
-                                                       const double* s5, double* dgamma, double* dbeta) {
-  // a half-wave per channel, its lanes over the images (one thread looping B images was B
-  // dependent load rounds on a handful of blocks)
+// a half-wave per channel, its lanes over the images (one thread looping B images was B
+// dependent load rounds on a handful of blocks); `blk` = this block's index among the combine's
+template <bool DSQ_FROM_DZ1>
+__device__ __forceinline__ void se_bn_combine_body(int B, int C, int blk, const float* gate, const float* dsq,
+                                                   const double* s5, double* dgamma, double* dbeta, int R = 0,
+                                                   int HW = 1, const float* dz1 = nullptr,
+                                                   const float* w1 = nullptr) {
   const int half = threadIdx.x >> 5, ln = threadIdx.x & 31;
-  const int c = blockIdx.x * 8 + half;
+  const int c = blk * 8 + half;
   double gb = 0.0, gg = 0.0;
   if (c < C)
     for (int n = ln; n < B; n += 32) {
-      const double gt = gate[(size_t)n * C + c], ds = dsq[(size_t)n * C + c];
+      double ds;
+      if constexpr (DSQ_FROM_DZ1) {  // k_se_wgrad's dsq loop, same order
+        float a = 0.f;
+#pragma unroll 8
+        for (int r = 0; r < R; ++r) a += dz1[(size_t)n * R + r] * w1[(size_t)r * C + c];
+        ds = a / (float)HW;
+      } else {
+        ds = dsq[(size_t)n * C + c];
+      }
+      const double gt = gate[(size_t)n * C + c];
       const size_t i = (size_t)n * C + c, BC = (size_t)B * C;
       gb += gt * s5[1 * BC + i] + ds * s5[2 * BC + i];
       gg += gt * s5[3 * BC + i] + ds * s5[4 * BC + i];
@@ -448,6 +460,11 @@ __global__ __launch_bounds__(256) void k_se_bn_combine(int B, int C, const float
     dbeta[c] += gb;
     dgamma[c] += gg;
   }
+}
+
+__global__ __launch_bounds__(256) void k_se_bn_combine(int B, int C, const float* gate, const float* dsq,
+                                                       const double* s5, double* dgamma, double* dbeta) {
+  se_bn_combine_body<false>(B, C, (int)blockIdx.x, gate, dsq, s5, dgamma, dbeta);
 }
 
 // SE excite: z1 = W1 s + b1 ; gate = sigmoid(W2 swish(z1) + b2)   (layers/se.py:36-39).
@@ -511,10 +528,10 @@ __global__ __launch_bounds__(256) void k_se_dz1(int B, int C, int R, const float
 //   dw2[c][r] += sum_n dz2[n][c] swish(z1[n][r])     dw1[r][c] += sum_n dz1[n][r] s[n][c]
 //   db2[c]    += sum_n dz2[n][c]                     db1[r]    += sum_n dz1[n][r]
 //   dsq[n][c]  = sum_r dz1[n][r] w1[r][c] / HW
-__global__ __launch_bounds__(256) void k_se_wgrad(int B, int C, int R, int HW, int nA, const double* s,
-                                                  const float* z1, const float* gate, const double* dgate,
-                                                  const float* dz1, const float* w1, float* dw1, float* db1,
-                                                  float* dw2, float* db2, float* dsq) {
+__device__ __forceinline__ void k_se_wgrad_body(int B, int C, int R, int HW, int nA, const double* s,
+                                                const float* z1, const float* gate, const double* dgate,
+                                                const float* dz1, const float* w1, float* dw1, float* db1,
+                                                float* dw2, float* db2, float* dsq) {
   if ((int)blockIdx.x < nA) {
     // dw2[c][r], dw1[r][c]: one half-wave per (c, r), its 32 lanes over the images, then a
     // 32-lane tree (the per-thread loop over B serialised B dependent load rounds)
@@ -565,6 +582,29 @@ __global__ __launch_bounds__(256) void k_se_wgrad(int B, int C, int R, int HW, i
     for (int n = 0; n < B; ++n) a += dz1[(size_t)n * R + idx];
     db1[idx] += a;
   }
+}
+
+__global__ __launch_bounds__(256) void k_se_wgrad(int B, int C, int R, int HW, int nA, const double* s,
+                                                  const float* z1, const float* gate, const double* dgate,
+                                                  const float* dz1, const float* w1, float* dw1, float* db1,
+                                                  float* dw2, float* db2, float* dsq) {
+  k_se_wgrad_body(B, C, R, HW, nA, s, z1, gate, dgate, dz1, w1, dw1, db1, dw2, db2, dsq);
+}
+
+// k_se_wgrad with k_se_bn_combine's blocks appended (nW = k_se_wgrad's grid).  dsq is written
+// by the k_se_wgrad blocks of the same launch, so the combine blocks re-derive the dsq values
+// they need from dz1 (final after k_se_dz1) with the same loop, bit for bit, instead of
+// taking a launch of their own
+__global__ __launch_bounds__(256) void k_se_wgrad_bn(int B, int C, int R, int HW, int nA, int nW, const double* s,
+                                                     const float* z1, const float* gate, const double* dgate,
+                                                     const float* dz1, const float* w1, float* dw1, float* db1,
+                                                     float* dw2, float* db2, float* dsq, const double* s5,
+                                                     double* dgamma, double* dbeta) {
+  if ((int)blockIdx.x < nW) {
+    k_se_wgrad_body(B, C, R, HW, nA, s, z1, gate, dgate, dz1, w1, dw1, db1, dw2, db2, dsq);
+    return;
+  }
+  se_bn_combine_body<true>(B, C, (int)blockIdx.x - nW, gate, dsq, s5, dgamma, dbeta, R, HW, dz1, w1);
 }
 
 // heads: out = v(x) * scale[seg][n] + v(res)   (class_net.py:93-96 with drop_connect.py:4-18)
@@ -835,6 +875,21 @@ int edet_se_fwd(int B, int C, int R, const double* s, const float* w1, const flo
   EDET_LAUNCH(k_se_reduce_c, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, s, w1, b1, z1);
   EDET_LAUNCH(k_se_excite, dim3(cdiv(B * C, 256)), dim3(256), 0, st, B, C, R, z1, w2, b2, gate);
   return check_launch("edet se_fwd");
+}
+
+int edet_se_bwd_bn(int B, int C, int R, int HW, const double* s, const float* z1,
+                   const float* gate, const double* dgate, const float* w1, const float* w2,
+                   float* dw1, float* db1, float* dw2, float* db2, float* dsq, float* dz1,
+                   const double* sums5, const edet_bngrad64* acc, edet_stream_t stream) {
+  EDET_REQUIRE(s && z1 && gate && dgate && w1 && w2 && dw1 && db1 && dw2 && db2 && dsq && dz1 && sums5 && acc &&
+                   acc->dgamma[0] && acc->dbeta[0],
+               "se_bwd_bn: null argument");
+  hipStream_t st = (hipStream_t)stream;
+  EDET_LAUNCH(k_se_dz1, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, z1, gate, dgate, w2, dz1);
+  const int nA = cdiv(C * R, 8), nB = cdiv(std::max(B * C, std::max(C, R)), 256);
+  EDET_LAUNCH(k_se_wgrad_bn, dim3(nA + nB + cdiv(C, 8)), dim3(256), 0, st, B, C, R, HW, nA, nA + nB, s, z1, gate,
+              dgate, dz1, w1, dw1, db1, dw2, db2, dsq, sums5, acc->dgamma[0], acc->dbeta[0]);
+  return check_launch("edet se_bwd_bn");
 }
 
 int edet_se_bwd(int B, int C, int R, int HW, const double* s, const float* z1,

@@ -298,9 +298,12 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   constexpr int WM = BM / 2, FM = WM / 16, FN = 2;
   const int LDA = KP + 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // B chunks are double-buffered and fetched one chunk ahead when a chunk is at most 4
+  // vectors per thread (KP <= 128); wider K keeps one buffer and loads each chunk in place
+  const bool bpipe = KP <= 128;
   T* As = reinterpret_cast<T*>(smem);
-  T* Bs = As + BM * LDA;
-  T* Cs = Bs + RNB * LDA;                                 // [BM][LDC] (this split's columns)
+  T* Bs = As + BM * LDA;                                  // [bpipe ? 2 : 1][RNB][LDA]
+  T* Cs = Bs + (bpipe ? 2 : 1) * RNB * LDA;               // [BM][LDC] (this split's columns)
   // per-block BN partials [sum|sq][wm][LDC]: each entry has exactly one writer lane, and the
   // two wm halves are added in a fixed order at the flush (LDS float atomics would make the
   // block partial depend on wave timing, and BN statistics must be reproducible)
@@ -410,16 +413,50 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
     }
   }
   const T* B = (const T*)g.b;
-  for (int ch = ch_begin; ch < ch_end; ++ch) {
-    const int col0 = ch * RNB;
+  using VB = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
+  constexpr int VWB = sizeof(T) == 2 ? 1 : 2, NBV = 4;
+  VB rb[NBV][VWB];
+  auto load_b = [&](int ch, T* bs) {  // in place (global -> LDS)
     for (int v = tid; v < RNB * kv8; v += 256) {
       const int n = v / kv8, kv = (v - n * kv8) * 8;
-      const int gn = col0 + n, nk = K - kv;
-      T* dst = &Bs[n * LDA + kv];
+      const int gn = ch * RNB + n, nk = K - kv;
+      T* dst = &bs[n * LDA + kv];
       if (gn < N && nk > 0) cp8(dst, B + (size_t)gn * g.ldb + kv, nk);
       else zero8(dst);
     }
-    __syncthreads();
+  };
+  auto fetch_b = [&](int ch) {  // registers, every load issued before any use (K % 8 == 0)
+#pragma unroll
+    for (int u = 0; u < NBV; ++u) {
+      const int v = tid + u * 256;
+      const int n = v / kv8, kv = (v - n * kv8) * 8;
+      const int gn = ch * RNB + n;
+      const bool ok = v < RNB * kv8 && gn < N && kv < K;
+      const VB* src = reinterpret_cast<const VB*>(B + (ok ? (size_t)gn * g.ldb + kv : 0));
+#pragma unroll
+      for (int w = 0; w < VWB; ++w) rb[u][w] = ok ? src[w] : VB{};
+    }
+  };
+  auto commit_b = [&](T* bs) {
+#pragma unroll
+    for (int u = 0; u < NBV; ++u) {
+      const int v = tid + u * 256;
+      if (v >= RNB * kv8) break;
+      const int n = v / kv8, kv = (v - n * kv8) * 8;
+#pragma unroll
+      for (int w = 0; w < VWB; ++w) reinterpret_cast<VB*>(&bs[n * LDA + kv])[w] = rb[u][w];
+    }
+  };
+  load_b(ch_begin, Bs);
+  __syncthreads();
+  if (bpipe && ch_begin + 1 < ch_end) fetch_b(ch_begin + 1);
+  for (int ch = ch_begin; ch < ch_end; ++ch) {
+    const int col0 = ch * RNB;
+    T* Bc = Bs + (bpipe ? ((ch - ch_begin) & 1) * RNB * LDA : 0);
+    if (!bpipe && ch > ch_begin) {
+      load_b(ch, Bs);
+      __syncthreads();
+    }
 
     floatx4 acc[FM][FN];
 #pragma unroll
@@ -434,7 +471,7 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
           af[i] = lds_frag_bf16(&As[(wm * WM + i * 16 + (lane & 15)) * LDA + k0 + 8 * (lane >> 4)]);
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          bfr[j] = lds_frag_bf16(&Bs[(wn * 32 + j * 16 + (lane & 15)) * LDA + k0 + 8 * (lane >> 4)]);
+          bfr[j] = lds_frag_bf16(&Bc[(wn * 32 + j * 16 + (lane & 15)) * LDA + k0 + 8 * (lane >> 4)]);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -447,7 +484,7 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
 #pragma unroll
           for (int i = 0; i < FM; ++i) af[i] = As[(wm * WM + i * 16 + (lane & 15)) * LDA + k0 + 4 * s + (lane >> 4)];
 #pragma unroll
-          for (int j = 0; j < FN; ++j) bfr[j] = Bs[(wn * 32 + j * 16 + (lane & 15)) * LDA + k0 + 4 * s + (lane >> 4)];
+          for (int j = 0; j < FN; ++j) bfr[j] = Bc[(wn * 32 + j * 16 + (lane & 15)) * LDA + k0 + 4 * s + (lane >> 4)];
 #pragma unroll
           for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -480,6 +517,10 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
           red[(2 + wm) * LDC + col - cbase] += q;
         }
       }
+    }
+    if (bpipe && ch + 1 < ch_end) {  // the other buffer was last read by chunk ch-1
+      commit_b(Bs + ((ch + 1 - ch_begin) & 1) * RNB * LDA);
+      if (ch + 2 < ch_end) fetch_b(ch + 2);
     }
     __syncthreads();
   }
@@ -1667,7 +1708,8 @@ static int launch_gemm(GemmArgs g, hipStream_t s) {
 
 template <typename T, int BM, bool LAZY>
 static size_t gemm_r_lds(int K, int KP, int LDC) {
-  return (size_t)(BM + RNB) * (KP + 8) * sizeof(T) + (size_t)BM * LDC * sizeof(T) + 4 * (size_t)LDC * sizeof(float) +
+  return (size_t)(BM + (KP <= 128 ? 2 : 1) * RNB) * (KP + 8) * sizeof(T) + (size_t)BM * LDC * sizeof(T) +
+         4 * (size_t)LDC * sizeof(float) +
          (LAZY ? (size_t)K * (sizeof(float2) + 2 * sizeof(float)) : 0);
 }
 

@@ -59,10 +59,6 @@ def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor
         else:
             dgate = eng.zeros64(B, out.C)
             L.call("edet_gate_grad", eng.dt, lz, B, HW, out.C, vp(rec.t), vp(dgate), s)
-        dsq = torch.empty((B, out.C), dtype=torch.float32, device=eng.device)
-        dz1 = torch.empty((B, se.R), dtype=torch.float32, device=eng.device)
-        L.call("edet_se_bwd", B, out.C, se.R, HW, vp(se.s), vp(se.z1), vp(se.gate), vp(dgate),
-               vp(se.w1), vp(se.w2), vp(se.dw1), vp(se.db1), vp(se.dw2), vp(se.db2), vp(dsq), vp(dz1), s)
     grads = acc = None
     if out.bns is not None:
         grads = _bn_grads(out.bns)
@@ -71,10 +67,17 @@ def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor
         acc = L.BnGrad64()
         for i in range(len(out.bns)):
             acc.dgamma[i], acc.dbeta[i] = acc_t[0, i].data_ptr(), acc_t[1, i].data_ptr()
-        if fused_se:
-            L.call("edet_se_bn_combine", out.pyr.batch, out.C, vp(out.gate), vp(dsq), vp(sums5), acc, s)
+    if out.se is not None:
+        dsq = torch.empty((B, out.C), dtype=torch.float32, device=eng.device)
+        dz1 = torch.empty((B, se.R), dtype=torch.float32, device=eng.device)
+        args = (B, out.C, se.R, HW, vp(se.s), vp(se.z1), vp(se.gate), vp(dgate), vp(se.w1), vp(se.w2),
+                vp(se.dw1), vp(se.db1), vp(se.dw2), vp(se.db2), vp(dsq), vp(dz1))
+        if fused_se:  # SE backward + the BN sums from sums5 (edet_se_bn_combine) in two launches
+            L.call("edet_se_bwd_bn", *args, vp(sums5), acc, s)
         else:
-            L.call("edet_lazy_bwd_reduce", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, s)
+            L.call("edet_se_bwd", *args, s)
+    if out.bns is not None and not fused_se:
+        L.call("edet_lazy_bwd_reduce", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, s)
     dx = eng.empty(out.pyr.rows, out.C)
     L.call("edet_lazy_bwd_apply", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, grads,
            vp(dx), 0, s)

@@ -248,9 +248,10 @@ def test_lazy_backward(dt, C, act, gate, dsq, scale, nseg):
 
 # ----------------------------------------------------------------- SE
 @pytest.mark.parametrize("dt", DTS)
-def test_squeeze_excite(dt):
-    rng = np.random.default_rng(5)
-    B, H, W, C, R = 3, 9, 7, 96, 4
+@pytest.mark.parametrize("C,R", [(96, 4), (1152, 48), (520, 100)])
+def test_squeeze_excite(dt, C, R):
+    rng = np.random.default_rng(5 + C)
+    B, H, W = 3, 9, 7
     pyr = Pyr(B, [(H, W)])
     x = pyr_data(rng, pyr, C, dt)
     bn = make_bn(x, pyr, C, rng)
@@ -688,3 +689,25 @@ def test_gate_bn_reduce_equals_separate_passes(dt, C, HW):
     torch.testing.assert_close(s5[0], dg, rtol=1e-5, atol=1e-6)
     scale = float(acc_t.abs().max())
     torch.testing.assert_close(acc2_t, acc_t, rtol=1e-4, atol=1e-5 * scale)
+    # edet_se_bwd_bn == edet_se_bwd then edet_se_bn_combine (its dsq): the SE gradients bit for
+    # bit, the fp64 BN sums to fp64 rounding (the combine kernel adds the images as a tree)
+    R = 8
+    sq = g(torch.rand(B, C).double(), "f32").double()
+    z1 = g(rnd(rng, B, R))
+    w1, w2 = g(rnd(rng, R, C, scale=0.2)), g(rnd(rng, C, R, scale=0.3))
+    outs = []
+    for fused in (False, True):
+        dws = [zeros(R, C), zeros(R), zeros(C, R), zeros(C)]
+        dsq2, dz1 = zeros(B, C), zeros(B, R)
+        a_t, a = bngrad64(1, C)
+        args = (B, C, R, HW, vp(sq), vp(z1), vp(gt), vp(s5[0]), vp(w1), vp(w2), *(vp(t) for t in dws), vp(dsq2), vp(dz1))
+        if fused:
+            L.call("edet_se_bwd_bn", *args, vp(s5), a, stream())
+        else:
+            L.call("edet_se_bwd", *args, stream())
+            L.call("edet_se_bn_combine", B, C, vp(gt), vp(dsq2), vp(s5), a, stream())
+        torch.cuda.synchronize()
+        outs.append([t.cpu() for t in dws] + [dsq2.cpu(), a_t.cpu()])
+    for u, v in zip(outs[0][:-1], outs[1][:-1]):
+        assert torch.equal(u, v)
+    torch.testing.assert_close(outs[1][-1], outs[0][-1], rtol=1e-12, atol=1e-12 * float(outs[0][-1].abs().max()))
