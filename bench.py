@@ -198,14 +198,14 @@ class KernelTimer:
         """Per-call table (slowest first): name, shape, us, achieved GB/s."""
         torch.cuda.synchronize()
         rows = []
-        for name, s, e, b, tag, _ in self.rec:
+        for name, s, e, b, tag, kern in self.rec:
             ms = s.elapsed_time(e)
-            rows.append((ms, name, tag, (b / (ms * 1e6)) if (b and ms > 0) else None, b or 0))
+            rows.append((ms, name, tag, (b / (ms * 1e6)) if (b and ms > 0) else None, b or 0, kern))
         rows.sort(reverse=True)
         with open(path, "w") as f:
-            for ms, name, tag, gbs, b in rows[:top]:
+            for ms, name, tag, gbs, b, kern in rows[:top]:
                 g = "" if gbs is None else f"{gbs:8.1f} GB/s"
-                f.write(f"{ms * 1e3:9.1f} us  {name:24s} {tag:40s} {g:14s} {b:12d} B\n")
+                f.write(f"{ms * 1e3:9.1f} us  {name:24s} {tag:40s} {g:14s} {b:12d} B  {kern}\n")
 
     def summary(self, by="entry"):
         """Per entry point (by="entry") or per device kernel (by="kernel", the first kernel a

@@ -329,89 +329,58 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   for (int c = tid; c < 4 * LDC; c += 256) red[c] = 0.f;
   int cur_seg = -1;
 
-  for (int tm = wt; tm < ntm; tm += G) {
-  const int row0 = tm * BM;
-  const int seg = seg_of_row(g.pyr, row0);
-  const int seg_off = g.pyr.row_off[seg];
-  const int seg_end = seg_off + seg_rows(g.pyr, seg);
-  const int hw = g.pyr.H[seg] * g.pyr.W[seg];
-  if (seg != cur_seg) {
-    __syncthreads();
-    if (cur_seg >= 0 && g.has_stats)
-      for (int c = tid; c < ncols; c += 256) {
-        stat_add(g.stats.sum[cur_seg] + cbase + c, (double)(red[c] + red[LDC + c]));
-        stat_add(g.stats.sq[cur_seg] + cbase + c, (double)(red[2 * LDC + c] + red[3 * LDC + c]));
-        red[c] = red[LDC + c] = red[2 * LDC + c] = red[3 * LDC + c] = 0.f;
-      }
-    if constexpr (LAZY) {
-      const float inv = 1.f / (float)seg_rows(g.pyr, seg);
-      for (int k = tid; k < K; k += 256) xf[k] = bn_affine(g.lz.bn, seg, k, inv);
-    }
-    cur_seg = seg;
-    __syncthreads();
-  }
-  // ---- SE gate rows of this tile's images in LDS (a tile spans <= 2 images when hw >= BM)
-  const bool gate_lds = LAZY && g.lz.gate != nullptr && hw >= BM;
-  const int n_lo = (row0 - seg_off) / hw;
-  if (gate_lds) {
-    for (int k = tid; k < 2 * K; k += 256) {
-      const int n = n_lo + (k >= K);
-      gt[k] = (n < g.pyr.batch) ? g.lz.gate[(size_t)n * K + (k >= K ? k - K : k)] : 0.f;
-    }
-    __syncthreads();
-  }
-  // ---- A tile (once per row tile); UNR vector loads in flight per thread before any use
+  // A tile rows: vector v = v0 + tid + u*256 is row v / kv8, channels (v % kv8) * 8 .. +8
   const T* A = (const T*)g.a;
   const int kv8 = KP / 8;
-  {
-    using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
-    constexpr int VW = sizeof(T) == 2 ? 1 : 2, UNR = 4;
-    for (int v0 = tid; v0 < BM * kv8; v0 += 256 * UNR) {
-      V raw[UNR][VW];
+  using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
+  constexpr int VW = sizeof(T) == 2 ? 1 : 2, UNR = 4;
+  auto fetch_a = [&](V (&raw)[UNR][VW], int tmt, int v0) {  // select-predicated, all in flight
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        const int v = v0 + u * 256;
-        const int r = v / kv8, kv = (v - r * kv8) * 8;
-        const int grow = row0 + r;
+    for (int u = 0; u < UNR; ++u) {
+      const int v = v0 + tid + u * 256;
+      const int r = v / kv8, kv = (v - r * kv8) * 8;
+      const int grow = tmt * BM + r;
+      const bool ok = v < BM * kv8 && grow < g.M && kv < K;  // K % 8 == 0: whole vectors
+      const V* src = reinterpret_cast<const V*>(A + (ok ? (size_t)grow * g.lda + kv : 0));
 #pragma unroll
-        for (int w = 0; w < VW; ++w) raw[u][w] = V{};
-        if (v < BM * kv8 && grow < g.M && kv < K) {  // K % 8 == 0: whole vectors
-          const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + kv);
+      for (int w = 0; w < VW; ++w) raw[u][w] = ok ? src[w] : V{};
+    }
+  };
+  auto commit_a = [&](const V (&raw)[UNR][VW], int v0, int row0, int seg_off, int hw, bool gate_lds, int n_lo) {
 #pragma unroll
-          for (int w = 0; w < VW; ++w) raw[u][w] = src[w];
-        }
-      }
+    for (int u = 0; u < UNR; ++u) {
+      const int v = v0 + tid + u * 256;
+      if (v >= BM * kv8) break;
+      const int r = v / kv8, kv = (v - r * kv8) * 8;
+      const int grow = row0 + r;
+      T* dst = &As[r * LDA + kv];
+      if constexpr (LAZY) {
+        const T* e = reinterpret_cast<const T*>(&raw[u][0]);
+        float vals[8];
+        const bool live = grow < g.M && kv < K;
+        const int img = (grow - seg_off) / hw;
+        const float* gp = nullptr;
+        if (live && g.lz.gate) gp = gate_lds ? gt + (img - n_lo) * K : g.lz.gate + (size_t)img * K;
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        const int v = v0 + u * 256;
-        if (v >= BM * kv8) break;
-        const int r = v / kv8, kv = (v - r * kv8) * 8;
-        const int grow = row0 + r;
-        T* dst = &As[r * LDA + kv];
-        if constexpr (LAZY) {
-          const T* e = reinterpret_cast<const T*>(&raw[u][0]);
-          float vals[8];
-          const bool live = grow < g.M && kv < K;
-          const int img = (grow - seg_off) / hw;
-          const float* gp = nullptr;
-          if (live && g.lz.gate) gp = gate_lds ? gt + (img - n_lo) * K : g.lz.gate + (size_t)img * K;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float x = 0.f;
-            if (live) {
-              x = lazy_apply(to_f<T>(e[j]), xf[kv + j], g.lz.act);
-              if (gp) x *= gp[kv + j];
-            }
-            vals[j] = x;
+        for (int j = 0; j < 8; ++j) {
+          float x = 0.f;
+          if (live) {
+            x = lazy_apply(to_f<T>(e[j]), xf[kv + j], g.lz.act);
+            if (gp) x *= gp[kv + j];
           }
-          st8(dst, vals);
-        } else {
-#pragma unroll
-          for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(dst)[w] = raw[u][w];
+          vals[j] = x;
         }
+        st8(dst, vals);
+      } else {
+#pragma unroll
+        for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(dst)[w] = raw[u][w];
       }
     }
-  }
+  };
+  const bool apre = BM * kv8 <= 256 * UNR;
+  V araw[UNR][VW];
+  if (apre && wt < ntm) fetch_a(araw, wt, 0);
+  const bool bres = ch_end - ch_begin == 1;  // this split's B chunk stays in LDS for every tile
   const T* B = (const T*)g.b;
   using VB = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
   constexpr int VWB = sizeof(T) == 2 ? 1 : 2, NBV = 4;
@@ -447,7 +416,54 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
       for (int w = 0; w < VWB; ++w) reinterpret_cast<VB*>(&bs[n * LDA + kv])[w] = rb[u][w];
     }
   };
-  load_b(ch_begin, Bs);
+  if (bres) load_b(ch_begin, Bs);  // (visible after the first tile's barrier)
+
+  for (int tm = wt; tm < ntm; tm += G) {
+  const int row0 = tm * BM;
+  const int seg = seg_of_row(g.pyr, row0);
+  const int seg_off = g.pyr.row_off[seg];
+  const int seg_end = seg_off + seg_rows(g.pyr, seg);
+  const int hw = g.pyr.H[seg] * g.pyr.W[seg];
+  if (seg != cur_seg) {
+    __syncthreads();
+    if (cur_seg >= 0 && g.has_stats)
+      for (int c = tid; c < ncols; c += 256) {
+        stat_add(g.stats.sum[cur_seg] + cbase + c, (double)(red[c] + red[LDC + c]));
+        stat_add(g.stats.sq[cur_seg] + cbase + c, (double)(red[2 * LDC + c] + red[3 * LDC + c]));
+        red[c] = red[LDC + c] = red[2 * LDC + c] = red[3 * LDC + c] = 0.f;
+      }
+    if constexpr (LAZY) {
+      const float inv = 1.f / (float)seg_rows(g.pyr, seg);
+      for (int k = tid; k < K; k += 256) xf[k] = bn_affine(g.lz.bn, seg, k, inv);
+    }
+    cur_seg = seg;
+    __syncthreads();
+  }
+  // ---- SE gate rows of this tile's images in LDS (a tile spans <= 2 images when hw >= BM)
+  const bool gate_lds = LAZY && g.lz.gate != nullptr && hw >= BM;
+  const int n_lo = (row0 - seg_off) / hw;
+  if (gate_lds) {
+    for (int k = tid; k < 2 * K; k += 256) {
+      const int n = n_lo + (k >= K);
+      gt[k] = (n < g.pyr.batch) ? g.lz.gate[(size_t)n * K + (k >= K ? k - K : k)] : 0.f;
+    }
+    __syncthreads();
+  }
+  // ---- A tile (once per row tile); UNR vector loads in flight per thread before any use.
+  // When the whole tile is one round of UNR vectors per thread, the next tile's round is
+  // fetched here and committed at the next tile's start (its HBM latency overlaps this tile's
+  // MFMAs, epilogue and write-out)
+  if (apre) {
+    commit_a(araw, 0, row0, seg_off, hw, gate_lds, n_lo);
+    if (tm + G < ntm) fetch_a(araw, tm + G, 0);
+  } else {
+    for (int v0 = 0; v0 < BM * kv8; v0 += 256 * UNR) {
+      V raw[UNR][VW];
+      fetch_a(raw, tm, v0);
+      commit_a(raw, v0, row0, seg_off, hw, gate_lds, n_lo);
+    }
+  }
+  if (!bres) load_b(ch_begin, Bs);
   __syncthreads();
   if (bpipe && ch_begin + 1 < ch_end) fetch_b(ch_begin + 1);
   for (int ch = ch_begin; ch < ch_end; ++ch) {
@@ -1502,7 +1518,9 @@ static int dispatch_pwb(const GemmArgs& g, hipStream_t s, bool& done) {
 constexpr int GS_PF = EDET_GS_PF;  // row groups in flight ahead of the one being computed
 template <typename T, int NF, int KS, bool LAZY>
 __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
-  __shared__ float red[2][4][NF * 16];
+  // BN statistics: per wave and segment (a wave's groups ascend, so it meets each segment
+  // once), summed over the block's waves in a fixed order at the end
+  __shared__ float red[EDET_MAX_SEG][2][4][NF * 16];
   constexpr int LDW = NF * 16 + 8;  // wave-private output staging row (bf16), padded
   __shared__ __attribute__((aligned(16))) uint16_t stg[4][16 * LDW];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1546,6 +1564,27 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   for (int f = 0; f < NF; ++f)
 #pragma unroll
     for (int r = 0; r < 4; ++r) { ss[f][r] = 0.f; sq[f][r] = 0.f; }
+  if (g.has_stats)
+    for (int i = threadIdx.x; i < EDET_MAX_SEG * 2 * 4 * NF * 16; i += 256) (&red[0][0][0][0])[i] = 0.f;
+  int cur_seg = -1, seg_end = g.has_stats ? 0 : M;
+  // lanes sharing (lane >> 4) hold the same 4 channels of 16 different rows
+  auto wflush = [&](int sg) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float a = ss[f][r], b = sq[f][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
+        if ((lane & 15) == 0) {
+          red[sg][0][wave][16 * f + 4 * (lane >> 4) + r] = a;
+          red[sg][1][wave][16 * f + 4 * (lane >> 4) + r] = b;
+        }
+        ss[f][r] = 0.f;
+        sq[f][r] = 0.f;
+      }
+  };
+  if (g.has_stats) __syncthreads();  // red zeroed before any wave flushes
   const int ngroups = (M + 15) / 16, gstride = gridDim.x * 4;
   // the next groups' A rows are fetched before this group's stores are issued (vmcnt
   // counts loads and stores in order: a load issued after the stores would wait for them)
@@ -1563,7 +1602,15 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   for (int u = 0; u < GS_PF; ++u) fetch(blockIdx.x * 4 + wave + u * gstride, pre[u]);
   for (int grp = blockIdx.x * 4 + wave; grp < ngroups; grp += gstride) {
     const int row = grp * 16 + (lane & 15);
-    const bool live = row < M;
+    if (g.has_stats && grp * 16 >= seg_end) {  // wave-uniform; segments start on 128-row multiples
+      const int sg = seg_of_row(g.pyr, grp * 16);  // (padding rows past a segment map to it)
+      if (sg != cur_seg) {
+        if (cur_seg >= 0) wflush(cur_seg);
+        cur_seg = sg;
+        seg_end = g.pyr.row_off[sg] + seg_rows(g.pyr, sg);
+      }
+    }
+    const bool live = row < M && row < seg_end;
     uint4 raw[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) raw[ks] = pre[0][ks];
@@ -1628,26 +1675,15 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   if (!g.has_stats) return;  // block-uniform
-  // lanes sharing (lane >> 4) hold the same 4 channels of 16 different rows
-#pragma unroll
-  for (int f = 0; f < NF; ++f)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float a = ss[f][r], b = sq[f][r];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
-      if ((lane & 15) == 0) {
-        red[0][wave][16 * f + 4 * (lane >> 4) + r] = a;
-        red[1][wave][16 * f + 4 * (lane >> 4) + r] = b;
-      }
-    }
+  if (cur_seg >= 0) wflush(cur_seg);
   __syncthreads();
-  for (int n = threadIdx.x; n < N; n += 256) {
-    const float a = (red[0][0][n] + red[0][1][n]) + (red[0][2][n] + red[0][3][n]);
-    const float b = (red[1][0][n] + red[1][1][n]) + (red[1][2][n] + red[1][3][n]);
-    stat_add(g.stats.sum[0] + n, (double)a);
-    stat_add(g.stats.sq[0] + n, (double)b);
-  }
+  for (int sg = 0; sg < g.pyr.nseg; ++sg)
+    for (int n = threadIdx.x; n < N; n += 256) {
+      const float a = (red[sg][0][0][n] + red[sg][0][1][n]) + (red[sg][0][2][n] + red[sg][0][3][n]);
+      const float b = (red[sg][1][0][n] + red[sg][1][1][n]) + (red[sg][1][2][n] + red[sg][1][3][n]);
+      stat_add(g.stats.sum[sg] + n, (double)a);
+      stat_add(g.stats.sq[sg] + n, (double)b);
+    }
 }
 
 template <typename T, bool LAZY, int NF, int KS>
@@ -1675,19 +1711,20 @@ static int launch_gemm_s_n(const GemmArgs& g, hipStream_t s) {
   }
 }
 
-// K <= 32 and N <= 160 with statistics or a lazy A (one segment); also 32 < K <= 64, N <= 96
-// for the plain statistics-free GEMMs (the 1x1 dgrads), on pyramids too: rows between
-// segments are padding and only ever written
+// K <= 32 and N <= 160 (a lazy A on one segment), and 32 < K <= 64, N <= 96 for a plain A
+// (the 1x1 dgrads and the BiFPN / head pointwise convs), with BN statistics per segment on
+// pyramids: rows between segments are padding, only ever written
 template <typename T, bool LAZY>
 static int dispatch_gemm_s(const GemmArgs& g, hipStream_t s, bool& done) {
   done = false;
   if (sizeof(T) != 2 || g.K % 8 || g.N % 8 || g.accumulate || g.ldc % 8 || g.lda % 8 || g.ldb % 8) return EDET_OK;
-  const bool plain = !LAZY && !g.has_stats;
-  if (g.K <= 32 && g.N <= 160 && (g.pyr.nseg == 1 || plain)) {
+  // a plain A may span a pyramid (statistics per segment); the lazy transform reads segment
+  // 0's BN affine and SE gate
+  if (g.K <= 32 && g.N <= 160 && (g.pyr.nseg == 1 || !LAZY)) {
     done = true;
     return launch_gemm_s_n<T, LAZY, 1>(g, s);
   }
-  if (plain && g.K <= 64 && g.N <= 96) {
+  if (!LAZY && g.K <= 64 && g.N <= 96) {
     done = true;
     return launch_gemm_s_n<T, LAZY, 2>(g, s);
   }
