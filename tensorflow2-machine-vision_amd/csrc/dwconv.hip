@@ -998,18 +998,22 @@ struct DwRaw {  // raw input vectors of a fetch, in registers until their commit
   uint32_t ok;
 };
 
-template <typename T, int K, int S, int CPG, bool WG>
+template <typename T, int K, int S, int CPG, bool WG, int P>
 __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
-  constexpr int TW = 8 * CPG, IWS = (TW - 1) * S + K, R = K + S;
+  // P output rows per step: they share (P-1)*S... of their K input rows, so each input row of
+  // the step is read from LDS once for all of them, and one barrier serves P rows
+  constexpr int TW = 8 * CPG, IWS = (TW - 1) * S + K;
+  constexpr int NR = (P - 1) * S + K;             // input rows one step reads
+  constexpr int R = NR + P * S;                   // ring: those + the next step's new rows
   constexpr int RV = IWS * (DCB / 8);             // 8-channel vectors per input row
-  constexpr int NVS = (S * RV + 255) / 256;       // per thread, S rows (one step)
-  constexpr int NVP = (K * RV + 255) / 256;       // per thread, K rows (block prologue)
+  constexpr int NVS = (P * S * RV + 255) / 256;   // per thread, P*S rows (one step)
+  constexpr int NVP = (NR * RV + 255) / 256;      // per thread, NR rows (block prologue)
   constexpr int WORDS = sizeof(T) == 2 ? 1 : 2;
   constexpr int WIN = (CPG - 1) * S + K;
   static_assert(R * IWS >= 8 * K, "wgrad reduction scratch exceeds the ring");
   __shared__ __attribute__((aligned(16))) float ring[R * IWS * DCB];
-  __shared__ __attribute__((aligned(16))) T ost[WG ? 1 : 2][WG ? 8 : TW * DCB];  // fwd output stage
-  __shared__ __attribute__((aligned(16))) float dys[WG ? 2 : 1][WG ? TW * DCB : 4];  // wgrad dy rows
+  __shared__ __attribute__((aligned(16))) T ost[WG ? 1 : 2][WG ? 8 : P * TW * DCB];  // fwd output stage
+  __shared__ __attribute__((aligned(16))) float dys[WG ? 2 : 1][WG ? P * TW * DCB : 4];  // wgrad dy rows
   __shared__ float2 xf[DCB];
   __shared__ float gt[DCB];
   const int tid = threadIdx.x, c = tid & 31, gc = tid >> 5;
@@ -1025,7 +1029,8 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
   const int c0 = cb * DCB, C = g.C;
   const int OH = g.pout.H[seg], OW = g.pout.W[seg], H = g.pin.H[seg], W = g.pin.W[seg];
   const int oy0 = rb * pl.TH, ox0 = strip * TW;
-  const int nsteps = min(pl.TH, OH - oy0);
+  const int nrows = min(pl.TH, OH - oy0);
+  const int nsteps = cdiv(nrows, P);
   const int iy0 = oy0 * S - same_pad(H, K, S), ix0 = ox0 * S - same_pad(W, K, S);
   const size_t obase = (size_t)g.pout.row_off[seg] + (size_t)n * OH * OW;
   const T* X = (const T*)g.x + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * g.lz.ld + c0;
@@ -1101,116 +1106,145 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
       reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
     }
   };
-  // wgrad: dy row of step i, pixel tid/4 of the strip, channels (tid%4)*8 (zero outside)
-  uint4 dyr[WORDS];
-  auto fetch_dy = [&](int i) {
-    const int px = tid >> 2, cv = (tid & 3) * 8, oy = oy0 + i;
-    const bool in = px < TW && oy < OH && ox0 + px < OW && c0 + cv < C;
-    const uint4* src = reinterpret_cast<const uint4*>(
-        (const T*)g.dy + (in ? (obase + (size_t)oy * OW + ox0 + px) * C + c0 + cv : 0));
-    dyr[0] = src[0];
-    if constexpr (WORDS == 2) dyr[1] = src[1];
-    if (!in) {
+  // wgrad: the P dy rows of step j; vector e = tid + u*256: row e / (4 TW), pixel, channels
+  constexpr int DYV = (P * TW * 4 + 255) / 256;
+  uint4 dyr[DYV][WORDS];
+  auto fetch_dy = [&](int j) {
 #pragma unroll
-      for (int w = 0; w < WORDS; ++w) dyr[w] = make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < DYV; ++u) {
+      const int e = tid + u * 256, p = e / (TW * 4), rem = e - p * (TW * 4);
+      const int px = rem >> 2, cv = (rem & 3) * 8, oy = oy0 + j * P + p;
+      const bool in = p < P && j * P + p < nrows && oy < OH && ox0 + px < OW && c0 + cv < C;
+      const uint4* src = reinterpret_cast<const uint4*>(
+          (const T*)g.dy + (in ? (obase + (size_t)oy * OW + ox0 + px) * C + c0 + cv : 0));
+      dyr[u][0] = src[0];
+      if constexpr (WORDS == 2) dyr[u][1] = src[1];
+      if (!in) {
+#pragma unroll
+        for (int w = 0; w < WORDS; ++w) dyr[u][w] = make_uint4(0, 0, 0, 0);
+      }
     }
   };
-  auto commit_dy = [&](int i) {
-    const int px = tid >> 2, cv = (tid & 3) * 8;
-    if (px < TW) {
-      float vals[8];
-      unpack8(dyr, vals);
-      float* d = &dys[WG ? (i & 1) : 0][px * DCB + cv];
-      reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
-      reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+  auto commit_dy = [&](int j) {
+#pragma unroll
+    for (int u = 0; u < DYV; ++u) {
+      const int e = tid + u * 256, p = e / (TW * 4), rem = e - p * (TW * 4);
+      if (p < P) {
+        const int px = rem >> 2, cv = (rem & 3) * 8;
+        float vals[8];
+        unpack8(dyr[u], vals);
+        float* d = &dys[WG ? (j & 1) : 0][(p * TW + px) * DCB + cv];
+        reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
+        reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+      }
     }
   };
-  auto rows_of = [&](int i) { return i * S + K - S; };  // first new input row of step i
+  auto rows_of = [&](int j) { return j * P * S + K - S; };  // first new input row of step j
 
-  // prologue: rows [0, K) (+ dy row 0) for step 0; step 1's in flight
+  // prologue: rows [0, NR) (+ dy rows) for step 0; step 1's in flight
   {
     DwRaw<NVP, WORDS> rp;
-    fetch(rp, 0, K);
+    fetch(rp, 0, NR);
     if constexpr (WG) fetch_dy(0);
     __syncthreads();  // xf / gt
-    commit(rp, 0, K);
+    commit(rp, 0, NR);
     if constexpr (WG) commit_dy(0);
   }
   DwRaw<NVS, WORDS> rs;
-  fetch(rs, rows_of(1), S);
+  fetch(rs, rows_of(1), P * S);
   if constexpr (WG) fetch_dy(1);
   __syncthreads();
 
   float s = 0.f, q = 0.f;                 // fwd BN statistics of channel c
-  float acc[WG ? K * K : CPG];            // wgrad taps of channel c
+  float acc[WG ? K * K : 1];              // wgrad taps of channel c
   if constexpr (WG) {
 #pragma unroll
     for (int t = 0; t < K * K; ++t) acc[t] = 0.f;
   }
-  auto store_row = [&](int i) {  // fwd output row i from stage buffer i & 1 (after a barrier)
-    const int oy = oy0 + i;
-    const int px = tid >> 2, cv = (tid & 3) * 8;
-    if (px < TW && ox0 + px < OW && c0 + cv < C) {
-      T* dst = (T*)g.y + (obase + (size_t)oy * OW + ox0 + px) * C + c0 + cv;
-      const T* src = &ost[WG ? 0 : (i & 1)][px * DCB + cv];
-      if constexpr (sizeof(T) == 2) {
-        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
-      } else {
-        reinterpret_cast<float4*>(dst)[0] = reinterpret_cast<const float4*>(src)[0];
-        reinterpret_cast<float4*>(dst)[1] = reinterpret_cast<const float4*>(src)[1];
+  auto store_step = [&](int j) {  // fwd output rows of step j from stage buffer j & 1 (after a barrier)
+    for (int e = tid; e < P * TW * 4; e += 256) {
+      const int p = e / (TW * 4), rem = e - p * (TW * 4);
+      const int px = rem >> 2, cv = (rem & 3) * 8, oy = oy0 + j * P + p;
+      if (j * P + p < nrows && ox0 + px < OW && c0 + cv < C) {
+        T* dst = (T*)g.y + (obase + (size_t)oy * OW + ox0 + px) * C + c0 + cv;
+        const T* src = &ost[WG ? 0 : (j & 1)][(p * TW + px) * DCB + cv];
+        if constexpr (sizeof(T) == 2) {
+          *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+        } else {
+          reinterpret_cast<float4*>(dst)[0] = reinterpret_cast<const float4*>(src)[0];
+          reinterpret_cast<float4*>(dst)[1] = reinterpret_cast<const float4*>(src)[1];
+        }
       }
     }
   };
-  for (int i = 0; i < nsteps; ++i) {
+  for (int j = 0; j < nsteps; ++j) {
     if constexpr (!WG) {
-      if (i > 0) store_row(i - 1);
+      if (j > 0) store_step(j - 1);
     }
-    if (i + 1 < nsteps) {  // rows of step i+1: ring slots and dy buffer step i does not read
-      commit(rs, rows_of(i + 1), S);
-      if constexpr (WG) commit_dy(i + 1);
+    if (j + 1 < nsteps) {  // rows of step j+1: ring slots and dy buffer step j does not read
+      commit(rs, rows_of(j + 1), P * S);
+      if constexpr (WG) commit_dy(j + 1);
     }
     // unconditional: a conditional refill joins old and new values in a copy, and the copy
     // waits for the load (rows past the block are real or predicated-off elements)
-    fetch(rs, rows_of(i + 2), S);
-    if constexpr (WG) fetch_dy(i + 2);
-    int slot = (i * S) % R;
+    fetch(rs, rows_of(j + 2), P * S);
+    if constexpr (WG) fetch_dy(j + 2);
+    int slot = (j * P * S) % R;
     if constexpr (!WG) {
-      float o[CPG];
+      float o[P][CPG];
 #pragma unroll
-      for (int j = 0; j < CPG; ++j) o[j] = 0.f;
+      for (int p = 0; p < P; ++p)
 #pragma unroll
-      for (int kh = 0; kh < K; ++kh) {
+        for (int t = 0; t < CPG; ++t) o[p][t] = 0.f;
+#pragma unroll
+      for (int ih = 0; ih < NR; ++ih) {  // input row ih feeds output row p through filter row ih - p*S
         const float* rp = ring + (slot * IWS + gc * CPG * S) * DCB + c;
         float win[WIN];
 #pragma unroll
         for (int x = 0; x < WIN; ++x) win[x] = rp[x * DCB];
 #pragma unroll
-        for (int kw = 0; kw < K; ++kw)
+        for (int p = 0; p < P; ++p) {
+          const int kh = ih - p * S;
+          if (kh < 0 || kh >= K) continue;
 #pragma unroll
-          for (int j = 0; j < CPG; ++j) o[j] += win[j * S + kw] * wr[kh * K + kw];
+          for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+            for (int t = 0; t < CPG; ++t) o[p][t] += win[t * S + kw] * wr[kh * K + kw];
+        }
         slot = slot + 1 == R ? 0 : slot + 1;
       }
 #pragma unroll
-      for (int j = 0; j < CPG; ++j) {
-        ost[i & 1][(gc * CPG + j) * DCB + c] = from_f<T>(o[j]);
-        if (cvalid && ox0 + gc * CPG + j < OW) { s += o[j]; q += o[j] * o[j]; }
+      for (int p = 0; p < P; ++p) {
+        const bool rowok = j * P + p < nrows;
+#pragma unroll
+        for (int t = 0; t < CPG; ++t) {
+          ost[j & 1][(p * TW + gc * CPG + t) * DCB + c] = from_f<T>(o[p][t]);
+          if (rowok && cvalid && ox0 + gc * CPG + t < OW) { s += o[p][t]; q += o[p][t] * o[p][t]; }
+        }
       }
     } else {
-      float dv[CPG];
+      float dv[P][CPG];
 #pragma unroll
-      for (int j = 0; j < CPG; ++j) dv[j] = dys[i & 1][(gc * CPG + j) * DCB + c];
+      for (int p = 0; p < P; ++p)
 #pragma unroll
-      for (int kh = 0; kh < K; ++kh) {
+        for (int t = 0; t < CPG; ++t) dv[p][t] = dys[j & 1][(p * TW + gc * CPG + t) * DCB + c];
+#pragma unroll
+      for (int ih = 0; ih < NR; ++ih) {
         const float* rp = ring + (slot * IWS + gc * CPG * S) * DCB + c;
         float win[WIN];
 #pragma unroll
         for (int x = 0; x < WIN; ++x) win[x] = rp[x * DCB];
 #pragma unroll
-        for (int kw = 0; kw < K; ++kw) {
-          float a = 0.f;
+        for (int p = 0; p < P; ++p) {
+          const int kh = ih - p * S;
+          if (kh < 0 || kh >= K) continue;
 #pragma unroll
-          for (int j = 0; j < CPG; ++j) a += win[j * S + kw] * dv[j];
-          acc[kh * K + kw] += a;
+          for (int kw = 0; kw < K; ++kw) {
+            float a = 0.f;
+#pragma unroll
+            for (int t = 0; t < CPG; ++t) a += win[t * S + kw] * dv[p][t];
+            acc[kh * K + kw] += a;
+          }
         }
         slot = slot + 1 == R ? 0 : slot + 1;
       }
@@ -1218,7 +1252,7 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
     __syncthreads();
   }
   if constexpr (!WG) {
-    store_row(nsteps - 1);
+    store_step(nsteps - 1);
     if (g.has_stats) {  // the ring is free after the last barrier
       float* red = ring;
       red[gc * DCB + c] = s;
@@ -1254,7 +1288,7 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
   }
 }
 
-template <typename T, int K, int S, int CPG, bool WG>
+template <typename T, int K, int S, int CPG, bool WG, int P>
 static int launch_dws(DwArgs g, hipStream_t s) {
   constexpr int TW = 8 * CPG;
   int ohmax = 0;
@@ -1276,7 +1310,7 @@ static int launch_dws(DwArgs g, hipStream_t s) {
   }
   if (total == 0) return EDET_OK;
   EDET_REQUIRE(total < (1L << 31), "dwconv: grid too large");
-  EDET_LAUNCH((k_dws<T, K, S, CPG, WG>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
+  EDET_LAUNCH((k_dws<T, K, S, CPG, WG, P>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
   return check_launch("edet dwconv (rows)");
 }
 
@@ -1287,11 +1321,14 @@ template <typename T, int K, int S, bool WG>
 static int dispatch_dws(const DwArgs& g, hipStream_t s) {
   int owmax = 0;
   for (int i = 0; i < g.pout.nseg; ++i) owmax = std::max(owmax, g.pout.W[i]);
+  // two output rows per step at stride 1 (dw_sweep: fwd 991 -> 975, wgrad even; at stride 2
+  // the ring would grow to K + 3S rows for little shared input)
+  constexpr int P = S == 1 ? 2 : 1;
   if constexpr (S == 1) {
-    if (owmax >= 32) return launch_dws<T, K, S, 4, WG>(g, s);
+    if (owmax >= 32) return launch_dws<T, K, S, 4, WG, P>(g, s);
   }
-  if (owmax >= 16) return launch_dws<T, K, S, 2, WG>(g, s);
-  return launch_dws<T, K, S, 1, WG>(g, s);
+  if (owmax >= 16) return launch_dws<T, K, S, 2, WG, P>(g, s);
+  return launch_dws<T, K, S, 1, WG, P>(g, s);
 }
 
 // Kernel forms: TILE = k_dw_fwd / k_dw_wgrad / k_dw_dgrad (8x8 LDS tiles), DW3 = k_dw3
