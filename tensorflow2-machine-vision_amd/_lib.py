@@ -82,6 +82,7 @@ SIGNATURES = {
     "edet_probe": [P, c_int, P],
     "edet_wall_clock_khz": [P],
     "edet_launched_kernels": [c_char_p, c_size_t],
+    "edet_dev_set": [c_int, c_int],
     "edet_conv1x1_fwd": [c_int, PLazy, PPyr, c_int, P, c_int, P, P, c_int, c_int, PStat, P],
     "edet_conv1x1_dgrad": [c_int, P, c_int, PPyr, c_int, P, c_int, P, c_int, c_int, P],
     "edet_conv1x1_wgrad": [c_int, PLazy, PPyr, c_int, P, c_int, c_int, P, P, P],

@@ -21,6 +21,8 @@ void note_kernel(const char* site);
     ::edet::note_kernel(#K);                \
     hipLaunchKernelGGL(K, __VA_ARGS__);     \
   } while (0)
+// development A/B slots (edet_dev_set); 0 everywhere in production
+int dev_knob(int slot);
 // registered scratch (edet_set_workspace) if it holds n floats, else nullptr
 float* workspace_f32(size_t n_floats);
 // out[i] += sum_s part[s*n + i], fixed order

@@ -1082,7 +1082,8 @@ struct WgsShape {
   int fn, fk;
 };
 // instantiated tiles (16FN x 16FK outputs per block)
-constexpr WgsShape WGS_SHAPES[] = {{1, 2}, {2, 2}, {2, 3}, {3, 2}, {6, 1}};
+constexpr WgsShape WGS_SHAPES[] = {{1, 2}, {2, 2}, {2, 3}, {3, 2}, {6, 1}, {4, 4}, {2, 4}, {4, 2}, {3, 3}};
+constexpr int WGS_NARROW = 5;  // the first five: the narrow tiles of the production plan
 
 template <int FN, int FK>
 static int launch_wgs(WgsArgs g, int grid, hipStream_t s) {
@@ -1098,6 +1099,7 @@ static int dispatch_wgs(WgsArgs g, int fn, int fk, int grid, hipStream_t s) {
 #define EDET_WGS_CASE(A, B) \
   if (fn == A && fk == B) return launch_wgs<A, B>(g, grid, s);
   EDET_WGS_CASE(1, 2) EDET_WGS_CASE(2, 2) EDET_WGS_CASE(2, 3) EDET_WGS_CASE(3, 2) EDET_WGS_CASE(6, 1)
+  EDET_WGS_CASE(4, 4) EDET_WGS_CASE(2, 4) EDET_WGS_CASE(4, 2) EDET_WGS_CASE(3, 3)
 #undef EDET_WGS_CASE
   set_error("wgrad: no tile %dx%d", fn, fk);
   return EDET_EUNSUPPORTED;
@@ -1106,11 +1108,13 @@ static int dispatch_wgs(WgsArgs g, int fn, int fk, int grid, hipStream_t s) {
 // the tile that moves the fewest bytes: each tile re-reads dY for every K tile and A for every
 // N tile (N rounded to the tile's 16-column fragments), plus a small charge per fragment for
 // the MFMA and LDS work of zero-padded columns
-static WgsShape pick_wgs(int N, int K) {
+static WgsShape pick_wgs(int N, int K, bool wide) {
   const int FNt = cdiv(N, 16), FKt = cdiv(K, 16);
   WgsShape best{0, 0};
   double bc = 1e300;
-  for (const WgsShape& t : WGS_SHAPES) {
+  const int nshapes = wide ? (int)(sizeof(WGS_SHAPES) / sizeof(WGS_SHAPES[0])) : WGS_NARROW;
+  for (int si = 0; si < nshapes; ++si) {
+    const WgsShape& t = WGS_SHAPES[si];
     const int ntn = cdiv(FNt, t.fn), ntk = cdiv(FKt, t.fk);
     const double bytes = (double)ntk * 16 * t.fn * ntn + (double)ntn * 16 * t.fk * ntk;
     const double frags = (double)ntn * ntk * t.fn * t.fk;
@@ -1893,8 +1897,10 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
   // wave streams its own rows against the whole N x K tile (k_wgs), each operand read once.
   // Wider tiles need too many accumulators for the occupancy this stream wants (measured
   // slower than the 64x64 cooperative tiles below on every other D0 shape, scripts/wg_probe.py)
-  if (dtype == EDET_BF16 && plain && K % 8 == 0 && cdiv(N, 16) * cdiv(K, 16) <= 6 && g.M >= (1 << 18)) {
-    const WgsShape t = pick_wgs(N, K);
+  const bool wide = dev_knob(3) == 1;
+  if (dtype == EDET_BF16 && plain && K % 8 == 0 &&
+      (wide || (cdiv(N, 16) * cdiv(K, 16) <= 6 && g.M >= (1 << 18)))) {
+    const WgsShape t = pick_wgs(N, K, wide);
     WgsArgs w{};
     w.a = (const uint16_t*)a->x; w.dy = (const uint16_t*)dy; w.dw = dwt; w.db = dbias; w.pyr = *rows;
     w.lda = a->ld; w.lddy = lddy; w.M = g.M; w.K = K; w.N = N;
@@ -1903,25 +1909,43 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
     w.ngrp = cdiv(g.M, 32);
     // 512 blocks of 4 waves, at least 16 row groups per wave; the block's folded tile goes out
     // as fp32 atomics (N*K per block: 1.5K floats at 96 x 16)
-    int splits = std::max(1, std::min(cdiv(512, wtiles), w.ngrp / 64));
+    const int wblocks = dev_knob(4) > 0 ? dev_knob(4) : 512, wmin = dev_knob(5) > 0 ? dev_knob(5) : 64;
+    int splits = std::max(1, std::min(cdiv(wblocks, wtiles), w.ngrp / wmin));
     w.gpb = cdiv(w.ngrp, splits);
     w.splits = cdiv(w.ngrp, w.gpb);
-    w.part = nullptr;
-    return dispatch_wgs(w, t.fn, t.fk, wtiles * w.splits, s);
+    // every block's folded tile lands on the same N*K addresses: hundreds of fp32 atomic adders
+    // per address serialise at the memory side, plain partial stores + the spread sum pass
+    // do not (2M x 16 -> 96: 130 -> 95 us, 2M x 32 -> 16: 57 -> 40 us)
+    w.part = w.splits > 1 ? workspace_f32((size_t)w.splits * ((size_t)N * K + N)) : nullptr;
+    int rc = dispatch_wgs(w, t.fn, t.fk, wtiles * w.splits, s);
+    if (rc || !w.part) return rc;
+    rc = sum_partials(w.part, w.splits, (long)N * K, dwt, s);
+    if (rc || !dbias) return rc;
+    return sum_partials(w.part + (size_t)w.splits * N * K, w.splits, N, dbias, s);
   }
   if (dtype == EDET_BF16) {
     // lazy A (BN / act / gate applied while staging): 64x64 tiles with transposing LDS reads.
     // Stages never straddle a segment: segments start on 128-row boundaries.  ~2048 blocks of
     // at least 8 stages each, fp32 atomics into dW.
-    int split = cdiv(2048, tiles);
-    const int max_split = std::max(1, cdiv(g.M, WT_BM * 8));
+    const int target = dev_knob(0) > 0 ? dev_knob(0) : 2048;
+    const int min_stages = dev_knob(1) > 0 ? dev_knob(1) : 8;
+    int split = cdiv(target, tiles);
+    const int max_split = std::max(1, cdiv(g.M, WT_BM * min_stages));
     if (split > max_split) split = max_split;
     g.rows_per = cdiv(cdiv(g.M, split), WT_BM) * WT_BM;
     split = std::max(1, cdiv(g.M, g.rows_per));
-    g.part = nullptr;
+    // few output tiles split over many row ranges: the same per-address atomic contention as
+    // k_wgs, partials + the sum pass instead (524288 x 24 -> 144: 71 -> 63 us, 131072 x 40 ->
+    // 240: 37 -> 27 us); many tiles keep the atomics (class predict 105 vs 124 us with partials)
+    const bool use_part = dev_knob(2) == 1 || (dev_knob(2) == 0 && tiles <= 4 && split >= 128);
+    g.part = use_part && split > 1 ? workspace_f32((size_t)split * ((size_t)N * K + N)) : nullptr;
     if (plain) EDET_LAUNCH((k_wgrad_tr<false>), dim3(tiles * split), dim3(256), 0, s, g);
     else EDET_LAUNCH((k_wgrad_tr<true>), dim3(tiles * split), dim3(256), 0, s, g);
-    return check_launch("edet wgrad");
+    int rc = check_launch("edet wgrad");
+    if (rc || !g.part) return rc;
+    rc = sum_partials(g.part, split, (long)N * K, dwt, s);
+    if (rc || !dbias) return rc;
+    return sum_partials(g.part + (size_t)split * N * K, split, N, dbias, s);
   }
   int split = cdiv(2048, tiles);
   const int max_split = cdiv(g.M, 32 * 4);  // at least 4 row-chunks per block

@@ -31,6 +31,9 @@ int check_launch(const char* what) {
   return EDET_OK;
 }
 
+static int g_dev[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+int dev_knob(int slot) { return (slot >= 0 && slot < 8) ? g_dev[slot] : 0; }
+
 // Caller-registered scratch for split reductions (weight gradients): blocks write partial
 // results with plain stores, one reduce kernel sums them in a fixed order.  The library still
 // allocates nothing; without a (large enough) workspace the kernels fall back to atomics.
@@ -40,22 +43,31 @@ float* workspace_f32(size_t n_floats) {
   return (g_ws && n_floats * sizeof(float) <= g_ws_bytes) ? (float*)g_ws : nullptr;
 }
 
-// out[i] += sum_{s < S} part[s * n + i]   (fixed order)
+// out[i] += sum_{s < S} part[s * n + i]: one thread per output and chunk of at most
+// SUM_CHUNK partials (8 independent loads in flight).  A single chunk adds in a fixed order;
+// more chunks (grid.y) spread the splits over the chip and add their sums with fp32 atomics
+// (a few adders per address: a long dependent loop over hundreds of splits on the handful of
+// blocks a small output needs was latency-bound)
+constexpr int SUM_CHUNK = 32;
 __global__ __launch_bounds__(256) void k_sum_partials(const float* part, int S, long n, float* out) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // 8 independent loads in flight
-  int s = 0;
-  for (; s + 8 <= S; s += 8)
+  const int s0 = blockIdx.y * SUM_CHUNK, s1 = min(S, s0 + SUM_CHUNK);
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int s = s0;
+  for (; s + 8 <= s1; s += 8)
 #pragma unroll
     for (int u = 0; u < 8; ++u) a[u] += part[(size_t)(s + u) * n + i];
-  for (; s < S; ++s) a[0] += part[(size_t)s * n + i];
-  out[i] += ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  for (; s < s1; ++s) a[0] += part[(size_t)s * n + i];
+  const float t = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  if (gridDim.y == 1) out[i] += t;
+  else atomicAdd(out + i, t);
 }
 
 int sum_partials(const float* part, int S, long n, float* out, hipStream_t st) {
   if (n <= 0) return EDET_OK;
-  EDET_LAUNCH(k_sum_partials, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, S, n, out);
+  const unsigned chunks = (unsigned)((S + SUM_CHUNK - 1) / SUM_CHUNK);
+  EDET_LAUNCH(k_sum_partials, dim3((unsigned)((n + 255) / 256), chunks), dim3(256), 0, st, part, S, n, out);
   return check_launch("edet sum_partials");
 }
 
@@ -94,6 +106,13 @@ int edet_launched_kernels(char* buf, size_t size) {
   const int total = edet::g_nlaunched;
   edet::g_nlaunched = 0;
   return total;
+}
+
+int edet_dev_set(int slot, int value) {
+  if (slot < 0 || slot >= 8) return 0;
+  const int old = edet::g_dev[slot];
+  edet::g_dev[slot] = value;
+  return old;
 }
 
 int edet_set_workspace(void* ptr, size_t bytes) {
