@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--model", default="efficientdet-d0")
     ap.add_argument("--out", default="")
+    ap.add_argument("--dev", default="", help="edet_dev_set slots for the timed replays, e.g. 7=1")
+    ap.add_argument("--seq", default="", help="also write every call's us in launch order")
     args = ap.parse_args()
 
     from tf2mv_amd import _lib as L
@@ -62,10 +64,15 @@ def main():
         rec.append((name, s, e, bench.algorithmic_bytes(name, a, 2), bench.shape_tag(name, a)))
         return r
 
+    for kv in filter(None, args.dev.split(",")):
+        k, v = kv.split("=")
+        L.lib().fns["edet_dev_set"](int(k), int(v))
     L.call = timed  # every package module calls through this one _lib module object
     model.train_step((x, t))
     torch.cuda.synchronize()
     L.call = orig
+    for i in range(8):
+        L.lib().fns["edet_dev_set"](i, 0)
 
     rows, agg = [], {}
     for name, s, e, b, tag in rec:
@@ -87,6 +94,10 @@ def main():
         lines.append(f"{us:9.1f} us  {name:24s} {tag:40s} {gb}")
     txt = "\n".join(lines)
     print(txt)
+    if args.seq:
+        with open(args.seq, "w") as f:
+            for name, s, e, b, tag in rec:
+                f.write(f"{s.elapsed_time(e) * 1e3 / args.reps:.2f} {name} {tag}\n")
     if args.out:
         with open(args.out, "w") as f:
             f.write(txt + "\n")

@@ -132,6 +132,22 @@ __device__ __forceinline__ float row4_sum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// Sum over the 16 lanes of a DPP row (lane bits 0-3), result in every lane: four DPP adds
+// (plain VALU) instead of four __shfl_xor rounds, each a ds_bpermute LDS round trip (the
+// k_gemm_s statistics flush meets a new pyramid level about once per row group: its
+// shuffles cost more than the group's MFMAs)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2 (each lane: its quad's sum)
+  v += dpp_f<0x141>(v);  // row_half_mirror: the other quad of the 8-lane half
+  v += dpp_f<0x140>(v);  // row_mirror: the other half of the row
+  return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -1578,8 +1578,8 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float a = ss[f][r], b = sq[f][r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
+        a = row16_sum(a);
+        b = row16_sum(b);
         if ((lane & 15) == 0) {
           red[sg][0][wave][16 * f + 4 * (lane >> 4) + r] = a;
           red[sg][1][wave][16 * f + 4 * (lane >> 4) + r] = b;
@@ -1589,7 +1589,12 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
       }
   };
   if (g.has_stats) __syncthreads();  // red zeroed before any wave flushes
-  const int ngroups = (M + 15) / 16, gstride = gridDim.x * 4;
+  // each block owns a contiguous range of 16-row groups (its waves interleave inside it), so
+  // a block meets one pyramid level, rarely two: per-wave flushes and the block's fp64
+  // atomics cover only the levels it touched (a grid-strided wave met a new level about once
+  // per group and every block flushed all five)
+  const int ngroups = (M + 15) / 16, gpb = (ngroups + gridDim.x - 1) / gridDim.x;
+  const int g_begin = blockIdx.x * gpb, g_end = min(ngroups, g_begin + gpb);
   // the next groups' A rows are fetched before this group's stores are issued (vmcnt
   // counts loads and stores in order: a load issued after the stores would wait for them)
   auto fetch = [&](int grp, uint4* v) {
@@ -1598,13 +1603,13 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
     for (int ks = 0; ks < KS; ++ks) {
       const int k = 32 * ks + kq;
       v[ks] = make_uint4(0, 0, 0, 0);
-      if (k < K && grp < ngroups) v[ks] = *reinterpret_cast<const uint4*>(A + (size_t)(row < M ? row : 0) * g.lda + k);
+      if (k < K && grp < g_end) v[ks] = *reinterpret_cast<const uint4*>(A + (size_t)(row < M ? row : 0) * g.lda + k);
     }
   };
   uint4 pre[GS_PF][KS];
 #pragma unroll
-  for (int u = 0; u < GS_PF; ++u) fetch(blockIdx.x * 4 + wave + u * gstride, pre[u]);
-  for (int grp = blockIdx.x * 4 + wave; grp < ngroups; grp += gstride) {
+  for (int u = 0; u < GS_PF; ++u) fetch(g_begin + wave + u * 4, pre[u]);
+  for (int grp = g_begin + wave; grp < g_end; grp += 4) {
     const int row = grp * 16 + (lane & 15);
     if (g.has_stats && grp * 16 >= seg_end) {  // wave-uniform; segments start on 128-row multiples
       const int sg = seg_of_row(g.pyr, grp * 16);  // (padding rows past a segment map to it)
@@ -1622,7 +1627,7 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
     for (int u = 0; u + 1 < GS_PF; ++u)
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) pre[u][ks] = pre[u + 1][ks];
-    fetch(grp + GS_PF * gstride, pre[GS_PF - 1]);
+    fetch(grp + GS_PF * 4, pre[GS_PF - 1]);
     bf16x8_t bfrag[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -1681,7 +1686,9 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   if (!g.has_stats) return;  // block-uniform
   if (cur_seg >= 0) wflush(cur_seg);
   __syncthreads();
-  for (int sg = 0; sg < g.pyr.nseg; ++sg)
+  if (g_begin >= g_end) return;
+  const int s_lo = seg_of_row(g.pyr, g_begin * 16), s_hi = seg_of_row(g.pyr, (g_end - 1) * 16);
+  for (int sg = s_lo; sg <= s_hi; ++sg)
     for (int n = threadIdx.x; n < N; n += 256) {
       const float a = (red[sg][0][0][n] + red[sg][0][1][n]) + (red[sg][0][2][n] + red[sg][0][3][n]);
       const float b = (red[sg][1][0][n] + red[sg][1][1][n]) + (red[sg][1][2][n] + red[sg][1][3][n]);

@@ -231,8 +231,8 @@ __global__ __launch_bounds__(256) void k_stem2_fwd(const uint16_t* x, int B, int
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float a = s[t][r], b = q[t][r];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) { a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64); }
+      a = row16_sum(a);
+      b = row16_sum(b);
       if ((lane & 15) == 0) {
         red[0][wave][t * 16 + 4 * g4 + r] = a;
         red[1][wave][t * 16 + 4 * g4 + r] = b;
