@@ -26,7 +26,9 @@ int dev_knob(int slot);
 // registered scratch (edet_set_workspace) if it holds n floats, else nullptr
 float* workspace_f32(size_t n_floats);
 // out[i] += sum_s part[s*n + i], fixed order
-int sum_partials(const float* part, int S, long n, float* out, hipStream_t st);
+// out[i] += sum_s part[s][i] (i < n), and out2[j] += sum_s part[S * n + s * n2 + j] (j < n2) in
+// the same launch when out2 is non-null
+int sum_partials(const float* part, int S, long n, float* out, hipStream_t st, long n2 = 0, float* out2 = nullptr);
 
 #define EDET_REQUIRE(cond, ...)            \
   do {                                     \

@@ -1926,9 +1926,7 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
     w.part = w.splits > 1 ? workspace_f32((size_t)w.splits * ((size_t)N * K + N)) : nullptr;
     int rc = dispatch_wgs(w, t.fn, t.fk, wtiles * w.splits, s);
     if (rc || !w.part) return rc;
-    rc = sum_partials(w.part, w.splits, (long)N * K, dwt, s);
-    if (rc || !dbias) return rc;
-    return sum_partials(w.part + (size_t)w.splits * N * K, w.splits, N, dbias, s);
+    return sum_partials(w.part, w.splits, (long)N * K, dwt, s, N, dbias);  // dW and db, one launch
   }
   if (dtype == EDET_BF16) {
     // lazy A (BN / act / gate applied while staging): 64x64 tiles with transposing LDS reads.
@@ -1950,9 +1948,7 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
     else EDET_LAUNCH((k_wgrad_tr<true>), dim3(tiles * split), dim3(256), 0, s, g);
     int rc = check_launch("edet wgrad");
     if (rc || !g.part) return rc;
-    rc = sum_partials(g.part, split, (long)N * K, dwt, s);
-    if (rc || !dbias) return rc;
-    return sum_partials(g.part + (size_t)split * N * K, split, N, dbias, s);
+    return sum_partials(g.part, split, (long)N * K, dwt, s, N, dbias);  // dW and db, one launch
   }
   int split = cdiv(2048, tiles);
   const int max_split = cdiv(g.M, 32 * 4);  // at least 4 row-chunks per block

@@ -49,9 +49,18 @@ float* workspace_f32(size_t n_floats) {
 // (a few adders per address: a long dependent loop over hundreds of splits on the handful of
 // blocks a small output needs was latency-bound)
 constexpr int SUM_CHUNK = 32;
-__global__ __launch_bounds__(256) void k_sum_partials(const float* part, int S, long n, float* out) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+// Two outputs in one launch (a weight gradient's dW and db): the partials of the second,
+// [S][n2], follow the first's [S][n] in the workspace; outputs i >= n map to out2[i - n].
+__global__ __launch_bounds__(256) void k_sum_partials(const float* part, int S, long n, float* out, long n2,
+                                                      float* out2) {
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n + n2) return;
+  if (i >= n) {
+    part += (size_t)S * n;
+    i -= n;
+    n = n2;
+    out = out2;
+  }
   const int s0 = blockIdx.y * SUM_CHUNK, s1 = min(S, s0 + SUM_CHUNK);
   float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   int s = s0;
@@ -64,10 +73,12 @@ __global__ __launch_bounds__(256) void k_sum_partials(const float* part, int S, 
   else atomicAdd(out + i, t);
 }
 
-int sum_partials(const float* part, int S, long n, float* out, hipStream_t st) {
-  if (n <= 0) return EDET_OK;
+int sum_partials(const float* part, int S, long n, float* out, hipStream_t st, long n2, float* out2) {
+  if (!out2) n2 = 0;
+  if (n + n2 <= 0) return EDET_OK;
   const unsigned chunks = (unsigned)((S + SUM_CHUNK - 1) / SUM_CHUNK);
-  EDET_LAUNCH(k_sum_partials, dim3((unsigned)((n + 255) / 256), chunks), dim3(256), 0, st, part, S, n, out);
+  EDET_LAUNCH(k_sum_partials, dim3((unsigned)((n + n2 + 255) / 256), chunks), dim3(256), 0, st, part, S, n, out, n2,
+              out2);
   return check_launch("edet sum_partials");
 }
 
