@@ -1831,6 +1831,10 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
   // K loop over 128-column tiles measured 1.3-1.4x faster (8192x192x1152, 32768x112x672)
   if (LAZY && g.K >= 112 && g.N > 320) return dispatch_gemm_kloop<T, LAZY>(g, s);
   if (g.K <= 512) {
+    // the largest row tile that still gives >= 256 (row tile, column chunk) blocks: at M = 8192
+    // the 128-row tiles left 64 blocks for 256 CUs (8192 x 320 -> 64: 21 us)
+    const bool fills = (long)cdiv(g.M, 128) * cdiv(g.N, RNB) >= 256;  // (21 -> 19 us at 8192 x 320 -> 64)
+    if (!fills && gemm_r_lds<T, 32, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 32, LAZY>(g, s);
     if (gemm_r_lds<T, 128, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 128, LAZY>(g, s);
     if (gemm_r_lds<T, 64, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 64, LAZY>(g, s);
     if (gemm_r_lds<T, 32, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 32, LAZY>(g, s);
