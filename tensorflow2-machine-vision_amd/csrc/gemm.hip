@@ -1936,8 +1936,15 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
     // lazy A (BN / act / gate applied while staging): 64x64 tiles with transposing LDS reads.
     // Stages never straddle a segment: segments start on 128-row boundaries.  ~2048 blocks of
     // at least 8 stages each, fp32 atomics into dW.
-    const int target = dev_knob(0) > 0 ? dev_knob(0) : 2048;
-    const int min_stages = dev_knob(1) > 0 ? dev_knob(1) : 8;
+    // ~2048 blocks of >= 8 stages; a single 64x64 tile over a long M (the head / BiFPN
+    // pointwise convs) 4096 of >= 4 (174592 x 64 -> 64: 23.8 -> 20.7 us, -> 36: 32.4 -> 23.6);
+    // many tiles over M <= 32768 >= 16 stages (32768 x 112 -> 672: 36.8 -> 32.1 us)
+    // (profiles/r02b_wgrad_plan_sweep.txt)
+    int target = 2048, min_stages = 8;
+    if (tiles == 1) target = 4096, min_stages = 4;
+    else if (tiles >= 22 && g.M >= 16384 && g.M <= 32768) min_stages = 16;
+    if (dev_knob(0) > 0) target = dev_knob(0);
+    if (dev_knob(1) > 0) min_stages = dev_knob(1);
     int split = cdiv(target, tiles);
     const int max_split = std::max(1, cdiv(g.M, WT_BM * min_stages));
     if (split > max_split) split = max_split;
