@@ -1937,12 +1937,13 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
     // Stages never straddle a segment: segments start on 128-row boundaries.  ~2048 blocks of
     // at least 8 stages each, fp32 atomics into dW.
     // ~2048 blocks of >= 8 stages; a single 64x64 tile over a long M (the head / BiFPN
-    // pointwise convs) 4096 of >= 4 (174592 x 64 -> 64: 23.8 -> 20.7 us, -> 36: 32.4 -> 23.6);
-    // many tiles over M <= 32768 >= 16 stages (32768 x 112 -> 672: 36.8 -> 32.1 us)
+    // pointwise convs) or a short M: 4096 of >= 4 (174592 x 64 -> 64: 23.8 -> 17.6 us,
+    // 2048 x 320 -> 64: 10.6 -> 7.7); >= 16 stages for many tiles over M <= 32768 (32768 x 112
+    // -> 672: 36.8 -> 32.1 us), the class predict (106 -> 100) and M >= 524288 (38 -> 35)
     // (profiles/r02b_wgrad_plan_sweep.txt)
     int target = 2048, min_stages = 8;
-    if (tiles == 1) target = 4096, min_stages = 4;
-    else if (tiles >= 22 && g.M >= 16384 && g.M <= 32768) min_stages = 16;
+    if (tiles == 1 || g.M <= 4096) target = 4096, min_stages = 4;
+    else if ((tiles >= 22 && g.M <= 32768) || (tiles >= 12 && g.M >= 131072) || g.M >= 524288) min_stages = 16;
     if (dev_knob(0) > 0) target = dev_knob(0);
     if (dev_knob(1) > 0) min_stages = dev_knob(1);
     int split = cdiv(target, tiles);
