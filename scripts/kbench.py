@@ -53,7 +53,7 @@ def main():
 
     def timed(name, *a):
         r = orig(name, *a)
-        if name in skip or (args.filter and args.filter not in name):
+        if name in skip or (args.filter and not any(f in name for f in args.filter.split(","))):
             return r
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         orig(name, *a)  # warm

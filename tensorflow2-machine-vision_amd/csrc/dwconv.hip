@@ -1295,7 +1295,21 @@ static int launch_dws(DwArgs g, hipStream_t s) {
   for (int i = 0; i < g.pout.nseg; ++i) ohmax = std::max(ohmax, g.pout.H[i]);
   DwsPlan pl{};
   long total = 0;
-  // rows per block: the most that still leaves >= DWS_BLOCKS blocks, at least 2
+  // block target per shape (kbench sweep 512 / 1024 / 2048 over the D0 step): half the blocks
+  // (longer strips) for the 32 x 32 layers and the BiFPN C = 64 filter gradients (32768 x 64
+  // wgrad: 18.1 -> 12.8 us, 32768 x 672 k5 fwd: 57.8 -> 52.8 us), twice for the 128 x 128 k3
+  // forward (148.6 -> 136.0 us)
+  long rows_in = 0;
+  for (int i = 0; i < g.pin.nseg; ++i) rows_in += (long)g.pin.batch * g.pin.H[i] * g.pin.W[i];
+  int target = DWS_BLOCKS;
+  if (WG) {
+    if (g.C <= 64 || rows_in <= 32768) target = DWS_BLOCKS / 2;
+  } else {
+    if (rows_in <= 32768 && g.C >= 256) target = DWS_BLOCKS / 2;
+    else if (K == 3 && S == 1 && rows_in >= 524288) target = 2 * DWS_BLOCKS;
+  }
+  if (dev_knob(6) > 0) target = dev_knob(6);
+  // rows per block: the most that still leaves >= target blocks, at least 2
   for (int TH = 256; TH >= 2; TH /= 2) {
     if (TH > 2 * ohmax && TH > 2) continue;
     total = 0;
@@ -1306,7 +1320,7 @@ static int launch_dws(DwArgs g, hipStream_t s) {
       total += pl.nblk[i];
     }
     pl.TH = TH;
-    if (total >= DWS_BLOCKS) break;
+    if (total >= target) break;
   }
   if (total == 0) return EDET_OK;
   EDET_REQUIRE(total < (1L << 31), "dwconv: grid too large");

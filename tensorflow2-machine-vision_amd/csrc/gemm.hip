@@ -1700,8 +1700,14 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
 template <typename T, bool LAZY, int NF, int KS>
 static int launch_gemm_s(const GemmArgs& g, hipStream_t s) {
   const int ngroups = (g.M + 15) / 16;
-  // 512 blocks (2 per CU): measured best over 512..2048 in the D0 step (scripts/kbench.py)
-  const int grid = std::max(1, std::min(cdiv(ngroups, 4), 512));
+  // 512 blocks (2 per CU): measured best over 512..2048 in the D0 step; 256 for the BiFPN /
+  // head 64 -> 64 convs with statistics (fewer blocks flushing the same channels: 32768 rows
+  // 17.4 -> 12.1 us), 1024 over 2M rows (2M x 32 -> 16: 50.1 -> 41.9 us) (scripts/kbench.py)
+  int cap = 512;
+  if (g.has_stats && g.N <= 64 && g.K >= 64 && g.M <= 262144) cap = 256;
+  else if (g.M >= (1 << 21)) cap = 1024;
+  if (dev_knob(7) > 0) cap = dev_knob(7);
+  const int grid = std::max(1, std::min(cdiv(ngroups, 4), cap));
   EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY>), dim3(grid), dim3(256), 0, s, g);
   return check_launch("edet gemm_s");
 }
