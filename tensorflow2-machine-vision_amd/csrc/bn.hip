@@ -769,11 +769,13 @@ int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, i
   // four rows per trip: 256 / 384 / 512 / 768 / 1024 / 2048 -> 1.49 / 1.45 / 1.43 / 1.51 /
   // 1.51 / 1.52 ms/step)
   // (scripts/row_probe.py: -20..-30 % on the C >= 240 and C = 16 layers, equal elsewhere).
-  g.geo = row_geom(C, 16);
+  // 32 passes for the wide layers (kbench sweep, round 2: 524288 x 144 60 -> 52 us, 32768 x 480
+  // 24 -> 21 us)
+  g.geo = row_geom(C, dev_knob(10) > 0 ? dev_knob(10) : (C >= 144 && p->nseg == 1 ? 32 : 16));
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 2 * C * sizeof(float2) + 2 * (size_t)g.geo.R * C * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    constexpr int rcap = 512;  // persistent blocks (r01h sweep: 1.51 -> 1.43 ms/step against 1024)
+    const int rcap = dev_knob(11) > 0 ? dev_knob(11) : 512;  // persistent blocks (r01h sweep: 1.51 -> 1.43 ms/step against 1024)
     const int grid = nb < rcap ? nb : rcap;
     const int f = (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0);
     if (nb) launch_reduce<T>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
@@ -795,11 +797,13 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
   if (acc) g.acc = *acc;
   if (grads && x->bn.enabled) { g.grads = *grads; g.has_grads = 1; }
   g.dsq = dsq; g.C = C; g.accumulate = accumulate;
-  g.geo = row_geom(C, 4);  // short chunks (persistent grid): 2.25 -> 2.21 ms/step against 8-16 passes
+  // short chunks (persistent grid): 2.25 -> 2.21 ms/step against 8-16 passes; 8 from C = 480 up
+  // (fewer, longer-lived blocks: M = 8192, C = 1152: 25 -> 21 us; kbench sweep, round 2)
+  g.geo = row_geom(C, dev_knob(8) > 0 ? dev_knob(8) : (C >= 480 ? 8 : 4));
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 3 * C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    constexpr int gcap = 2048;  // resident blocks per launch
+    const int gcap = dev_knob(9) > 0 ? dev_knob(9) : 2048;  // resident blocks per launch
     const int grid = nb > gcap ? gcap : nb;
     const int f = (x->bn.enabled ? AF_BN : 0) | (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0);
     if (nb) launch_apply<T>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
@@ -848,8 +852,8 @@ int edet_gate_bn_reduce(int dtype, const edet_lazy* x, int B, int HW, int C, con
   g.p.nseg = 1; g.p.batch = B; g.p.row_off[0] = 0; g.p.H[0] = HW; g.p.W[0] = 1;
   g.dv = dv; g.out64 = sums5; g.C = C; g.hw = HW;
   // long chunks: every block ends in 5C fp64 atomics (0.69 -> 0.54 ms/step at 16 passes vs ~8;
-  // 32 passes: 0.58)
-  g.geo = row_geom(C, 16);
+  // 32 passes: 0.58 in round 1, 0.45 against 0.48 in the round-2 sweep after the table hoists)
+  g.geo = row_geom(C, dev_knob(12) > 0 ? dev_knob(12) : 32);
   g.chunks_per_img = cdiv(HW, g.geo.CH);
   const int nb = B * g.chunks_per_img;
   const size_t lds = 2 * C * sizeof(float2) + (size_t)g.geo.R * C * sizeof(float);
@@ -932,7 +936,8 @@ int edet_lazy_materialize(int dtype, const edet_lazy* x, const edet_pyramid* p, 
   EDET_REQUIRE(out, "lazy_materialize: null out");
   LArgs g{};
   g.lz = *x; g.p = *p; g.dx = out; g.C = C;
-  g.geo = row_geom(C, 4);  // 0.60 -> 0.56 ms/step against ~8 passes
+  // 0.60 -> 0.56 ms/step against ~8 passes; 8 for C >= 1024 (M = 8192, C = 1152: 15 -> 13 us)
+  g.geo = row_geom(C, dev_knob(13) > 0 ? dev_knob(13) : (C >= 1024 ? 8 : 4));
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {
