@@ -952,7 +952,14 @@ static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s) {
     const int pt = same_pad(g.pin.H[i], K, S), pl = same_pad(g.pin.W[i], K, S);
     patches += (long)g.pin.batch * cdiv(g.pin.H[i] + pt, 2) * cdiv(g.pin.W[i] + pl, 2);
   }
-  const int grid = (int)std::max<long>(1, std::min<long>(4096, (patches + geo.R - 1) / geo.R));
+  // block cap (kbench sweep, round 2): 4096 for k3; the k5 patches carry 4x the work, fewer
+  // blocks won there (8192 x 1152: 46.8 -> 40.5 us at 1024, 32768 x 480: 51.5 -> 43.2 at 2048)
+  int cap = 4096;
+  long rows_in = 0;
+  for (int i = 0; i < g.pin.nseg; ++i) rows_in += (long)g.pin.batch * g.pin.H[i] * g.pin.W[i];
+  if (K == 5) cap = rows_in <= 8192 ? 1024 : 2048;
+  if (dev_knob(14) > 0) cap = dev_knob(14);
+  const int grid = (int)std::max<long>(1, std::min<long>(cap, (patches + geo.R - 1) / geo.R));
   if (patches) EDET_LAUNCH((k_dw4_dgrad<T, K, S, CPT, 2, 2>), dim3(grid, ncs), dim3(geo.TPR * geo.R), 0, s, g, geo);
   return check_launch("edet dwconv dgrad");
 }
