@@ -140,7 +140,7 @@ int edet_wall_clock_khz(int* khz);
  * comma-separated base names (e.g. "k_wgrad_tr,k_sum_partials") into buf; returns the number
  * of launches (not a status). */
 int edet_launched_kernels(char* buf, size_t size);
-/* development: A/B slots 0..15 read by some launchers' plan choices (0 = the production plan).
+/* development: A/B slots 0..31 read by some launchers' plan choices (0 = the production plan).
  * For probe scripts only; the model never sets them.  Returns the previous value. */
 int edet_dev_set(int slot, int value);
 

@@ -71,7 +71,7 @@ def main():
     model.train_step((x, t))
     torch.cuda.synchronize()
     L.call = orig
-    for i in range(16):
+    for i in range(32):
         L.lib().fns["edet_dev_set"](i, 0)
 
     rows, agg = [], {}

@@ -1500,6 +1500,9 @@ static int dispatch_pwb(const GemmArgs& g, hipStream_t s, bool& done) {
   const int KP = cdiv(g.K, 32) * 32;
   const bool lazy_in = LAZY;
   if (ks || !(lazy_in ? (g.N >= 192 && KP <= 96) : (g.N >= 128 && KP <= 192))) return EDET_OK;
+  // except the stage-6 expand dgrad (8192 x 192 -> 1152): the A-resident form is faster there
+  // (90 -> 63 us for its three calls, kbench round 2)
+  if (g.M <= 8192 && g.N >= 1024) return EDET_OK;
   done = true;
   if (!ks) return launch_pwb<T, 2, false, LAZY>(g, p, s);
   if (FN == 2) return launch_pwb<T, 2, true, LAZY>(g, p, s);

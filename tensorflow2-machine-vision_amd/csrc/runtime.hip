@@ -31,8 +31,8 @@ int check_launch(const char* what) {
   return EDET_OK;
 }
 
-static int g_dev[16] = {};
-int dev_knob(int slot) { return (slot >= 0 && slot < 16) ? g_dev[slot] : 0; }
+static int g_dev[32] = {};
+int dev_knob(int slot) { return (slot >= 0 && slot < 32) ? g_dev[slot] : 0; }
 
 // Caller-registered scratch for split reductions (weight gradients): blocks write partial
 // results with plain stores, one reduce kernel sums them in a fixed order.  The library still
@@ -120,7 +120,7 @@ int edet_launched_kernels(char* buf, size_t size) {
 }
 
 int edet_dev_set(int slot, int value) {
-  if (slot < 0 || slot >= 16) return 0;
+  if (slot < 0 || slot >= 32) return 0;
   const int old = edet::g_dev[slot];
   edet::g_dev[slot] = value;
   return old;
