@@ -1361,7 +1361,8 @@ enum DwForm { DW_TILE = 0, DW_DW3 = 1, DW_DIRECT = 2, DW_DW4 = 3, DW_ROWS = 4 };
 // block targets of the tile forms (kbench sweep 1024..8192: fwd 2048, wgrad 4096)
 constexpr int DW_GRID_FWD = 2048, DW_GRID_WGRAD = 4096;
 
-static DwForm dw_form(int which, int K, int S, int C, int nseg) {
+static DwForm dw_form_prod(int which, int K, int S, int C, int nseg);
+static DwForm dw_form(int which, int K, int S, int C, int nseg, long rows_in) {
   const bool direct_ok = C <= 2048;
   const bool dw4_ok = C % 8 == 0;  // channel rows split over blockIdx.y past 256 vectors
   if (which == 0) {
@@ -1372,6 +1373,11 @@ static DwForm dw_form(int which, int K, int S, int C, int nseg) {
     // the row-streaming form (k_dws_fwd) wins every k5 shape (1.0-1.37x) and the k3 shapes
     // below; the 8x8 tiles keep k3 s2 at C = 96 (256^2 input: 194 vs 214 us) and k3 s1 at
     // C >= 480 (even, or 23 vs 29 us at 16^2 x 1152)
+    // round-2 form sweep (kbench --dev): the 8x8 tiles for the C = 64 heads / BiFPN levels at
+    // 32x32 and the pyramid (209 -> 192 us for the 8 head calls), rows for k3 s1 at
+    // 32768 x 480 (63 -> 57 us)
+    if (K == 3 && S == 1 && C == 64 && (nseg > 1 || rows_in <= 32768)) return DW_TILE;
+    if (K == 3 && S == 1 && C == 480 && rows_in <= 32768) return DW_ROWS;
     if (C <= 2048 && (K == 5 || (S == 1 && C <= 144) || (S == 2 && C >= 192))) return DW_ROWS;
     if ((K == 3 && S == 2 && C >= 192) || (S == 1 && C == 240) || C > 2048) return DW_DW3;
     return DW_TILE;
@@ -1383,6 +1389,11 @@ static DwForm dw_form(int which, int K, int S, int C, int nseg) {
   // wgrad: the row-streaming form wins 1.1-1.5x on single tensors up to C = 672 except k3 s2 at
   // C = 96 (256^2 input); the BiFPN / head pyramids (C = 64, five levels) keep the pipelined
   // tiles (30.4 vs 33.2 us), C = 1152 the 8x8 tiles (21.4 vs 25.6 us at k3)
+  // round-2 sweep: the pipelined tiles for the small C = 64 BiFPN levels (8192 rows: 66 -> 48 us
+  // over 6 calls), rows for the C = 64 pyramid (231 -> 223) and the k5 C = 1152 layers (96 -> 80)
+  if (S == 1 && C == 64 && nseg == 1 && rows_in <= 8192) return DW_DW3;
+  if (S == 1 && C == 64 && nseg > 1) return DW_ROWS;
+  if (K == 5 && S == 1 && C == 1152) return DW_ROWS;
   if (nseg == 1 && C <= 672 && (K == 5 || S == 1 || C >= 192)) return DW_ROWS;
   return (S == 1 && (C <= 64 || (K == 5 && C == 240))) ? DW_DW3 : DW_TILE;
 }
@@ -1390,7 +1401,9 @@ static DwForm dw_form(int which, int K, int S, int C, int nseg) {
 template <typename T, int K, int S>
 static int launch_dw(int which, DwArgs g, hipStream_t s) {
   g.ncb = cdiv(g.C, DCB);
-  const DwForm form = dw_form(which, K, S, g.C, g.pin.nseg);
+  long rows_in = 0;
+  for (int i = 0; i < g.pin.nseg; ++i) rows_in += (long)g.pin.batch * g.pin.H[i] * g.pin.W[i];
+  const DwForm form = dw_form(which, K, S, g.C, g.pin.nseg, rows_in);
   if (which == 0) {
     if (form == DW_ROWS) return dispatch_dws<T, K, S, false>(g, s);
     if (form == DW_DW3) return launch_dw3<T, K, S, false>(g, s);

@@ -130,7 +130,12 @@ def dw_ref(v, pyr_in, k, s, w):  # v: fp64 [rows, C] values; returns [rows_out, 
 @pytest.mark.parametrize("k,s,H,W,C,lazy,nseg", [(3, 1, 16, 16, 32, 0, 1), (3, 2, 17, 13, 96, 1, 1),
                                                  (5, 2, 20, 9, 144, 1, 1), (5, 1, 11, 12, 40, 2, 1),
                                                  (3, 1, 9, 9, 64, 3, 2), (3, 1, 6, 7, 2112, 1, 1),
-                                                 (5, 2, 9, 8, 2112, 1, 1)])
+                                                 (5, 2, 9, 8, 2112, 1, 1),
+                                                 # forms chosen per shape in round 2 (dw_form):
+                                                 # k5 C = 1152 rows wgrad, k3 C = 480 rows fwd,
+                                                 # C = 64 tiles fwd / pipelined-tile wgrad
+                                                 (5, 1, 10, 11, 1152, 1, 1), (3, 1, 8, 9, 480, 1, 1),
+                                                 (3, 1, 12, 10, 64, 1, 1)])
 def test_dwconv_fwd_bwd(dt, k, s, H, W, C, lazy, nseg, workspace_mode):
     rng = np.random.default_rng(k * 100 + s * 10 + H)
     B = 2
