@@ -118,16 +118,23 @@ def test_keras_layout_roundtrip():
     assert kr["efficientnet-b0/blocks_0/se/conv2d/kernel:0"].shape == (1, 1, 32, 8)
     assert kr["class_net/class-predict/pointwise_kernel:0"].shape == (1, 1, 64, 45)
     assert kr["efficientnet-b0/stem/conv2d/kernel:0"].shape == (3, 3, 3, 32)
-    assert kr["fpn_cell_0/node_0/WSM:0"].shape == (2,)
+    assert kr["bi_fpn/bi_fpn_node/WSM_0:0"].shape == ()  # scalars (bifpn.py:45-54)
     # the transposition really moves elements (not a reshape)
     w = sd["efficientnet-b0/blocks_0/conv2d/kernel"]
     assert kr["efficientnet-b0/blocks_0/conv2d/kernel:0"][0, 0, 3, 5] == w[5, 3]
     d = sd["efficientnet-b0/blocks_0/depthwise_conv2d/depthwise_kernel"]
     assert kr["efficientnet-b0/blocks_0/depthwise_conv2d/depthwise_kernel:0"][1, 2, 7, 0] == d[1 * 3 + 2, 7]
-    back = {CK.product_name(k): CK.from_keras(CK.product_name(k), v, sd[CK.product_name(k)].shape) for k, v in kr.items()}
-    assert back.keys() == sd.keys()
+    class _M:
+        def state_dict(self):
+            return {k: np.zeros_like(v) for k, v in sd.items()}
+
+        def load_state_dict(self, d):
+            self.d = d
+    m = _M()
+    CK.load_keras_state_dict(m, kr, strict=True)
+    assert m.d.keys() == sd.keys()
     for k in sd:
-        np.testing.assert_array_equal(back[k], sd[k])
+        np.testing.assert_array_equal(m.d[k], sd[k])
 
 
 def test_load_keras_state_dict_strictness():
