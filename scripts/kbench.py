@@ -66,13 +66,16 @@ def main():
 
     for kv in filter(None, args.dev.split(",")):
         k, v = kv.split("=")
-        L.lib().fns["edet_dev_set"](int(k), int(v))
+        if L.lib().fns["edet_dev_set"](int(k), int(v)) < 0:
+            raise SystemExit("--dev needs the EDET_DEV build: make -C tensorflow2-machine-vision_amd dev; "
+                             "EDET_LIB=tensorflow2-machine-vision_amd/lib/libedet_dev.so")
     L.call = timed  # every package module calls through this one _lib module object
     model.train_step((x, t))
     torch.cuda.synchronize()
     L.call = orig
-    for i in range(32):
-        L.lib().fns["edet_dev_set"](i, 0)
+    if args.dev:
+        for i in range(32):
+            L.lib().fns["edet_dev_set"](i, 0)
 
     rows, agg = [], {}
     for name, s, e, b, tag in rec:

@@ -20,10 +20,7 @@ namespace edet {
 constexpr int RVPT = 2;  // vectors per thread (C <= 4096)
 // rows per trip in the streaming row loops: both rows' loads are issued before either is
 // consumed (in apply, before either store: vmcnt orders loads behind earlier stores)
-#ifndef EDET_APPLY_EU
-#define EDET_APPLY_EU 2
-#endif
-constexpr int EU = EDET_APPLY_EU;
+constexpr int EU = 2;
 // the reduce-type row kernels (BN-backward reduce, SE squeeze, SE-fused BN reduce) and the
 // materialize pass take four rows per trip (reduce 1.59 -> 1.51, materialize 0.61 -> 0.58
 // ms/step); apply is unchanged at four.  The SE-fused reduce was slower at four with ~8-pass

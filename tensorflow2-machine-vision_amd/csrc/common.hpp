@@ -21,8 +21,14 @@ void note_kernel(const char* site);
     ::edet::note_kernel(#K);                \
     hipLaunchKernelGGL(K, __VA_ARGS__);     \
   } while (0)
-// development A/B slots (edet_dev_set); 0 everywhere in production
+// Development A/B slots (edet_dev_set): plan overrides for scripts/kbench.py --dev, compiled
+// only into the EDET_DEV build (`make dev` -> lib/libedet_dev.so).  The production library
+// folds every slot to 0 (the measured plans) and its edet_dev_set returns EDET_EUNSUPPORTED.
+#ifdef EDET_DEV
 int dev_knob(int slot);
+#else
+constexpr int dev_knob(int) { return 0; }
+#endif
 // registered scratch (edet_set_workspace) if it holds n floats, else nullptr
 float* workspace_f32(size_t n_floats);
 // out[i] += sum_s part[s*n + i], fixed order

@@ -1139,9 +1139,6 @@ static WgsShape pick_wgs(int N, int K, bool wide) {
 // Output: each wave stages its 32 x 16*FN accumulator tile in a private LDS patch and writes
 // it back as 16-byte row vectors (no block barrier).  BN statistics: per-block fp32 partials
 // in LDS with one owner lane each, flushed as fp64 atomics once per segment.
-#ifndef EDET_PW_ABL
-#define EDET_PW_ABL 0
-#endif
 struct PwPlan {
   int R, KC, KP, nkc, NG, ngroups, nrg, LDA, LDB, nsub, NGtot;
 };
@@ -1209,11 +1206,7 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
       const int r = v / KV, kv = (v - r * KV) * 8;
       const int grow = rbase + r, gk = kc * p.KC + kv;
       const bool live = v < nvec && grow < M && gk < K;
-#if EDET_PW_ABL == 3
-      if (false) {
-#else
       if (live) {
-#endif
         const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + gk);
 #pragma unroll
         for (int ww = 0; ww < VW; ++ww) ra[u][ww] = src[ww];
@@ -1262,9 +1255,6 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
 
   // ---- MFMA over k in [0, kn) of A rows (a_row0 ..) x B rows (b_row0 ..) at B column kb0
   auto mma = [&](floatx4 (&acc)[2][FN], const T* Ab, int a_row0, int b_row0, int kb0, int kn) {
-#if EDET_PW_ABL == 2
-    return;
-#endif
     const T* ap = Ab + (size_t)(a_row0 + wm * 32 + (lane & 15)) * p.LDA;
     const T* bp = Bs + (size_t)(b_row0 + wn * 16 * FN + (lane & 15)) * p.LDB + kb0;
     for (int ks = 0; ks < kn; ks += 32) {
@@ -1335,11 +1325,7 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
     for (int e = lane; e < 32 * VPR; e += 64) {
       const int rr = e / VPR, cv = (e - rr * VPR) * 8;
       const int grow = wrow0 + rr, gcol = col_base + wcl0 + cv;
-#if EDET_PW_ABL == 1
-      if (grow < 0) {
-#else
       if (grow < M && gcol < N) {
-#endif
         float vals[8];
         const T* src = cw + rr * CWLD + cv;
 #pragma unroll
@@ -1519,10 +1505,7 @@ static int dispatch_pwb(const GemmArgs& g, hipStream_t s, bool& done) {
 // With A as the B operand each lane holds 4 consecutive output channels of one row: 8-byte
 // stores, whole rows written by one wave back to back.  BN statistics stay in registers per
 // lane until the end (one lane tree, one LDS pass and one fp64 atomic per channel per block).
-#ifndef EDET_GS_PF
-#define EDET_GS_PF 2
-#endif
-constexpr int GS_PF = EDET_GS_PF;  // row groups in flight ahead of the one being computed
+constexpr int GS_PF = 2;  // row groups in flight ahead of the one being computed
 template <typename T, int NF, int KS, bool LAZY>
 __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   // BN statistics: per wave and segment (a wave's groups ascend, so it meets each segment
@@ -1823,13 +1806,11 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
     const int rc = dispatch_gemm_s<T, LAZY>(g, s, done);
     if (done || rc) return rc;
   }
-#ifndef EDET_NO_PWB
   {
     bool done = false;
     const int rc = dispatch_pwb<T, LAZY>(g, s, done);
     if (done || rc) return rc;
   }
-#endif
   // A-resident kernel whenever its LDS image fits (<= 96 KB: >= 1 block per CU with room);
   // BM = rows per block chosen as the largest that fits.  Otherwise stream K (N <= 320).
   const int KP = cdiv(g.K, 32) * 32;

@@ -1,4 +1,5 @@
 // Library-level entry points: error reporting, ABI version, async memset.
+#include <limits.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include "common.hpp"
@@ -12,7 +13,7 @@ static thread_local const char* g_launched[8];
 static thread_local int g_nlaunched = 0;
 void note_kernel(const char* site) {
   if (g_nlaunched < 8) g_launched[g_nlaunched] = site;
-  ++g_nlaunched;
+  if (g_nlaunched < INT_MAX) ++g_nlaunched;  // saturates when never queried (long eager runs)
 }
 
 void set_error(const char* fmt, ...) {
@@ -31,8 +32,10 @@ int check_launch(const char* what) {
   return EDET_OK;
 }
 
+#ifdef EDET_DEV
 static int g_dev[32] = {};
 int dev_knob(int slot) { return (slot >= 0 && slot < 32) ? g_dev[slot] : 0; }
+#endif
 
 // Caller-registered scratch for split reductions (weight gradients): blocks write partial
 // results with plain stores, one reduce kernel sums them in a fixed order.  The library still
@@ -120,10 +123,17 @@ int edet_launched_kernels(char* buf, size_t size) {
 }
 
 int edet_dev_set(int slot, int value) {
+#ifdef EDET_DEV
   if (slot < 0 || slot >= 32) return 0;
   const int old = edet::g_dev[slot];
   edet::g_dev[slot] = value;
   return old;
+#else
+  (void)slot;
+  (void)value;
+  edet::set_error("edet_dev_set: development slots exist only in the EDET_DEV build (make dev)");
+  return EDET_EUNSUPPORTED;
+#endif
 }
 
 int edet_set_workspace(void* ptr, size_t bytes) {

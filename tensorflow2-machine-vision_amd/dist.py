@@ -118,10 +118,18 @@ def graphed_train_step(model, data, allreduce: Optional[Callable[[torch.Tensor],
     (targets, this replica's N+) | compute (forward, fused loss, backward) | optimizer -- with
     the N+ all-reduce and the flat gradient all-reduce issued between them on the same
     stream, so the collectives stay outside the captured work (RCCL/gloo calls are not
-    captured).  ``data``'s tensors must stay alive and in place while the graphs are used."""
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
+    captured).  ``data``'s tensors must stay alive and in place while the graphs are used.
+
+    The model must have run one eager step on ``data``'s shapes first: persistent buffers
+    (drop-connect masks, split-reduction workspaces, the engine's activation arena) are
+    allocated on first use, and an allocation inside capture would be baked into the graph
+    from the capture pool.  Capture runs on torch.cuda.graph's own side stream."""
+    if getattr(model, "steps_run", 0) < 1:
+        raise RuntimeError("graphed_train_step: run one eager model.train_step(data) first (warm-up)")
     if allreduce is None:
+        # the single graph captures model.train_step, which would call the hooks inside capture
+        if model.grad_allreduce is not None or model.npos_allreduce is not None:
+            raise ValueError("graphed_train_step: the model has all-reduce hooks but allreduce is None")
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             model.train_step(data)

@@ -465,6 +465,7 @@ class EfficientDetNetTrain(EfficientDetNet):
         sc.fixed_lr = s.get("fixed_lr", 0.0)
         self.sched = sc
         self.drop_masks = None
+        self.steps_run = 0  # compute_step calls (graphed_train_step needs one eager warm-up)
         self.fixed_masks = None  # test hook: {'class_net': [rep-1, nseg, B], 'box_net': ...}
 
     # ------------------------------------------------------------------ data
@@ -539,6 +540,7 @@ class EfficientDetNetTrain(EfficientDetNet):
         eng.tape.backward()
         eng.tape = None
         eng.training = False
+        self.steps_run += 1
         return t
 
     def forward_backward(self, data):
