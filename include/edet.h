@@ -199,6 +199,17 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
                         const edet_bngrad64* acc, const edet_segout* grads, void* dx,
                         int accumulate, edet_stream_t stream);
 
+/* ---- fused depthwise backward, stride 1: one pass over dy and x gives
+ *   dx (= edet_dwconv_dgrad, `accumulate` as there), dw += (= edet_dwconv_wgrad), and, when
+ *   `fold` is non-NULL, x's BN-backward sums fold->dbeta[s] += sum du,
+ *   fold->dgamma[s] += sum du * xhat with du = dx * act'(bn(x)) (= edet_lazy_bwd_reduce with
+ *   dv = dx, no dv_scale / dsq; needs accumulate == 0, no gate on x and x->bn enabled).
+ *   stride != 1 returns EDET_EUNSUPPORTED. */
+int edet_dwconv_bwd(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
+                    int stride, const void* dy, const edet_pyramid* pout, const void* w,
+                    void* dx, int accumulate, float* dw, const edet_bngrad64* fold,
+                    edet_stream_t stream);
+
 /* ---- squeeze-excitation ---- */
 /* s += mean_hw v(x) into a zeroed fp64 [B][C] (fp64 cross-block sums: the squeeze feeds the
  * forward, so it is kept reproducible like the BN statistics) */

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
   __shared__ float gt[DCB];
   __shared__ float red[2][8][DCB];
   const int tid = threadIdx.x, c = tid & 31, r = tid >> 5;
-  const int w = blockIdx.x;
+  const int w = xcd_remap(blockIdx.x, gridDim.x);  // a pixel's channel blocks on one XCD
   const int cb = w % g.ncb, G = gridDim.x / g.ncb;
   const int c0 = cb * DCB;
   const bool cvalid = (c0 + c) < g.C;
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void k_dw_dgrad(DwArgs g) {
   __shared__ __attribute__((aligned(16))) float tile[HR * HR * DCB];
   const int tid = threadIdx.x, c = tid & 31, r = tid >> 5;
 
-  int id = blockIdx.x;
+  int id = xcd_remap(blockIdx.x, gridDim.x);
   const int cb = id % g.ncb;
   id /= g.ncb;
   int seg, n, ty, tx;
@@ -336,8 +336,9 @@ __global__ __launch_bounds__(256) void k_dw_wgrad(DwArgs g) {
   __shared__ float gt[DCB];
   const int tid = threadIdx.x, c = tid & 31, r = tid >> 5;
 
-  const int cb = blockIdx.x % g.ncb;
-  const int chunk = blockIdx.x / g.ncb;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int cb = bid % g.ncb;
+  const int chunk = bid / g.ncb;
   const int c0 = cb * DCB;
   const bool cvalid = (c0 + c) < g.C;
   const int t_begin = chunk * g.tiles_per_wg;
@@ -429,7 +430,7 @@ __global__ __launch_bounds__(256) void k_dw3(DwArgs g) {
   __shared__ float2 xf[DCB];
   __shared__ float red[2][8][DCB];
   const int tid = threadIdx.x, c = tid & 31, r = tid >> 5;
-  const int w = blockIdx.x;
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
   const int cb = w % g.ncb, G = gridDim.x / g.ncb;
   const int c0 = cb * DCB;
   const int C = g.C;
@@ -690,11 +691,13 @@ __global__ __launch_bounds__(256) void k_dw3(DwArgs g) {
 // segment.  No LDS staging, no barriers inside the pixel loop.
 struct DwGeom {
   int TPR, R;  // threads per pixel (C/8), pixels per block pass
+  int ncs;     // k_dw4_dgrad: channel splits per pixel (consecutive blocks)
 };
 static DwGeom dw_geom(int C) {
   DwGeom d;
   d.TPR = C / 8;
   d.R = std::max(1, 256 / d.TPR);
+  d.ncs = 1;
   return d;
 }
 
@@ -862,7 +865,10 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo) {
   constexpr int DLO = -((K - 1) / S), DHR = (PH - 1) / S, DHC = (PW - 1) / S;
   const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
   if (rr >= geo.R) return;
-  const int c = (blockIdx.y * geo.TPR + tv) * CPT, C = g.C;  // channel blocks over blockIdx.y
+  // channel splits innermost (geo.ncs consecutive logical blocks = one XCD, the same pixels)
+  const int bx = xcd_remap(blockIdx.x, gridDim.x), cs = bx % geo.ncs, pb = bx / geo.ncs;
+  const int pgrid = gridDim.x / geo.ncs;
+  const int c = (cs * geo.TPR + tv) * CPT, C = g.C;
   const T* DY = (const T*)g.dy;
   T* DX = (T*)g.dx;
   float w[K * K][CPT];
@@ -873,7 +879,7 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo) {
     const int pt = same_pad(H, K, S), pl = same_pad(W, K, S);
     const int PR = cdiv(H + pt, PH), PC = cdiv(W + pl, PW), per_img = PR * PC;
     const int npatch = g.pin.batch * per_img;
-    for (int q = blockIdx.x * geo.R + rr; q < npatch; q += gridDim.x * geo.R) {
+    for (int q = pb * geo.R + rr; q < npatch; q += pgrid * geo.R) {
       const int n = q / per_img, rem = q - n * per_img;
       const int pr = rem / PC, pc = rem - pr * PC;
       const int A = pr * (PH / S), Bc = pc * (PW / S);
@@ -947,6 +953,7 @@ static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s) {
   while (g.C / CPT / ncs > 256 || (g.C / CPT) % ncs) ++ncs;
   geo.TPR = g.C / CPT / ncs;
   geo.R = std::max(1, 256 / geo.TPR);
+  geo.ncs = ncs;
   long patches = 0;
   for (int i = 0; i < g.pin.nseg; ++i) {
     const int pt = same_pad(g.pin.H[i], K, S), pl = same_pad(g.pin.W[i], K, S);
@@ -960,7 +967,7 @@ static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s) {
   if (K == 5) cap = rows_in <= 8192 ? 1024 : 2048;
   if (dev_knob(14) > 0) cap = dev_knob(14);
   const int grid = (int)std::max<long>(1, std::min<long>(cap, (patches + geo.R - 1) / geo.R));
-  if (patches) EDET_LAUNCH((k_dw4_dgrad<T, K, S, CPT, 2, 2>), dim3(grid, ncs), dim3(geo.TPR * geo.R), 0, s, g, geo);
+  if (patches) EDET_LAUNCH((k_dw4_dgrad<T, K, S, CPT, 2, 2>), dim3(grid * ncs), dim3(geo.TPR * geo.R), 0, s, g, geo);
   return check_launch("edet dwconv dgrad");
 }
 
@@ -996,6 +1003,7 @@ struct DwsPlan {
   int strips[EDET_MAX_SEG];    // column strips per segment
   int rowblk[EDET_MAX_SEG];    // row blocks per segment
   int nblk[EDET_MAX_SEG];      // blocks per segment (ncb * batch * rowblk * strips)
+  int cb_inner;                // channel block innermost in the block order (see k_dws)
 };
 
 template <int N, int WORDS>
@@ -1025,14 +1033,23 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
   __shared__ float gt[DCB];
   const int tid = threadIdx.x, c = tid & 31, gc = tid >> 5;
 
-  // ---- block -> (seg, cb, n, row block, strip); consecutive logical ids share an XCD
+  // ---- block -> (seg, cb, n, row block, strip); consecutive logical ids share an XCD.
+  // A block reads 32 channels = 64 B of each pixel, half of a 128-B line when C >= 64; with
+  // the channel block innermost the blocks reading the other parts of the same lines are
+  // consecutive logical ids, i.e. the same XCD (L2) at about the same time.
   int id = xcd_remap(blockIdx.x, gridDim.x), seg = 0;
   while (seg < g.pout.nseg - 1 && id >= pl.nblk[seg]) id -= pl.nblk[seg++];
+  int cb = 0;
+  if (pl.cb_inner) {
+    cb = id % g.ncb;
+    id /= g.ncb;
+  }
   const int strip = id % pl.strips[seg];
   id /= pl.strips[seg];
   const int rb = id % pl.rowblk[seg];
   id /= pl.rowblk[seg];
-  const int n = id % g.pout.batch, cb = id / g.pout.batch;
+  const int n = id % g.pout.batch;
+  if (!pl.cb_inner) cb = id / g.pout.batch;
   const int c0 = cb * DCB, C = g.C;
   const int OH = g.pout.H[seg], OW = g.pout.W[seg], H = g.pin.H[seg], W = g.pin.W[seg];
   const int oy0 = rb * pl.TH, ox0 = strip * TW;
@@ -1330,6 +1347,7 @@ static int launch_dws(DwArgs g, hipStream_t s) {
     if (total >= target) break;
   }
   if (total == 0) return EDET_OK;
+  pl.cb_inner = dev_knob(15) != 2;
   EDET_REQUIRE(total < (1L << 31), "dwconv: grid too large");
   EDET_LAUNCH((k_dws<T, K, S, CPG, WG, P>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
   return check_launch("edet dwconv (rows)");
@@ -1350,6 +1368,299 @@ static int dispatch_dws(const DwArgs& g, hipStream_t s) {
   }
   if (owmax >= 16) return launch_dws<T, K, S, 2, WG, P>(g, s);
   return launch_dws<T, K, S, 1, WG, P>(g, s);
+}
+
+
+// ------------------------------------------------------------------ fused backward (stride 1)
+// One pass over dy and the lazy input x gives all three results of a stride-1 depthwise
+// layer's backward, which the separate entry points compute in three passes (the transposed
+// stencil and the filter gradient each read dy, and the BN-backward reduce of x's BatchNorm
+// reads dx and x again, layers/mb_conv_block.py:144-154):
+//   dx[r][c]   = sum_{kh,kw} dy[r+p-kh][c+p-kw] * w[kh][kw]              (p = (K-1)/2)
+//   dW[kh][kw] += sum_{r,c} dy[r][c] * v(x)[r-p+kh][c-p+kw]
+//   fold (optional): dbeta += sum du, dgamma += sum du * xhat with du = dx * act'(bn(x)):
+//     edet_lazy_bwd_reduce over (x, dv = dx) without its own pass over HBM.
+// Block = image x 32 channels x a strip of TW = 8*CPG columns x TH rows (channel block
+// innermost, as in k_dws).  At stride 1 both results of row r read the same K rows of dy and
+// v around r with the same column halo p, so the block walks down its rows keeping the last K
+// of each in an LDS ring (dy in storage precision, exact; v transformed once, fp32); the next
+// row is in flight in registers; one barrier per row.  Thread (c, gc) owns channel c and
+// columns gc*CPG..: dx leaves as direct stores, the filter-gradient taps and the fold sums stay
+// in registers until the block ends.
+template <typename T, int K, int CPG, bool FOLD>
+__global__ __launch_bounds__(256) void k_dwb(DwArgs g, DwsPlan pl, edet_bngrad64 fold) {
+  constexpr int P = (K - 1) / 2;
+  constexpr int TW = 8 * CPG, IWS = TW + K - 1;
+  constexpr int R = K + 1;                      // ring rows: the K in use + the one committed
+  constexpr int RV = IWS * (DCB / 8);           // 8-channel vectors per row and ring
+  constexpr int WORDS = sizeof(T) == 2 ? 1 : 2;
+  constexpr int WIN = CPG + K - 1;
+  constexpr int RINGF = R * IWS * DCB;                     // v ring (floats)
+  constexpr int RINGB = RINGF * 4 + R * IWS * DCB * (int)sizeof(T);  // + dy ring
+  constexpr int REDB = (K * K + 2) * 8 * DCB * 4;          // end-of-block reductions
+  constexpr int LDSB = RINGB > REDB ? RINGB : REDB;
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
+  float* vring = reinterpret_cast<float*>(smem);
+  T* dring = reinterpret_cast<T*>(smem + RINGF * 4);
+  __shared__ float2 xf[DCB];
+  __shared__ float gt[DCB];
+  const int tid = threadIdx.x, c = tid & 31, gc = tid >> 5;
+
+  int id = xcd_remap(blockIdx.x, gridDim.x), seg = 0;
+  while (seg < g.pout.nseg - 1 && id >= pl.nblk[seg]) id -= pl.nblk[seg++];
+  const int cb = id % g.ncb;
+  id /= g.ncb;
+  const int strip = id % pl.strips[seg];
+  id /= pl.strips[seg];
+  const int rb = id % pl.rowblk[seg];
+  const int n = id / pl.rowblk[seg];
+  const int c0 = cb * DCB, C = g.C;
+  const int H = g.pin.H[seg], W = g.pin.W[seg];  // = the output's (stride 1)
+  const int r0 = rb * pl.TH, x0 = strip * TW;
+  const int nrows = min(pl.TH, H - r0);
+  const T* X = (const T*)g.x + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * g.lz.ld + c0;
+  const T* DY = (const T*)g.dy + ((size_t)g.pout.row_off[seg] + (size_t)n * H * W) * C + c0;
+  T* DX = (T*)g.dx + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * C + c0;
+  const bool cvalid = c0 + c < C;
+
+  float wr[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(((const T*)g.w)[(size_t)i * C + c0 + c]) : 0.f;
+  const float inv = 1.f / (float)seg_rows(g.pin, seg);
+  if (tid < DCB) {
+    const int cc = c0 + tid;
+    xf[tid] = cc < C ? bn_affine(g.lz.bn, seg, cc, inv) : make_float2(1.f, 0.f);
+    gt[tid] = (g.lz.gate && cc < C) ? g.lz.gate[(size_t)n * C + cc] : 1.f;
+  }
+  // the fold's per-channel constants of this thread's channel
+  float2 myaf = make_float2(1.f, 0.f), mymr = make_float2(0.f, 1.f);
+  if constexpr (FOLD) {
+    if (cvalid) {
+      myaf = bn_affine(g.lz.bn, seg, c0 + c, inv);
+      mymr = bn_mean_rstd(g.lz.bn, seg, c0 + c, inv);
+    }
+  }
+
+  // ring row t <-> image row q = r0 - P + t.  Each row is RV dy vectors and RV x vectors; dy
+  // vector e of a fetch goes to thread e, x vector e to thread 255 - e (two uniform loops: one
+  // loop over both with a per-lane choice held both paths' registers, ~190 VGPRs at k5)
+  auto fetch = [&](auto& rg, auto& rx, int t0, int nt) {
+    constexpr int NV = std::remove_reference_t<decltype(rg)>::NV;
+    rg.ok = 0;
+    rx.ok = 0;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const int v = (side ? 255 - tid : tid) + u * 256;
+        const int row = v / RV, e = v - row * RV, xx = e >> 2, cv = (e & 3) * 8;
+        const int q = r0 - P + t0 + row, gx = x0 - P + xx;
+        const bool in = row < nt && q >= 0 && q < H && gx >= 0 && gx < W && c0 + cv < C;
+        const uint32_t pix = in ? (uint32_t)(q * W + gx) : 0u;
+        const uint4* src = reinterpret_cast<const uint4*>(side ? X + (size_t)pix * g.lz.ld + (in ? cv : 0)
+                                                               : DY + (size_t)pix * C + (in ? cv : 0));
+        auto& dst = side ? rx : rg;
+        dst.v[u][0] = src[0];
+        if constexpr (WORDS == 2) dst.v[u][1] = src[1];
+        dst.ok |= (uint32_t)in << u;
+      }
+    }
+  };
+  auto commit = [&](const auto& rg, const auto& rx, int t0, int nt) {
+    constexpr int NV = std::remove_reference_t<decltype(rg)>::NV;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {  // dy: copied as stored (zero outside the image)
+      const int v = tid + u * 256;
+      const int row = v / RV, e = v - row * RV, xx = e >> 2;
+      if (row >= nt) break;
+      const bool in = (rg.ok >> u) & 1;
+      T* d = dring + (((t0 + row) % R) * IWS + xx) * DCB + (e & 3) * 8;
+#pragma unroll
+      for (int w = 0; w < WORDS; ++w) reinterpret_cast<uint4*>(d)[w] = in ? rg.v[u][w] : make_uint4(0, 0, 0, 0);
+    }
+    const int cv0 = ((255 - tid) & 3) * 8;  // this thread's 8 x channels, the same for every u
+    float2 a8[8];
+    float g8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a8[j] = xf[cv0 + j]; g8[j] = gt[cv0 + j]; }
+    const int act = g.lz.act;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {  // x: transformed once (lazy BN / act / gate), fp32
+      const int v = 255 - tid + u * 256;
+      const int row = v / RV, e = v - row * RV, xx = e >> 2;
+      if (row >= nt) break;
+      float vals[8];
+      if constexpr (WORDS == 1) {
+        const uint32_t w4[4] = {rx.v[u][0].x, rx.v[u][0].y, rx.v[u][0].z, rx.v[u][0].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          vals[2 * i] = __uint_as_float(w4[i] << 16);
+          vals[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+        }
+      } else {
+        const uint32_t w8[8] = {rx.v[u][0].x, rx.v[u][0].y, rx.v[u][0].z, rx.v[u][0].w,
+                                rx.v[u][1].x, rx.v[u][1].y, rx.v[u][1].z, rx.v[u][1].w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vals[i] = __uint_as_float(w8[i]);
+      }
+      // transform unconditionally, zero the padding by a multiply (see k_dws commit)
+      const float m = ((rx.ok >> u) & 1) ? 1.f : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vals[j] = lazy_apply(vals[j], a8[j], act) * (g8[j] * m);
+      float* d = vring + (((t0 + row) % R) * IWS + xx) * DCB + cv0;
+      reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
+      reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+    }
+  };
+
+  constexpr int NVS = (RV + 255) / 256;  // per thread and side, one row
+  constexpr int NV2 = (2 * RV + 255) / 256;
+  DwRaw<NVS, WORDS> rs, rsx;
+  {
+    // prologue rows two at a time (all K-1 at once held ~20 more VGPRs for the whole kernel)
+    DwRaw<NV2, WORDS> rp, rpx;
+    fetch(rp, rpx, 0, K - 1 < 2 ? K - 1 : 2);
+    __syncthreads();  // xf / gt
+#pragma unroll
+    for (int t = 0; t < K - 1; t += 2) {
+      commit(rp, rpx, t, K - 1 - t < 2 ? K - 1 - t : 2);
+      if (t + 2 < K - 1) fetch(rp, rpx, t + 2, K - 1 - (t + 2) < 2 ? K - 1 - (t + 2) : 2);
+    }
+  }
+  fetch(rs, rsx, K - 1, 1);
+
+  float acc[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
+  float fs = 0.f, fq = 0.f;
+  const int act = g.lz.act;
+  for (int j = 0; j < nrows; ++j) {
+    const int r = r0 + j;
+    T xr[CPG];
+    if constexpr (FOLD) {  // x of this thread's dx elements (read K-1 rows ago: cache-hot)
+#pragma unroll
+      for (int i = 0; i < CPG; ++i) {
+        const int col = x0 + gc * CPG + i;
+        const bool ok = col < W && cvalid;
+        xr[i] = X[ok ? (size_t)(r * W + col) * g.lz.ld + c : 0];
+      }
+    }
+    commit(rs, rsx, j + K - 1, 1);
+    // unconditional refill (rows past the block are real or predicated-off elements)
+    fetch(rs, rsx, j + K, 1);
+    __syncthreads();
+
+    float dxv[CPG], dyc[CPG];
+#pragma unroll
+    for (int i = 0; i < CPG; ++i) {
+      dxv[i] = 0.f;
+      dyc[i] = to_f<T>(dring[(((j + P) % R) * IWS + gc * CPG + i + P) * DCB + c]);
+    }
+#pragma unroll
+    for (int rr = 0; rr < K; ++rr) {
+      const int slot = (j + rr) % R;
+      float dwin[WIN], vwin[WIN];
+#pragma unroll
+      for (int x = 0; x < WIN; ++x) {
+        dwin[x] = to_f<T>(dring[(slot * IWS + gc * CPG + x) * DCB + c]);
+        vwin[x] = vring[(slot * IWS + gc * CPG + x) * DCB + c];
+      }
+#pragma unroll
+      for (int kw = 0; kw < K; ++kw) {
+        const float wv = wr[(K - 1 - rr) * K + kw];
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < CPG; ++i) {
+          dxv[i] += dwin[i + 2 * P - kw] * wv;
+          a += dyc[i] * vwin[i + kw];
+        }
+        acc[rr * K + kw] += a;
+      }
+      // one ring row's windows live at a time (hoisting all K rows' LDS reads took the k5
+      // forms to ~190 VGPRs, 2 waves per SIMD)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = 0; i < CPG; ++i) {
+      const int col = x0 + gc * CPG + i;
+      if (col < W && cvalid) {
+        T* p = DX + (size_t)(r * W + col) * C + c;
+        *p = from_f<T>(g.accumulate ? to_f<T>(*p) + dxv[i] : dxv[i]);
+        if constexpr (FOLD) {
+          const float xv = to_f<T>(xr[i]);
+          const float du = act ? dxv[i] * dswishf_(xv * myaf.x + myaf.y) : dxv[i];
+          fs += du;
+          fq += du * ((xv - mymr.x) * mymr.y);
+        }
+      }
+    }
+  }
+  // block reductions over the 8 column groups: filter taps (+ fold sums), one atomic each
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) red[(i * 8 + gc) * DCB + c] = acc[i];
+  if constexpr (FOLD) {
+    red[(K * K * 8 + gc) * DCB + c] = fs;
+    red[((K * K + 1) * 8 + gc) * DCB + c] = fq;
+  }
+  __syncthreads();
+  constexpr int NOUT = (K * K + (FOLD ? 2 : 0)) * DCB;
+  for (int e = tid; e < NOUT; e += 256) {
+    const int i = e / DCB, cc = e - i * DCB;
+    if (c0 + cc >= C) continue;
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sum += red[(i * 8 + k) * DCB + cc];
+    if (i < K * K) atomicAdd(g.dw + (size_t)i * C + c0 + cc, sum);
+    else if constexpr (FOLD) stat_add((i == K * K ? fold.dbeta[seg] : fold.dgamma[seg]) + c0 + cc, (double)sum);
+  }
+}
+
+template <typename T, int K, int CPG, bool FOLD>
+static int launch_dwb(DwArgs g, const edet_bngrad64& fold, hipStream_t s) {
+  constexpr int TW = 8 * CPG;
+  int hmax = 0;
+  for (int i = 0; i < g.pin.nseg; ++i) hmax = std::max(hmax, g.pin.H[i]);
+  DwsPlan pl{};
+  pl.cb_inner = 1;
+  long total = 0;
+  int target = DWS_BLOCKS;
+  if (dev_knob(16) > 0) target = dev_knob(16);
+  for (int TH = 256; TH >= 2; TH /= 2) {
+    if (TH > 2 * hmax && TH > 2) continue;
+    total = 0;
+    for (int i = 0; i < g.pin.nseg; ++i) {
+      pl.strips[i] = cdiv(g.pin.W[i], TW);
+      pl.rowblk[i] = cdiv(g.pin.H[i], TH);
+      pl.nblk[i] = g.ncb * g.pin.batch * pl.rowblk[i] * pl.strips[i];
+      total += pl.nblk[i];
+    }
+    pl.TH = TH;
+    if (total >= target) break;
+  }
+  if (total == 0) return EDET_OK;
+  EDET_REQUIRE(total < (1L << 31), "dwconv_bwd: grid too large");
+  EDET_LAUNCH((k_dwb<T, K, CPG, FOLD>), dim3((unsigned)total), dim3(256), 0, s, g, pl, fold);
+  return check_launch("edet dwconv bwd");
+}
+
+template <typename T, int K, bool FOLD>
+static int dispatch_dwb_cpg(const DwArgs& g, const edet_bngrad64& fold, hipStream_t s) {
+  int wmax = 0;
+  for (int i = 0; i < g.pin.nseg; ++i) wmax = std::max(wmax, g.pin.W[i]);
+  if (wmax >= 32) return launch_dwb<T, K, 4, FOLD>(g, fold, s);
+  if (wmax >= 16) return launch_dwb<T, K, 2, FOLD>(g, fold, s);
+  return launch_dwb<T, K, 1, FOLD>(g, fold, s);
+}
+
+template <typename T>
+static int dispatch_dwb(int k, const DwArgs& g, const edet_bngrad64* fold, hipStream_t s) {
+  const edet_bngrad64 f = fold ? *fold : edet_bngrad64{};
+  if (k == 3) return fold ? dispatch_dwb_cpg<T, 3, true>(g, f, s) : dispatch_dwb_cpg<T, 3, false>(g, f, s);
+  if (k == 5) return fold ? dispatch_dwb_cpg<T, 5, true>(g, f, s) : dispatch_dwb_cpg<T, 5, false>(g, f, s);
+  set_error("dwconv_bwd: unsupported kernel %d", k);
+  return EDET_EUNSUPPORTED;
 }
 
 // Kernel forms: TILE = k_dw_fwd / k_dw_wgrad / k_dw_dgrad (8x8 LDS tiles), DW3 = k_dw3
@@ -1514,6 +1825,26 @@ int edet_dwconv_wgrad(int dtype, const edet_lazy* x, const edet_pyramid* pin, in
   DwArgs g{};
   g.x = x->x; g.dy = dy; g.dw = dw; g.lz = *x; g.pin = *pin; g.pout = *pout; g.C = C;
   EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_dw<T>(2, k, stride, g, (hipStream_t)stream); });
+}
+
+int edet_dwconv_bwd(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
+                    int stride, const void* dy, const edet_pyramid* pout, const void* w,
+                    void* dx, int accumulate, float* dw, const edet_bngrad64* fold,
+                    edet_stream_t stream) {
+  EDET_REQUIRE(x && dy && w && dx && dw, "dwconv_bwd: null argument");
+  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0, "dwconv_bwd: need C%%8==0 and ld%%8==0");
+  if (stride != 1) {
+    set_error("dwconv_bwd: stride %d (the fused backward is stride 1; use edet_dwconv_dgrad/wgrad)", stride);
+    return EDET_EUNSUPPORTED;
+  }
+  int rc = check_pyrs(pin, pout, k, stride);
+  if (rc) return rc;
+  EDET_REQUIRE(!fold || (!accumulate && x->gate == nullptr && x->bn.enabled),
+               "dwconv_bwd: the BN fold needs accumulate == 0, no gate and a BatchNorm on x");
+  DwArgs g{};
+  g.x = x->x; g.lz = *x; g.dy = dy; g.w = w; g.dx = dx; g.dw = dw; g.pin = *pin; g.pout = *pout;
+  g.C = C; g.accumulate = accumulate; g.ncb = cdiv(C, DCB);
+  EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_dwb<T>(k, g, fold, (hipStream_t)stream); });
 }
 
 }  // extern "C"

@@ -16,6 +16,7 @@ Reference call sites replaced (AIServer/ai_api/ai_models/...):
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 
@@ -60,10 +61,11 @@ def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor
             dgate = eng.zeros64(B, out.C)
             L.call("edet_gate_grad", eng.dt, lz, B, HW, out.C, vp(rec.t), vp(dgate), s)
     grads = acc = None
+    folded = rec.bn_sums is not None
     if out.bns is not None:
         grads = _bn_grads(out.bns)
         # fp64 dgamma/dbeta sums (edet_bngrad64): their order must not reach the rounding of dx
-        acc_t = eng.zeros64(2, len(out.bns), out.C)
+        acc_t = rec.bn_sums if folded else eng.zeros64(2, len(out.bns), out.C)
         acc = L.BnGrad64()
         for i in range(len(out.bns)):
             acc.dgamma[i], acc.dbeta[i] = acc_t[0, i].data_ptr(), acc_t[1, i].data_ptr()
@@ -76,7 +78,7 @@ def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor
             L.call("edet_se_bwd_bn", *args, vp(sums5), acc, s)
         else:
             L.call("edet_se_bwd", *args, s)
-    if out.bns is not None and not fused_se:
+    if out.bns is not None and not fused_se and not folded:
         L.call("edet_lazy_bwd_reduce", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, s)
     dx = eng.empty(out.pyr.rows, out.C)
     L.call("edet_lazy_bwd_apply", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, grads,
@@ -123,6 +125,7 @@ def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optio
             out_buf: Optional[torch.Tensor] = None, name: str = "") -> Act:
     """y = v(x) @ W^T (+ b); output is lazy BN/act when ``bns`` given.  W stored [N][K]."""
     K = x.C
+    x.consume()
     ldy = N if ldy is None else ldy
     y = out_buf if out_buf is not None else eng.empty(x.pyr.rows, ldy)
     bias = P.view(bname) if bname else None
@@ -155,9 +158,15 @@ def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optio
 
 
 # --------------------------------------------------------------------------- depthwise
+# stride-1 backward as one fused pass (edet_dwconv_bwd), with the BN-backward fold of the
+# input's BatchNorm when this op is the input's only consumer
+FUSED_DW_BWD = os.environ.get("EDET_FUSED_DW", "1") != "0"
+FOLD_DW_BN = os.environ.get("EDET_FOLD_DW_BN", "1") != "0"
+
 def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
            bns: Optional[List[BNParam]] = None, act: int = L.ACT_NONE, name: str = "") -> Act:
     C = x.C
+    x.consume()
     pout = x.pyr.strided(stride)
     y = eng.empty(pout.rows, C)
     L.call("edet_dwconv_fwd", eng.dt, x.lazy(), x.pyr.c, C, k, stride, vp(P.wcv(wname)), vp(y), pout.c,
@@ -170,6 +179,21 @@ def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
             return
         d, ld = value_grad_to_raw(eng, out, rec)
         assert ld == C
+        if stride == 1 and FUSED_DW_BWD and not eng.overlap:
+            # one pass over (d, x): dx, the filter gradient and, when this op owns x's whole
+            # gradient, x's BN-backward sums (the reduce pass of value_grad_to_raw is skipped)
+            dx, acc = eng.tape.dst(x)
+            fold = None
+            if (FOLD_DW_BN and acc == 0 and x.uses == 1 and x.bns is not None and x.gate is None
+                    and x.se is None):
+                sums = eng.zeros64(2, len(x.bns), C)
+                fold = L.BnGrad64()
+                for i in range(len(x.bns)):
+                    fold.dgamma[i], fold.dbeta[i] = sums[0, i].data_ptr(), sums[1, i].data_ptr()
+                eng.tape.g[x].bn_sums = sums
+            L.call("edet_dwconv_bwd", eng.dt, x.lazy(), x.pyr.c, C, k, stride, vp(d), pout.c, vp(P.wcv(wname)),
+                   vp(dx), acc, vp(P.grad(wname)), fold, stream())
+            return
         with eng.side(x.raw, x.gate, d):
             L.call("edet_dwconv_wgrad", eng.dt, x.lazy(), x.pyr.c, C, k, stride, vp(d), pout.c, vp(P.grad(wname)),
                    stream())
@@ -205,6 +229,7 @@ def materialize(eng: Engine, x: Act, name: str = "") -> Act:
     """Write v(x) once as a plain tensor (same bf16 rounding the GEMM A-operand staging
     applies, so the consumer's inputs are unchanged).  Backward: the gradient of the plain copy
     IS the gradient of x's value, handed to x's own backward as is."""
+    x.consume()
     y = eng.empty(x.pyr.rows, x.C)
     L.call("edet_lazy_materialize", eng.dt, x.lazy(), x.pyr.c, x.C, vp(y), stream())
     out = Act(y, x.pyr, x.C, training=eng.training, name=name)
@@ -222,6 +247,7 @@ def materialize(eng: Engine, x: Act, name: str = "") -> Act:
 # --------------------------------------------------------------------------- resampling
 def maxpool(eng: Engine, x: Act, name: str = "") -> Act:
     assert x.pyr.nseg == 1
+    x.consume()
     B, H, W, C = x.pyr.batch, x.pyr.H, x.pyr.W, x.C
     pout = x.pyr.strided(2)
     y = eng.empty(pout.rows, C)
@@ -254,6 +280,7 @@ def bifpn_fuse(eng: Engine, P: ParamStore, inputs: Sequence[Tuple[Act, int]], wn
             for (_, mode) in inputs]
     for i, (a, mode) in enumerate(inputs):
         assert a.pyr.nseg == 1 and a.C == C
+        a.consume()
         fi[i].v = a.lazy()
         fi[i].H, fi[i].W, fi[i].mode = a.pyr.H, a.pyr.W, mode
         fi[i].pool_arg = taps[i].data_ptr() if taps[i] is not None else None
@@ -286,6 +313,8 @@ def bifpn_fuse(eng: Engine, P: ParamStore, inputs: Sequence[Tuple[Act, int]], wn
 def residual(eng: Engine, x: Act, res: Act, scale: Optional[torch.Tensor], name: str = "") -> Act:
     """out = v(x) * scale[level][image] + v(res)  (drop-connect survival scale, 1 at inference)."""
     C = x.C
+    x.consume()
+    res.consume()
     y = eng.empty(x.pyr.rows, C)
     L.call("edet_residual_fwd", eng.dt, x.lazy(), res.lazy(), x.pyr.c, C, vp(scale), vp(y), stream())
     out = Act(y, x.pyr, C, training=eng.training, name=name)
@@ -308,6 +337,8 @@ def assemble_pyramid(eng: Engine, buf: torch.Tensor, pyr: Pyr, parts: Sequence[A
     """The last BiFPN cell writes its five node outputs into one pyramid buffer; this op is
     the (copy-free) join and, backwards, the split of the pyramid gradient into views."""
     C = parts[0].C
+    for a in parts:
+        a.consume()
     out = Act(buf, pyr, C, bns, L.ACT_NONE, training=eng.training, name=name)
 
     def bwd():

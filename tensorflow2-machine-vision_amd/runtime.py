@@ -114,7 +114,7 @@ class SERec:
 class Act:
     """Raw activation buffer + pending transform v = act(bn(raw)) * gate."""
 
-    __slots__ = ("raw", "pyr", "C", "ld", "bns", "act", "gate", "se", "training", "name", "_lz")
+    __slots__ = ("raw", "pyr", "C", "ld", "bns", "act", "gate", "se", "training", "name", "_lz", "uses")
 
     def __init__(self, raw: torch.Tensor, pyr: Pyr, C: int, bns: Optional[List[BNParam]] = None,
                  act: int = L.ACT_NONE, ld: Optional[int] = None, training: bool = False,
@@ -128,6 +128,14 @@ class Act:
         self.act, self.gate, self.se = act, None, None
         self.training, self.name = training, name
         self._lz = None
+        self.uses = 0  # forward ops that will send a gradient into this value (consume())
+
+    def consume(self) -> "Act":
+        """Count a training-mode consumer: a backward that owns the whole gradient of the
+        value (uses == 1) may fold the value's BN-backward sums into its own pass."""
+        if self.training:
+            self.uses += 1
+        return self
 
     @property
     def has_transform(self) -> bool:
@@ -381,10 +389,13 @@ def _init_values(sp: ParamSpec, rng: np.random.Generator) -> np.ndarray:
 
 # --------------------------------------------------------------------------- tape
 class GradRec:
-    __slots__ = ("t", "ld", "scale")
+    __slots__ = ("t", "ld", "scale", "bn_sums")
 
     def __init__(self, t: torch.Tensor, ld: int, scale: Optional[torch.Tensor] = None):
         self.t, self.ld, self.scale = t, ld, scale
+        # fp64 [2][nseg][C] (dgamma, dbeta) BN-backward sums of the value's BatchNorm, already
+        # accumulated by the kernel that wrote t (edet_dwconv_bwd's fold); None: not yet
+        self.bn_sums = None
 
 
 class Tape:

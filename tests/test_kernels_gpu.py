@@ -173,6 +173,72 @@ def test_dwconv_fwd_bwd(dt, k, s, H, W, C, lazy, nseg, workspace_mode):
     close(dw, wr.grad, dt, scale=pout.rows ** 0.5 * 3)
 
 
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("k,H,W,C,act,nseg,fold,acc", [
+    (3, 16, 16, 32, 1, 1, True, 0), (5, 11, 12, 40, 1, 1, True, 0), (3, 9, 9, 64, 1, 2, True, 0),
+    (5, 10, 11, 1152, 1, 1, True, 0), (3, 34, 37, 96, 0, 1, True, 0), (5, 33, 20, 144, 1, 1, False, 1),
+    (3, 8, 9, 480, 1, 1, False, 0), (5, 70, 66, 64, 1, 1, True, 0)])
+def test_dwconv_bwd_fused(dt, k, H, W, C, act, nseg, fold, acc):
+    """edet_dwconv_bwd (stride 1): dx, the filter gradient and the folded BN-backward sums of
+    the input's BatchNorm from one pass, against fp64 autograd and against the separate entry
+    points (dgrad, wgrad, lazy_bwd_reduce over the same dx)."""
+    rng = np.random.default_rng(k * 1000 + H * 10 + C)
+    B = 2
+    pin = Pyr(B, [(H, W), ((H + 1) // 2, (W + 1) // 2)]) if nseg == 2 else Pyr(B, [(H, W)])
+    x = pyr_data(rng, pin, C, dt, scale=2.0)
+    bn = make_bn(x, pin, C, rng)
+    lz = LazyDesc(x, pin, C, bn=bn, act=act)
+    w = g(rnd(rng, k * k, C, scale=0.3), dt)
+    dy = pyr_data(rng, pin, C, dt)
+    base = 0.25 if acc else 0.0
+    dx = g(torch.full((pin.rows, C), base), dt)
+    dw = zeros(k * k, C)
+    sums_t, sums = bngrad64(nseg, C) if fold else (None, None)
+    L.call("edet_dwconv_bwd", DT[dt], lz.c, pin.c, C, k, 1, vp(dy), pin.c, vp(w), vp(dx), acc, vp(dw), sums,
+           stream())
+    # fp64 autograd reference through v = act(bn(x)) and the stencil
+    v = lz.cpu_value().requires_grad_(True)
+    wr = w.double().cpu().requires_grad_(True)
+    mask = torch.zeros(pin.rows, 1, dtype=torch.float64)
+    for sg in range(nseg):
+        mask[pin.seg_slice(sg)] = 1
+    (dw_ref(v, pin, k, 1, wr) * dy.double().cpu() * mask).sum().backward()
+    for sg in range(nseg):
+        sl = pin.seg_slice(sg)
+        close(dx[sl], v.grad[sl] + base, dt)
+    close(dw, wr.grad, dt, scale=pin.rows ** 0.5 * 3)
+    # the separate entry points agree
+    dx2 = g(torch.full((pin.rows, C), base), dt)
+    L.call("edet_dwconv_dgrad", DT[dt], vp(dy), pin.c, C, k, 1, vp(w), vp(dx2), pin.c, acc, stream())
+    dw2 = zeros(k * k, C)
+    L.call("edet_dwconv_wgrad", DT[dt], lz.c, pin.c, C, k, 1, vp(dy), pin.c, vp(dw2), stream())
+    for sg in range(nseg):
+        sl = pin.seg_slice(sg)
+        close(dx[sl], dx2[sl].double(), dt)
+    close(dw, dw2, "f32", rtol=1e-4, atol=1e-4 * pin.rows ** 0.5)
+    if not fold:
+        return
+    # folded sums = the reduce pass over (x, dv = dx), and = fp64 du / du * xhat sums
+    acc2_t, acc2 = bngrad64(nseg, C)
+    L.call("edet_lazy_bwd_reduce", DT[dt], lz.c, pin.c, C, vp(dx), None, None, acc2, stream())
+    xc = x[:, :C].double().cpu()
+    for sg in range(nseg):
+        sl = pin.seg_slice(sg)
+        n = pin.seg_rows(sg)
+        su, sq, ga, be = (t.double().cpu() for t in bn[sg])
+        mean = su / n
+        rstd = 1.0 / torch.sqrt(torch.clamp(sq / n - mean * mean, min=0) + 1e-3)
+        xhat = (xc[sl] - mean) * rstd
+        u = xhat * ga + be
+        sgm = torch.sigmoid(u)
+        du = v.grad[sl] * (sgm * (1 + u * (1 - sgm)) if act else 1.0)
+        close(sums_t[1, sg], du.sum(0), dt, scale=n ** 0.5 * 2)
+        close(sums_t[0, sg], (du * xhat).sum(0), dt, scale=n ** 0.5 * 2)
+        # bf16: the fold sums the unrounded dx the reduce pass reads rounded
+        tol = dict(rtol=1e-4, atol=1e-4 * n ** 0.5) if dt == "f32" else dict(rtol=2e-2, atol=2e-2 * n ** 0.5)
+        torch.testing.assert_close(sums_t[:, sg].cpu(), acc2_t[:, sg].cpu(), **tol)
+
+
 @pytest.mark.parametrize("k,s,B,H,C", [(5, 1, 16, 64, 240), (3, 1, 8, 100, 64), (5, 2, 16, 72, 144)])
 def test_dwconv_long_blocks(k, s, B, H, C):
     """Forward and weight gradient at batch sizes where a row-streaming block walks many
