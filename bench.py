@@ -309,17 +309,37 @@ def probe_roofline(model, data, funcs, kernel, steps, es):
     return r
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC summary (two passes,
-    FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction; scripts/pmc_traffic.py), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def _pmc_entry(fname, kernel, calls_per_step):
+    """``kernel``'s entry of a committed rocprofv3 PMC summary under profiles/, or None when
+    absent or stale: the profiled run's dispatches per step must equal the launches this
+    step makes (a summary from an older tree counts other launches)."""
+    path = os.path.join(ROOT, "profiles", fname)
     try:
         with open(path) as f:
             d = json.load(f)
         k = d.get("kernels", {}).get(kernel)
-        return None if k is None else float(k["traffic_bytes_per_launch"])
+        if k is None:
+            return None
+        per = k.get("dispatches_per_step")
+        if per is None or calls_per_step is None or abs(per - calls_per_step) > 0.5:
+            return None
+        return k
     except (OSError, ValueError, KeyError):
         return None
+
+
+def pmc_traffic(kernel, calls_per_step=None):
+    """HBM bytes per launch of ``kernel`` from profiles/pmc_traffic.json (two PMC passes,
+    FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction; scripts/pmc_traffic.py), or None."""
+    k = _pmc_entry("pmc_traffic.json", kernel, calls_per_step)
+    return None if k is None else float(k["traffic_bytes_per_launch"])
+
+
+def pmc_mfma(kernel, calls_per_step=None):
+    """Fraction of the chip's MFMA issue cycles ``kernel`` used (SQ_VALU_MFMA_BUSY_CYCLES over
+    1024 SIMDs x the kernel's cycles, profiles/pmc_mfma.json from scripts/pmc_mfma.py), or None."""
+    k = _pmc_entry("pmc_mfma.json", kernel, calls_per_step)
+    return None if k is None else float(k["mfma_busy_frac"])
 
 
 def _cpu_share():
@@ -568,13 +588,15 @@ def main():
             if a[1] < 0.02 * total_ms:
                 continue
             gbs = a[2] / (a[1] * 1e6) if a[3] and a[1] > 0 else None
-            tr = pmc_traffic(k)
+            tr = pmc_traffic(k, a[0])
+            mf = pmc_mfma(k, a[0])
             table.append({"kernel": k, "calls": a[0], "ms": round(a[1], 4), "share": round(a[1] / total_ms, 4),
                           "avg_us": round(a[1] * 1e3 / a[0], 2),
                           "bytes_per_launch": round(a[2] / a[0]) if a[3] else None,
                           "achieved_GBps": None if gbs is None else round(gbs, 1),
                           "frac": None if gbs is None else round(gbs / HBM_PEAK_GBS, 4),
                           "pmc_traffic_ratio": (round(tr / (a[2] / a[0]), 3) if (tr and a[3] and a[2]) else None),
+                          "mfma_frac": None if mf is None else round(mf, 4),
                           "entry_points": sorted(a[4])})
         known = sum(a[2] for a in kag.values() if a[3])
         step_level = {"algorithmic_bytes": round(known), "ms_per_step": round(el / args.steps * 1e3, 3),
@@ -590,7 +612,7 @@ def main():
             kname, a = dom
             pr = probe_roofline(model, data, a[4], kname, args.steps, es)
             ach = pr["achieved_GBps"]
-            traffic = pmc_traffic(kname)
+            traffic = pmc_traffic(kname, a[0])
             roofline = {"bound": "hbm", "kernel": kname, "entry_points": sorted(a[4]), "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                         "traffic": None if traffic is None else round(traffic),

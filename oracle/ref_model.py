@@ -147,11 +147,18 @@ def maxpool_same(x, route=None, stats=None):
     rp = Fn.pad(torch.as_tensor(route, dtype=x.dtype), (pl, pr, pt, pb), value=-math.inf)
     _, idx = Fn.max_pool2d(rp, 3, 2, return_indices=True)
     N, C, Ho, Wo = idx.shape
+    out = xp.reshape(N, C, -1).gather(2, idx.reshape(N, C, -1)).reshape(N, C, Ho, Wo)
     if stats is not None:
-        _, own = Fn.max_pool2d(xp.detach(), 3, 2, return_indices=True)
-        stats["rerouted"] = stats.get("rerouted", 0) + int((own != idx).sum())
+        ownv, own = Fn.max_pool2d(xp.detach(), 3, 2, return_indices=True)
+        moved = own != idx
+        stats["rerouted"] = stats.get("rerouted", 0) + int(moved.sum())
         stats["windows"] = stats.get("windows", 0) + idx.numel()
-    return xp.reshape(N, C, -1).gather(2, idx.reshape(N, C, -1)).reshape(N, C, Ho, Wo)
+        # the tie gap: how far below its own window maximum the routed value lies, relative
+        # to the tensor's largest magnitude (0 when nothing moved)
+        if bool(moved.any()):
+            gap = float((ownv - out.detach())[moved].max()) / max(float(x.detach().abs().max()), 1e-30)
+            stats["max_gap_rel"] = max(stats.get("max_gap_rel", 0.0), gap)
+    return out
 
 
 def resize_nearest(x, H, W):

@@ -43,12 +43,16 @@ def main():
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--steps", type=int, default=6,
+                    help="train steps the profiled command ran (bench.py --steps 3 --warmup 1 --graph 0: 2 eager "
+                         "warm-ups + 1 + 3); bench.py uses dispatches / steps to reject a stale entry")
+    ap.add_argument("--tag", default="")
     a = ap.parse_args()
     fe = per_kernel(a.fetch, "FETCH_SIZE")
     wr = per_kernel(a.write, "WRITE_SIZE")
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), KiB per dispatch; "
                      "read bytes = 2 x FETCH_SIZE (gfx950 correction), write bytes = WRITE_SIZE",
-           "kernels": {}}
+           "tag": a.tag, "steps": a.steps, "kernels": {}}
     for k in sorted(set(fe) | set(wr)):
         f_kib, nf = fe.get(k, (0.0, 0))
         w_kib, nw = wr.get(k, (0.0, 0))
@@ -56,8 +60,8 @@ def main():
             continue
         rd = 2.0 * f_kib * 1024.0 / nf
         wb = w_kib * 1024.0 / nw
-        out["kernels"][k] = {"dispatches": nf, "read_bytes_per_launch": rd, "write_bytes_per_launch": wb,
-                             "traffic_bytes_per_launch": rd + wb}
+        out["kernels"][k] = {"dispatches": nf, "dispatches_per_step": nf / a.steps, "read_bytes_per_launch": rd,
+                             "write_bytes_per_launch": wb, "traffic_bytes_per_launch": rd + wb}
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
     for k, v in sorted(out["kernels"].items(), key=lambda kv: -kv[1]["traffic_bytes_per_launch"] * kv[1]["dispatches"])[:25]:

@@ -21,7 +21,11 @@ Tolerances (stated here, used below):
                 gradient 1e-3 (+1e-6 gnorm for analytically-zero gradients)
   D4 fp32       noise floor: at most 3x the fp32 oracle's deviation from the fp64 oracle
   bf16          RMS deviation at most 1.5x that of the oracle with bf16 storage rounding;
-                inference mode also max <= BF16_OUT * RMS, BF16_OUT = 0.1, RMS <= 2 %
+                inference mode also max <= BF16_OUT * RMS, BF16_OUT = 0.1, RMS <= 2 %;
+                training mode also max <= BF16_TRAIN_MAX = 3x the emulation's max (+1e-3 max|ref|)
+  pool routing  windows whose winner the product's fp32 values moved: at most POOL_REROUTE =
+                1e-4 of all windows, each within POOL_GAP = 1e-5 (relative to max|x|) of its
+                own maximum (a near-tie, not a miswired pool)
 """
 import json
 import os
@@ -38,6 +42,9 @@ from tf2mv_amd.model import EfficientDetNet, EfficientDetNetTrain
 pytestmark = pytest.mark.gpu
 OUT_FLOOR = 3e-5
 BF16_OUT = 0.1
+BF16_TRAIN_MAX = 3.0
+POOL_REROUTE = 1e-4
+POOL_GAP = 1e-5
 REPORT = os.environ.get("EDET_REPORT_DIR")
 
 
@@ -204,7 +211,8 @@ def train_parity(name, S, B, NC, seed, with_fp32_floor=False):
     if with_fp32_floor:
         fl = oracle_step(cfg, sd0, x, omasks, targets, routes, dtype=torch.float32)
     rep = {"loss": loss, "ref_loss": rloss, "gnorm": gn, "ref_gnorm": rgn, "npos": float(m.scalars[5]),
-           "pool_windows": rstats.get("windows", 0), "pool_rerouted": rstats.get("rerouted", 0), "levels": []}
+           "pool_windows": rstats.get("windows", 0), "pool_rerouted": rstats.get("rerouted", 0),
+           "pool_max_gap_rel": rstats.get("max_gap_rel", 0.0), "levels": []}
     if fl is not None:
         rep["fp32_oracle_loss"], rep["fp32_oracle_gnorm"] = fl[2], fl[4]
     for l in range(5):
@@ -227,6 +235,9 @@ def check_train_report(rep, floor_mult=None):
     gradients 1e-3).  Otherwise the noise-floor bars: the GPU's deviation from the fp64 oracle
     at most floor_mult times the fp32 oracle's (same semantics, same inputs, fp32 arithmetic)."""
     assert abs(rep["loss"] - rep["ref_loss"]) / rep["ref_loss"] < 1e-4, (rep["loss"], rep["ref_loss"])
+    # pool routing (see test_d0_512_nc81_train_step_parity_fp32): only near-ties may move
+    assert rep["pool_rerouted"] <= POOL_REROUTE * max(rep["pool_windows"], 1), rep
+    assert rep["pool_max_gap_rel"] <= POOL_GAP, rep
     gtol = 1e-3 if floor_mult is None else max(1e-3, floor_mult * abs(rep["fp32_oracle_gnorm"] - rep["ref_gnorm"])
                                                / rep["ref_gnorm"])
     assert abs(rep["gnorm"] - rep["ref_gnorm"]) / rep["ref_gnorm"] < gtol, (rep["gnorm"], rep["ref_gnorm"])
@@ -314,7 +325,9 @@ def test_d0_512_nc81_forward_bf16(training):
     _report(f"d0_512_nc81_forward_bf16_{'train' if training else 'infer'}", {"levels": rep})
     for l, kind, e in rep:
         assert e["rms_err"] <= 1.5 * e["floor_rms_err"] + 1e-3 * e["rms_ref"], (l, kind, e)
-        if not training:
+        if training:
+            assert e["max_abs"] <= BF16_TRAIN_MAX * e["floor_max_abs"] + 1e-3 * e["max_ref"], (l, kind, e)
+        else:
             assert e["max_abs"] <= BF16_OUT * e["rms_ref"], (l, kind, e)
             assert e["rms_err"] <= 0.02 * e["rms_ref"], (l, kind, e)
 
@@ -343,3 +356,74 @@ def test_d0_512_b32_bf16_five_steps():
     assert all(0.3 <= v <= 30.0 for v in gnorms), gnorms
     assert bool(torch.isfinite(m.P.w).all()) and bool(torch.isfinite(m.P.bn_mm).all())
     assert bool(torch.isfinite(m.P.bn_mv).all()) and float(m.P.bn_mv.min()) > 0
+
+
+@pytest.mark.timeout(900)
+def test_d4_1024_forward_bf16():
+    """BASELINE config 5's model in the metric's dtype: EfficientDet-D4 at 1024x1024 (7 BiFPN
+    cells of 224 channels, C up to 2688: the bf16 kernels at D4 shapes), B = 1, inference
+    mode, against the fp64 oracle on the same bf16-rounded weights and input and against the
+    oracle with bf16 storage rounding emulated.  Bars as for D0 inference: RMS deviation at
+    most 1.5x the emulation's (+1e-3 RMS), max <= BF16_OUT * RMS, RMS error <= 2 %."""
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    S, B, NC = 1024, 1, 81
+    cfg = get_efficientdet_config("efficientdet-d4", {"image_size": S, "num_classes": NC})
+    m = EfficientDetNet(efficientnet_b0_blocks(), cfg, dtype="bf16", seed=14)
+    m.load_state_dict(_bf16_round_sd(perturb(m.state_dict(), 114)))
+    x, *_ = synth(B, S, NC, 14)
+    xr = torch.tensor(x).to(torch.bfloat16)
+    bo, co = m.call(xr.cuda(), training=False)
+    ref = RefEfficientDet(cfg, m.state_dict())
+    emu = RefEfficientDet(cfg, m.state_dict())
+    emu.store = lambda t: t.to(torch.bfloat16).to(t.dtype)
+    with torch.no_grad():
+        rb, rc = ref.forward(xr.float().numpy(), False)
+        eb, ec = emu.forward(xr.float().numpy(), False)
+    rep = []
+    for l in range(5):
+        for kind, a, b, f in (("box", bo[l], rb[l], eb[l]), ("cls", co[l], rc[l], ec[l])):
+            rep.append((l, kind, out_errors(a.float().cpu(), b, f)))
+    _report("d4_1024_forward_bf16_infer", {"levels": rep})
+    for l, kind, e in rep:
+        assert e["rms_err"] <= 1.5 * e["floor_rms_err"] + 1e-3 * e["rms_ref"], (l, kind, e)
+        assert e["max_abs"] <= BF16_OUT * e["rms_ref"], (l, kind, e)
+        assert e["rms_err"] <= 0.02 * e["rms_ref"], (l, kind, e)
+
+
+@pytest.mark.timeout(600)
+def test_d4_1024_b8_bf16_three_steps():
+    """BASELINE config 5's per-GPU workload (D4, 1024x1024, B = 8, bf16, 81 classes): three
+    train steps on one synthetic batch with the bench's schedule.  Properties: loss and
+    gradient norm finite on every step; the step-0 loss within 1 % and the step-0 gradient
+    norm within 2x of the same step in fp32 storage (same weights, batch and drop-connect
+    draws); the loss stays within 2 % of its start (D4's loss is dominated by the L2 term and
+    the clip at 10 is active, profiles/r02_d4_gnorm.txt); gradient norms in [10, 5000];
+    parameters and BN moving statistics finite."""
+    S, B = 1024, 8
+    cfg = get_efficientdet_config("efficientdet-d4")
+    anchors = Anchors(cfg.min_level, cfg.max_level, (S, S), cfg.num_scales, cfg.aspect_ratios, cfg.anchor_scale)
+    x, boxes, cls, n = synth(B, S, 81, 1004)
+    t = anchors.generate_targets_batched(torch.tensor(boxes), torch.tensor(cls), torch.tensor(n))
+    first = {}
+    for dt in ("f32", "bf16"):
+        m = EfficientDetNetTrain(efficientnet_b0_blocks(), cfg, anchors, dtype=dt, seed=0,
+                                 lr_schedule={"warmup_steps": 100, "total_steps": 10000, "adjusted_lr": 0.08 * B / 64})
+        xs = torch.tensor(x).cuda().to(m.eng.tdtype)
+        losses, gnorms = [], []
+        for _ in range(1 if dt == "f32" else 3):
+            out = m.train_step((xs, t))
+            losses.append(float(out["loss"]))
+            gnorms.append(float(out["gnorm"]))
+        first[dt] = (losses, gnorms)
+        if dt == "bf16":
+            assert bool(torch.isfinite(m.P.w).all()) and bool(torch.isfinite(m.P.bn_mm).all())
+            assert bool(torch.isfinite(m.P.bn_mv).all()) and float(m.P.bn_mv.min()) > 0
+        del m
+        torch.cuda.empty_cache()
+    (lf, gf), (lb, gb) = first["f32"], first["bf16"]
+    _report("d4_1024_b8_bf16_three_steps", {"loss": lb, "gnorm": gb, "f32_loss0": lf[0], "f32_gnorm0": gf[0]})
+    assert np.all(np.isfinite(lb)) and np.all(np.isfinite(gb)), (lb, gb)
+    assert abs(lb[0] - lf[0]) / lf[0] < 1e-2, (lb[0], lf[0])
+    assert 0.5 <= gb[0] / gf[0] <= 2.0, (gb[0], gf[0])
+    assert all(abs(v - lb[0]) / lb[0] < 0.02 for v in lb), lb
+    assert all(10.0 <= v <= 5000.0 for v in gb), gb

@@ -174,7 +174,7 @@ def test_train_step_bf16_within_fp32_noise_floor():
     test_train_step_parity_fp32).  The EfficientDet gradient at initialisation is chaotic: the
     fp32 path run on bf16-ROUNDED weights and input -- the smallest perturbation bf16 storage
     implies (2^-9 relative) -- already moves the gradient (cosine ~0.85, median per-tensor
-    change ~50 %, scripts/debug_bf16b.py).  That run defines the noise floor; the
+    change ~50 %, tools/dev/debug_bf16b.py).  That run defines the noise floor; the
     bf16 step must stay within a small multiple of it, its loss within 3x the floor's loss
     change (or 0.2 %), and the loss-adjacent predict-layer gradients likewise (and cosine > 0.95)."""
     x, boxes, cls, n = synth(5)

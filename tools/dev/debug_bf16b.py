@@ -1,7 +1,7 @@
 """Debug 2: gradient sensitivity. (i) fp32 vs fp32 with a 2^-9 relative input perturbation and
 bf16-rounded weights; (ii) bf16 vs fp32 at a realistic size (B=8, 512x512)."""
 import os, sys
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
 import numpy as np
 import torch
 from tf2mv_amd.anchors import Anchors

@@ -1,8 +1,8 @@
 """Run the same fp32 train step (same weights, same data) several times and report how far
 the BN statistics and per-tensor gradients move between runs (atomics-order noise vs races)."""
 import sys, os
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
 import numpy as np
 import torch
 from test_model_gpu import _train_model, synth, make_targets

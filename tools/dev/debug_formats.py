@@ -1,8 +1,8 @@
 """Compact targets vs targets converted from the reference format: compare the target
 tensors on segment rows, then the loss parts and gradients of the same fp32 step."""
 import sys, os
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
 import torch
 from tf2mv_amd.anchors import Targets
 from test_model_gpu import _train_model, synth, make_targets

@@ -1,8 +1,8 @@
 """Snapshot every bifpn_fuse_bwd launch (dF in, each input's dx out, weight grads) over 4
 identical fp32 steps and report the first launch whose outputs differ between runs."""
 import sys, os, ctypes
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
 import torch
 from tf2mv_amd import _lib as L
 from tf2mv_amd.runtime import stream

@@ -1,8 +1,8 @@
 """Which BN's statistics vary between identical train steps (fp64 order noise ~1e-16; a real
 divergence is >1e-10)?  Prints the first drifting BN in forward order for each rerun."""
 import sys, os
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
 import torch
 from test_model_gpu import _train_model, synth, make_targets
 

@@ -1,8 +1,8 @@
 """Run the same fp32 step 4 times with the tape's gradient trace on and print, in backward
 order, the first activations whose d(value) differs between runs by more than 1e-3."""
 import sys, os
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
 import torch
 from test_model_gpu import _train_model, synth, make_targets
 

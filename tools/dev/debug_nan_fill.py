@@ -2,8 +2,8 @@
 memory nobody wrote turns it into NaN.  Reports the first traced gradient / final tensors
 that are non-finite."""
 import sys, os
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
 import torch
 from tf2mv_amd import runtime
 from test_model_gpu import _train_model, synth, make_targets

@@ -1,8 +1,8 @@
 """Is load_state_dict(state_dict()) an identity for the next step's gradients?  Compare
 buffers and gradients of: fresh model, and the same model after one train_step + reload."""
 import sys, os
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
 import torch
 from test_model_gpu import _train_model, synth, make_targets
 

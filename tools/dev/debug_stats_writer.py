@@ -1,8 +1,8 @@
 """Find which C-ABI call modifies the BN statistics arena after the forward pass
 (snapshot bn_tstats after every call of one fp32 train step)."""
 import sys, os
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "tests"))
 import torch
 from tf2mv_amd import _lib as L
 from test_model_gpu import _train_model, synth, make_targets
