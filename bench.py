@@ -91,6 +91,9 @@ def algorithmic_bytes(name, args, es):
     if name == "edet_dwconv_dgrad":
         pout, C, pin, acc = args[2], args[3], args[8], args[9]
         return (rows(pout) + rows(pin) * (1 + acc)) * C * es
+    if name == "edet_dwconv_bwd":  # (dtype, lz, pin, C, k, s, dy, pout, w, dx, acc, dw, fold, stream)
+        pin, C, pout, acc = args[2], args[3], args[7], args[10]
+        return (rows(pout) + rows(pin) * (2 + acc)) * C * es  # dy, x, dx (+ dx read)
     if name == "edet_lazy_materialize":
         return 2 * rows(args[2]) * args[3] * es
     if name == "edet_lazy_bwd_reduce":
@@ -151,6 +154,8 @@ def shape_tag(name, args):
             return f"M={rows(args[2])} K={args[3]} N={args[6]} {lazy(args[1])}"
         if name in ("edet_dwconv_fwd", "edet_dwconv_wgrad"):
             return f"in={rows(args[2])} C={args[3]} k={args[4]} s={args[5]}"
+        if name == "edet_dwconv_bwd":
+            return f"in={rows(args[2])} C={args[3]} k={args[4]} s={args[5]}" + (" fold" if args[12] else "")
         if name == "edet_dwconv_dgrad":
             return f"out={rows(args[2])} C={args[3]} k={args[4]} s={args[5]}"
         if name in ("edet_lazy_bwd_reduce", "edet_lazy_bwd_apply", "edet_lazy_materialize"):

@@ -1387,7 +1387,7 @@ static int dispatch_dws(const DwArgs& g, hipStream_t s) {
 // row is in flight in registers; one barrier per row.  Thread (c, gc) owns channel c and
 // columns gc*CPG..: dx leaves as direct stores, the filter-gradient taps and the fold sums stay
 // in registers until the block ends.
-template <typename T, int K, int CPG, bool FOLD>
+template <typename T, int K, int CPG, bool FOLD, int PF>
 __global__ __launch_bounds__(256) void k_dwb(DwArgs g, DwsPlan pl, edet_bngrad64 fold) {
   constexpr int P = (K - 1) / 2;
   constexpr int TW = 8 * CPG, IWS = TW + K - 1;
@@ -1528,13 +1528,17 @@ __global__ __launch_bounds__(256) void k_dwb(DwArgs g, DwsPlan pl, edet_bngrad64
     }
   }
   fetch(rs, rsx, K - 1, 1);
+  // PF = 2: a second register set keeps the row after next in flight too (rows alternate
+  // between the sets; the loop is unrolled by two so both stay in registers)
+  DwRaw<PF == 2 ? NVS : 1, WORDS> rs2, rsx2;
+  if constexpr (PF == 2) fetch(rs2, rsx2, K, 1);
 
   float acc[K * K];
 #pragma unroll
   for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
   float fs = 0.f, fq = 0.f;
   const int act = g.lz.act;
-  for (int j = 0; j < nrows; ++j) {
+  auto row_step = [&](int j, auto& rg, auto& rx) {
     const int r = r0 + j;
     T xr[CPG];
     if constexpr (FOLD) {  // x of this thread's dx elements (read K-1 rows ago: cache-hot)
@@ -1545,9 +1549,9 @@ __global__ __launch_bounds__(256) void k_dwb(DwArgs g, DwsPlan pl, edet_bngrad64
         xr[i] = X[ok ? (size_t)(r * W + col) * g.lz.ld + c : 0];
       }
     }
-    commit(rs, rsx, j + K - 1, 1);
+    commit(rg, rx, j + K - 1, 1);
     // unconditional refill (rows past the block are real or predicated-off elements)
-    fetch(rs, rsx, j + K, 1);
+    fetch(rg, rx, j + K - 1 + PF, 1);
     __syncthreads();
 
     float dxv[CPG], dyc[CPG];
@@ -1594,6 +1598,14 @@ __global__ __launch_bounds__(256) void k_dwb(DwArgs g, DwsPlan pl, edet_bngrad64
         }
       }
     }
+  };
+  if constexpr (PF == 1) {
+    for (int j = 0; j < nrows; ++j) row_step(j, rs, rsx);
+  } else {
+    for (int j = 0; j < nrows; j += 2) {
+      row_step(j, rs, rsx);
+      if (j + 1 < nrows) row_step(j + 1, rs2, rsx2);
+    }
   }
   // block reductions over the 8 column groups: filter taps (+ fold sums), one atomic each
   __syncthreads();
@@ -1619,6 +1631,8 @@ __global__ __launch_bounds__(256) void k_dwb(DwArgs g, DwsPlan pl, edet_bngrad64
 
 template <typename T, int K, int CPG, bool FOLD>
 static int launch_dwb(DwArgs g, const edet_bngrad64& fold, hipStream_t s) {
+  // rows in flight ahead of the one committed (development slot 17 = 2 selects two)
+  const int pf = dev_knob(17) == 2 ? 2 : 1;
   constexpr int TW = 8 * CPG;
   int hmax = 0;
   for (int i = 0; i < g.pin.nseg; ++i) hmax = std::max(hmax, g.pin.H[i]);
@@ -1641,7 +1655,8 @@ static int launch_dwb(DwArgs g, const edet_bngrad64& fold, hipStream_t s) {
   }
   if (total == 0) return EDET_OK;
   EDET_REQUIRE(total < (1L << 31), "dwconv_bwd: grid too large");
-  EDET_LAUNCH((k_dwb<T, K, CPG, FOLD>), dim3((unsigned)total), dim3(256), 0, s, g, pl, fold);
+  if (pf == 2) EDET_LAUNCH((k_dwb<T, K, CPG, FOLD, 2>), dim3((unsigned)total), dim3(256), 0, s, g, pl, fold);
+  else EDET_LAUNCH((k_dwb<T, K, CPG, FOLD, 1>), dim3((unsigned)total), dim3(256), 0, s, g, pl, fold);
   return check_launch("edet dwconv bwd");
 }
 
