@@ -1013,8 +1013,9 @@ struct DwRaw {  // raw input vectors of a fetch, in registers until their commit
   uint32_t ok;
 };
 
-template <typename T, int K, int S, int CPG, bool WG, int P>
+template <typename T, int K, int S, int CPG, bool WG, int P, int PF = 1>
 __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
+  static_assert(PF == 1 || (PF == 2 && !WG), "two steps in flight: forward only");
   // P output rows per step: they share (P-1)*S... of their K input rows, so each input row of
   // the step is read from LDS once for all of them, and one barrier serves P rows
   constexpr int TW = 8 * CPG, IWS = (TW - 1) * S + K;
@@ -1177,6 +1178,10 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
   DwRaw<NVS, WORDS> rs;
   fetch(rs, rows_of(1), P * S);
   if constexpr (WG) fetch_dy(1);
+  // PF = 2: a second register set keeps the step after next in flight too (steps alternate
+  // between the sets; the loop is unrolled by two so both stay in registers)
+  DwRaw<PF == 2 ? NVS : 1, WORDS> rs2;
+  if constexpr (PF == 2) fetch(rs2, rows_of(2), P * S);
   __syncthreads();
 
   float s = 0.f, q = 0.f;                 // fwd BN statistics of channel c
@@ -1201,17 +1206,17 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
       }
     }
   };
-  for (int j = 0; j < nsteps; ++j) {
+  auto step = [&](int j, auto& rsj) {
     if constexpr (!WG) {
       if (j > 0) store_step(j - 1);
     }
     if (j + 1 < nsteps) {  // rows of step j+1: ring slots and dy buffer step j does not read
-      commit(rs, rows_of(j + 1), P * S);
+      commit(rsj, rows_of(j + 1), P * S);
       if constexpr (WG) commit_dy(j + 1);
     }
     // unconditional: a conditional refill joins old and new values in a copy, and the copy
     // waits for the load (rows past the block are real or predicated-off elements)
-    fetch(rs, rows_of(j + 2), P * S);
+    fetch(rsj, rows_of(j + 1 + PF), P * S);
     if constexpr (WG) fetch_dy(j + 2);
     int slot = (j * P * S) % R;
     if constexpr (!WG) {
@@ -1274,6 +1279,14 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
       }
     }
     __syncthreads();
+  };
+  if constexpr (PF == 1) {
+    for (int j = 0; j < nsteps; ++j) step(j, rs);
+  } else {
+    for (int j = 0; j < nsteps; j += 2) {
+      step(j, rs);
+      if (j + 1 < nsteps) step(j + 1, rs2);
+    }
   }
   if constexpr (!WG) {
     store_step(nsteps - 1);
@@ -1349,6 +1362,10 @@ static int launch_dws(DwArgs g, hipStream_t s) {
   if (total == 0) return EDET_OK;
   pl.cb_inner = dev_knob(15) != 2;
   EDET_REQUIRE(total < (1L << 31), "dwconv: grid too large");
+  if (!WG && dev_knob(18) == 2) {  // development: two steps in flight (forward)
+    EDET_LAUNCH((k_dws<T, K, S, CPG, false, P, 2>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
+    return check_launch("edet dwconv (rows)");
+  }
   EDET_LAUNCH((k_dws<T, K, S, CPG, WG, P>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
   return check_launch("edet dwconv (rows)");
 }
@@ -1540,13 +1557,24 @@ __global__ __launch_bounds__(256) void k_dwb(DwArgs g, DwsPlan pl, edet_bngrad64
   const int act = g.lz.act;
   auto row_step = [&](int j, auto& rg, auto& rx) {
     const int r = r0 + j;
-    T xr[CPG];
-    if constexpr (FOLD) {  // x of this thread's dx elements (read K-1 rows ago: cache-hot)
+    // this row's global reads (the fold's x, read K-1 rows ago and cache-hot; dx for an
+    // accumulating store) go out before the next row's prefetch: a load issued after it
+    // would make its consumer wait for the prefetch too (vmcnt counts in issue order)
+    T xr[CPG], dold[CPG];
+    if constexpr (FOLD) {
 #pragma unroll
       for (int i = 0; i < CPG; ++i) {
         const int col = x0 + gc * CPG + i;
         const bool ok = col < W && cvalid;
         xr[i] = X[ok ? (size_t)(r * W + col) * g.lz.ld + c : 0];
+      }
+    }
+    if (g.accumulate) {
+#pragma unroll
+      for (int i = 0; i < CPG; ++i) {
+        const int col = x0 + gc * CPG + i;
+        const bool ok = col < W && cvalid;
+        dold[i] = DX[ok ? (size_t)(r * W + col) * C + c : 0];
       }
     }
     commit(rg, rx, j + K - 1, 1);
@@ -1588,8 +1616,7 @@ __global__ __launch_bounds__(256) void k_dwb(DwArgs g, DwsPlan pl, edet_bngrad64
     for (int i = 0; i < CPG; ++i) {
       const int col = x0 + gc * CPG + i;
       if (col < W && cvalid) {
-        T* p = DX + (size_t)(r * W + col) * C + c;
-        *p = from_f<T>(g.accumulate ? to_f<T>(*p) + dxv[i] : dxv[i]);
+        DX[(size_t)(r * W + col) * C + c] = from_f<T>(g.accumulate ? to_f<T>(dold[i]) + dxv[i] : dxv[i]);
         if constexpr (FOLD) {
           const float xv = to_f<T>(xr[i]);
           const float du = act ? dxv[i] * dswishf_(xv * myaf.x + myaf.y) : dxv[i];

@@ -74,8 +74,13 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   constexpr int AV = (BM * KV + 255) / 256, BV = (BN * KV + 255) / 256;
   using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
   constexpr int VW = sizeof(T) == 2 ? 1 : 2;  // 16-byte words per 8 elements
-  __shared__ __attribute__((aligned(16))) T As[2][BM * LDK];
-  __shared__ __attribute__((aligned(16))) T Bs[2][BN * LDK];
+  // A / B chunk buffers, reused after the K loop as the C tile staged for 16-byte row stores
+  constexpr int LDC_S = BN + 8;
+  constexpr int AB_BYTES = 2 * (BM + BN) * LDK * (int)sizeof(T), C_BYTES = BM * LDC_S * (int)sizeof(T);
+  __shared__ __attribute__((aligned(16))) char smem_ab[AB_BYTES > C_BYTES ? AB_BYTES : C_BYTES];
+  T (*As)[BM * LDK] = reinterpret_cast<T (*)[BM * LDK]>(smem_ab);
+  T (*Bs)[BN * LDK] = reinterpret_cast<T (*)[BN * LDK]>(smem_ab + 2 * BM * LDK * sizeof(T));
+  T* Cs = reinterpret_cast<T*>(smem_ab);
   __shared__ float red[2][2][BN];  // [sum|sq][wm][col]: one writer each, summed in fixed order
   extern __shared__ float2 xf[];   // [K] lazy affine per input channel, then [2][K] gate rows
   float* gts = reinterpret_cast<float*>(xf + (LAZY ? g.K : 0));
@@ -109,7 +114,9 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 
   const T* A = (const T*)g.a;
   const T* B = (const T*)g.b;
-  V ra[AV][VW], rb[BV][VW];
+  struct Chunk {
+    V ra[AV][VW], rb[BV][VW];
+  };
   // per-thread A rows are fixed across chunks: resolve their gate rows once
   const float* gpu_[AV];
 #pragma unroll
@@ -122,17 +129,17 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     }
   }
   // global -> registers (raw); invalid lanes hold zeros
-  auto fetch = [&](int k0) {
+  auto fetch = [&](Chunk& R, int k0) {
 #pragma unroll
     for (int u = 0; u < AV; ++u) {
       const int v = tid + u * 256;
       const int r = v / KV, kv = (v % KV) * 8, grow = row0 + r, gk = k0 + kv;
 #pragma unroll
-      for (int w = 0; w < VW; ++w) ra[u][w] = V{};
+      for (int w = 0; w < VW; ++w) R.ra[u][w] = V{};
       if (v < BM * KV && grow < g.M && gk < g.K) {
         const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + gk);
 #pragma unroll
-        for (int w = 0; w < VW; ++w) ra[u][w] = src[w];
+        for (int w = 0; w < VW; ++w) R.ra[u][w] = src[w];
       }
     }
 #pragma unroll
@@ -140,16 +147,16 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
       const int v = tid + u * 256;
       const int n = v / KV, kv = (v % KV) * 8, gn = col0 + n, gk = k0 + kv;
 #pragma unroll
-      for (int w = 0; w < VW; ++w) rb[u][w] = V{};
+      for (int w = 0; w < VW; ++w) R.rb[u][w] = V{};
       if (v < BN * KV && gn < g.N && gk < g.K) {
         const V* src = reinterpret_cast<const V*>(B + (size_t)gn * g.ldb + gk);
 #pragma unroll
-        for (int w = 0; w < VW; ++w) rb[u][w] = src[w];
+        for (int w = 0; w < VW; ++w) R.rb[u][w] = src[w];
       }
     }
   };
   // registers -> LDS buffer, lazy transform of A on the way
-  auto commit = [&](int buf, int k0) {
+  auto commit = [&](const Chunk& R, int buf, int k0) {
 #pragma unroll
     for (int u = 0; u < AV; ++u) {
       const int v = tid + u * 256;
@@ -158,7 +165,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         T* dst = &As[buf][r * LDK + kv];
         if constexpr (LAZY) {
           const int grow = row0 + r, gk = k0 + kv;
-          const T* e = reinterpret_cast<const T*>(&ra[u][0]);
+          const T* e = reinterpret_cast<const T*>(&R.ra[u][0]);
           float vals[8];
           const float* gp = gpu_[u];
 #pragma unroll
@@ -173,7 +180,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
           st8(dst, vals);
         } else {
 #pragma unroll
-          for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(dst)[w] = ra[u][w];
+          for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(dst)[w] = R.ra[u][w];
         }
       }
     }
@@ -183,7 +190,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
       if (v < BN * KV) {
         const int n = v / KV, kv = (v % KV) * 8;
 #pragma unroll
-        for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(&Bs[buf][n * LDK + kv])[w] = rb[u][w];
+        for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(&Bs[buf][n * LDK + kv])[w] = R.rb[u][w];
       }
     }
   };
@@ -194,14 +201,17 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  // Two register chunks in flight: chunk k+1 was fetched two iterations before its commit (one
+  // chunk ahead left every 32-wide K step waiting a memory round trip behind a handful of MFMAs)
   const int nk = cdiv(g.K, KC);
-  fetch(0);
-  commit(0, 0);
+  Chunk R0, R1;
+  fetch(R0, 0);
+  commit(R0, 0, 0);
+  if (1 < nk) fetch(R0, KC);
+  if (2 < nk) fetch(R1, 2 * KC);
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
+  auto kstep = [&](Chunk& R, int kt) {
     const int buf = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) fetch((kt + 1) * KC);
     const T* Ab = As[buf];
     const T* Bb = Bs[buf];
 #pragma unroll
@@ -235,30 +245,49 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         }
       }
     }
-    if (more) commit(buf ^ 1, (kt + 1) * KC);
+    if (kt + 1 < nk) commit(R, buf ^ 1, (kt + 1) * KC);
+    if (kt + 3 < nk) fetch(R, (kt + 3) * KC);
     __syncthreads();
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    kstep(R0, kt);
+    if (kt + 1 < nk) kstep(R1, kt + 1);
   }
 
-  // ---- epilogue: bias, store (optionally accumulate), BN statistics
+  // ---- epilogue: bias, BN statistics, the tile staged in LDS (the K loop's last barrier freed
+  // the chunk buffers), then written as 16-byte row vectors (the MFMA layout's per-lane 2-byte
+  // stores left 32-byte pieces of lines: 8192 x 192 -> 1152 ran at 0.65 TB/s)
   T* C = (T*)g.c;
   float ssum[FN], ssq[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) { ssum[j] = 0.f; ssq[j] = 0.f; }
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
-    const int col = col0 + wn * WN + j * 16 + (lane & 15);
+    const int cl = wn * WN + j * 16 + (lane & 15), col = col0 + cl;
     const float bv = (g.bias && col < g.N) ? g.bias[col] : 0.f;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = row0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        const int rl = wm * WM + i * 16 + (lane >> 4) * 4 + r, row = row0 + rl;
         const float v = acc[i][j][r] + bv;
-        if (row < g.M && col < g.N) {
-          T* p = C + (size_t)row * g.ldc + col;
-          *p = from_f<T>(g.accumulate ? to_f<T>(*p) + v : v);
-          if (row < seg_end) { ssum[j] += v; ssq[j] += v * v; }
-        }
+        Cs[rl * LDC_S + cl] = from_f<T>(v);
+        if (row < g.M && col < g.N && row < seg_end) { ssum[j] += v; ssq[j] += v * v; }
+      }
+    }
+  }
+  __syncthreads();
+  {
+    constexpr int VPR = BN / 8;  // 8-element vectors per tile row
+    for (int e = tid; e < BM * VPR; e += 256) {
+      const int rl = e / VPR, cv = (e - rl * VPR) * 8;
+      const int row = row0 + rl, col = col0 + cv;
+      if (row < g.M && col < g.N) {
+        float vals[8];
+        const T* src = Cs + rl * LDC_S + cv;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) vals[jj] = to_f<T>(src[jj]);
+        acc8m(C + (size_t)row * g.ldc + col, g.N - col, vals, g.accumulate);
       }
     }
   }
@@ -772,50 +801,52 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
   }
   // each thread moves rows (tid>>3) and (tid>>3)+32, 8-column vector (tid&7)*8 of both tiles
   const int lr = tid >> 3, lc = (tid & 7) * 8;
-  uint4 rd[2], rx[2];
-  int rseg[2];
-  auto fetch = [&](int m0) {
+  struct Stage {
+    uint4 rd[2], rx[2];
+    int rseg[2];
+  };
+  auto fetch = [&](Stage& S, int m0) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int row = m0 + lr + 32 * h;
       const int sg = seg_of_row(g.pyr, row);
       const bool live = row < m_end && row < g.pyr.row_off[sg] + seg_rows(g.pyr, sg);
-      rseg[h] = live ? sg : -1;
+      S.rseg[h] = live ? sg : -1;
       const int nn = g.N - (n0 + lc), nk = g.K - (kk0 + lc);
-      rd[h] = make_uint4(0, 0, 0, 0);
-      rx[h] = make_uint4(0, 0, 0, 0);
-      if (live && nn >= 8) rd[h] = *reinterpret_cast<const uint4*>(DY + (size_t)row * g.lddy + n0 + lc);
+      S.rd[h] = make_uint4(0, 0, 0, 0);
+      S.rx[h] = make_uint4(0, 0, 0, 0);
+      if (live && nn >= 8) S.rd[h] = *reinterpret_cast<const uint4*>(DY + (size_t)row * g.lddy + n0 + lc);
       else if (live && nn > 0) {
         float v[8];
         ld8m(DY + (size_t)row * g.lddy + n0 + lc, nn, v);
         uint16_t t[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) t[j] = from_f<uint16_t>(v[j]);
-        rd[h] = *reinterpret_cast<uint4*>(t);
+        S.rd[h] = *reinterpret_cast<uint4*>(t);
       }
-      if (live && nk >= 8) rx[h] = *reinterpret_cast<const uint4*>(A + (size_t)row * g.lda + kk0 + lc);
+      if (live && nk >= 8) S.rx[h] = *reinterpret_cast<const uint4*>(A + (size_t)row * g.lda + kk0 + lc);
       else if (live && nk > 0) {
         float v[8];
         ld8m(A + (size_t)row * g.lda + kk0 + lc, nk, v);
         uint16_t t[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) t[j] = from_f<uint16_t>(v[j]);
-        rx[h] = *reinterpret_cast<uint4*>(t);
+        S.rx[h] = *reinterpret_cast<uint4*>(t);
       }
     }
   };
   // SE gate of this thread's 8 columns, cached per image (the image changes every hw rows)
   int gimg[2] = {-1, -1};
   float gcache[2][8];
-  auto commit = [&](int buf, int m0) {
+  auto commit = [&](const Stage& S, int buf, int m0) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int r = lr + 32 * h;
-      *reinterpret_cast<uint4*>(&Ds[buf][r * WT_LDM + lc]) = rd[h];
-      uint4 x = rx[h];
+      *reinterpret_cast<uint4*>(&Ds[buf][r * WT_LDM + lc]) = S.rd[h];
+      uint4 x = S.rx[h];
       if constexpr (LAZY) {
-        if (rseg[h] >= 0) {
-          const int row = m0 + r, sg = rseg[h];
+        if (S.rseg[h] >= 0) {
+          const int row = m0 + r, sg = S.rseg[h];
           const uint16_t* t = reinterpret_cast<const uint16_t*>(&x);
           if (g.lz.gate) {
             const int img = (row - g.pyr.row_off[sg]) / (g.pyr.H[sg] * g.pyr.W[sg]);
@@ -852,15 +883,18 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
     for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   float dbacc = 0.f;
   if constexpr (LAZY) __syncthreads();  // xf tables
+  // Two register stages in flight: stage m+1 was fetched two iterations before its commit
+  // (one stage ahead left each 64-row stage waiting a full memory round trip; the mid-size
+  // shapes run ~1 block per CU, so nothing else hid it: 8192 x 672 -> 192 at 0.7 TB/s)
+  Stage S0, S1;
   if (m_begin < m_end) {
-    fetch(m_begin);
-    commit(0, m_begin);
+    fetch(S0, m_begin);
+    commit(S0, 0, m_begin);
   }
+  if (m_begin + WT_BM < m_end) fetch(S0, m_begin + WT_BM);
+  if (m_begin + 2 * WT_BM < m_end) fetch(S1, m_begin + 2 * WT_BM);
   __syncthreads();
-  int buf = 0;
-  for (int m0 = m_begin; m0 < m_end; m0 += WT_BM) {
-    const bool more = m0 + WT_BM < m_end;
-    if (more) fetch(m0 + WT_BM);
+  auto iter = [&](Stage& S, int m0, int buf) {
 #pragma unroll
     for (int ks = 0; ks < WT_BM; ks += 32) {
       bf16x8_t af[2], bfr[2];
@@ -879,9 +913,13 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
 #pragma unroll
       for (int m = 0; m < 16; ++m) dbacc += to_f<uint16_t>(col[m * WT_LDM]);
     }
-    if (more) commit(buf ^ 1, m0 + WT_BM);
+    if (m0 + WT_BM < m_end) commit(S, buf ^ 1, m0 + WT_BM);
+    if (m0 + 3 * WT_BM < m_end) fetch(S, m0 + 3 * WT_BM);
     __syncthreads();
-    buf ^= 1;
+  };
+  for (int m0 = m_begin; m0 < m_end; m0 += 2 * WT_BM) {
+    iter(S0, m0, 0);
+    if (m0 + WT_BM < m_end) iter(S1, m0 + WT_BM, 1);
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)

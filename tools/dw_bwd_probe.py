@@ -1,10 +1,12 @@
 """Depthwise backward A/B over the D0 b32 stride-1 shapes (development; EDET_DEV library).
 
 For each shape: the separate path (edet_dwconv_dgrad + edet_dwconv_wgrad + the BN-backward
-reduce of the input) against the fused edet_dwconv_bwd (with the fold), the latter at several
-block targets (development slot 16), and the forward at several block targets (slot 6).
+reduce of the input) against the fused edet_dwconv_bwd (with the fold), and the forward, each
+under several development-slot settings ("slot=value+slot=value", comma-separated variants;
+bwd: 16 = block target, 17 = 2 for two rows in flight; fwd: 6 = block target, 18 = 2).
 
-    EDET_LIB=tensorflow2-machine-vision_amd/lib/libedet_dev.so python tools/dw_bwd_probe.py [targets]
+    EDET_LIB=tensorflow2-machine-vision_amd/lib/libedet_dev.so python tools/dw_bwd_probe.py \
+        "16=0,17=2,16=2048+17=2" "6=0,18=2"
 """
 import os
 import sys
@@ -38,7 +40,13 @@ def timeit(fn, reps=20):
 
 
 def main():
-    targets = [int(t) for t in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 512, 2048, 4096, 8192]
+    def variants(arg):
+        out = []
+        for v in arg.split(","):
+            out.append((v, [tuple(int(a) for a in kv.split("=")) for kv in v.split("+") if kv]))
+        return out
+    bwd_vars = variants(sys.argv[1] if len(sys.argv) > 1 else "16=0")
+    fwd_vars = variants(sys.argv[2] if len(sys.argv) > 2 else "6=0")
     dev = L.lib().fns["edet_dev_set"]
     rng = np.random.default_rng(0)
     s = stream()
@@ -58,19 +66,36 @@ def main():
         row["dgrad"] = timeit(lambda: L.call("edet_dwconv_dgrad", L.BF16, vp(dy), pin.c, C, k, 1, vp(w), vp(dx), pin.c, 0, s))
         row["wgrad"] = timeit(lambda: L.call("edet_dwconv_wgrad", L.BF16, lz.c, pin.c, C, k, 1, vp(dy), pin.c, vp(dw), s))
         row["reduce"] = timeit(lambda: L.call("edet_lazy_bwd_reduce", L.BF16, lz.c, pin.c, C, vp(dx), None, None, acc, s))
-        for t in targets:
-            dev(16, t)
-            row[f"bwd@{t}"] = timeit(lambda: L.call("edet_dwconv_bwd", L.BF16, lz.c, pin.c, C, k, 1, vp(dy), pin.c,
-                                                     vp(w), vp(dx), 0, vp(dw), acc, s))
-        dev(16, 0)
-        for t in targets:
-            dev(6, t)
-            row[f"fwd@{t}"] = timeit(lambda: L.call("edet_dwconv_fwd", L.BF16, lz.c, pin.c, C, k, 1, vp(w), vp(y),
-                                                     pin.c, so, s))
-        dev(6, 0)
+        for name, kvs in bwd_vars:
+            for a, b in kvs:
+                dev(a, b)
+            row[f"bwd@{name}"] = timeit(lambda: L.call("edet_dwconv_bwd", L.BF16, lz.c, pin.c, C, k, 1, vp(dy), pin.c,
+                                                        vp(w), vp(dx), 0, vp(dw), acc, s))
+            for a, _ in kvs:
+                dev(a, 0)
+        for name, kvs in fwd_vars:
+            for a, b in kvs:
+                dev(a, b)
+            row[f"fwd@{name}"] = timeit(lambda: L.call("edet_dwconv_fwd", L.BF16, lz.c, pin.c, C, k, 1, vp(w), vp(y),
+                                                        pin.c, so, s))
+            for a, _ in kvs:
+                dev(a, 0)
+        # every variant must give the default's results bit for bit (same arithmetic order)
+        def outputs(kvs):
+            for a, b in kvs:
+                dev(a, b)
+            dw.zero_()
+            L.call("edet_dwconv_bwd", L.BF16, lz.c, pin.c, C, k, 1, vp(dy), pin.c, vp(w), vp(dx), 0, vp(dw), None, s)
+            L.call("edet_dwconv_fwd", L.BF16, lz.c, pin.c, C, k, 1, vp(w), vp(y), pin.c, None, s)
+            torch.cuda.synchronize()
+            for a, _ in kvs:
+                dev(a, 0)
+            return dx.clone(), y.clone()
+        ref_dx, ref_y = outputs([])
+        same = all(torch.equal(a, b) for _, kvs in bwd_vars + fwd_vars for a, b in zip(outputs(kvs), (ref_dx, ref_y)))
         mb = pin.rows * C * 2 / 1e6
         sep = row["dgrad"] + row["wgrad"] + row["reduce"]
-        print(f"B={B} H={H} C={C} k={k} ({mb:.0f} MB/tensor): separate {sep:.1f} "
+        print(f"B={B} H={H} C={C} k={k} ({mb:.0f} MB/tensor) identical={same}: separate {sep:.1f} "
               f"(dgrad {row['dgrad']:.1f} wgrad {row['wgrad']:.1f} reduce {row['reduce']:.1f}) | "
               + " ".join(f"{n} {v:.1f}" for n, v in row.items() if "@" in n), flush=True)
         for n, v in row.items():
