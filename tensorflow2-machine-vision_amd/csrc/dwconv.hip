@@ -1013,9 +1013,13 @@ struct DwRaw {  // raw input vectors of a fetch, in registers until their commit
   uint32_t ok;
 };
 
-template <typename T, int K, int S, int CPG, bool WG, int P, int PF = 1>
+template <typename T, int K, int S, int CPG, bool WG, int P, int PF = 1, bool RB = false>
 __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
   static_assert(PF == 1 || (PF == 2 && !WG), "two steps in flight: forward only");
+  // RB: the ring holds the transformed input rounded to bf16 (as the GEMMs stage their lazy A
+  // operand) -- half the LDS, so more blocks per CU; forward with bf16 storage only
+  static_assert(!RB || (!WG && sizeof(T) == 2), "bf16 ring: bf16 forward only");
+  using RT = typename std::conditional<RB, uint16_t, float>::type;
   // P output rows per step: they share (P-1)*S... of their K input rows, so each input row of
   // the step is read from LDS once for all of them, and one barrier serves P rows
   constexpr int TW = 8 * CPG, IWS = (TW - 1) * S + K;
@@ -1027,7 +1031,9 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
   constexpr int WORDS = sizeof(T) == 2 ? 1 : 2;
   constexpr int WIN = (CPG - 1) * S + K;
   static_assert(R * IWS >= 8 * K, "wgrad reduction scratch exceeds the ring");
-  __shared__ __attribute__((aligned(16))) float ring[R * IWS * DCB];
+  static_assert(R * IWS * DCB * sizeof(RT) >= 16 * DCB * sizeof(float), "statistics scratch exceeds the ring");
+  __shared__ __attribute__((aligned(16))) RT ringb[R * IWS * DCB];
+  float* ring = reinterpret_cast<float*>(ringb);  // the fp32 view (RB: end-of-block scratch only)
   __shared__ __attribute__((aligned(16))) T ost[WG ? 1 : 2][WG ? 8 : P * TW * DCB];  // fwd output stage
   __shared__ __attribute__((aligned(16))) float dys[WG ? 2 : 1][WG ? P * TW * DCB : 4];  // wgrad dy rows
   __shared__ float2 xf[DCB];
@@ -1126,9 +1132,16 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
       for (int j = 0; j < 8; ++j) vals[j] = lazy_apply(vals[j], a8[j], act) * (g8[j] * m);
       int slot = (r0 % R) + row;
       if (slot >= R) slot -= R;
-      float* d = ring + (slot * IWS + x) * DCB + cv0;
-      reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
-      reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+      RT* d = ringb + (slot * IWS + x) * DCB + cv0;
+      if constexpr (RB) {
+        uint32_t w4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w4[i] = (uint32_t)f2bf(vals[2 * i]) | ((uint32_t)f2bf(vals[2 * i + 1]) << 16);
+        *reinterpret_cast<uint4*>(d) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      } else {
+        reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
+        reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+      }
     }
   };
   // wgrad: the P dy rows of step j; vector e = tid + u*256: row e / (4 TW), pixel, channels
@@ -1227,10 +1240,13 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
         for (int t = 0; t < CPG; ++t) o[p][t] = 0.f;
 #pragma unroll
       for (int ih = 0; ih < NR; ++ih) {  // input row ih feeds output row p through filter row ih - p*S
-        const float* rp = ring + (slot * IWS + gc * CPG * S) * DCB + c;
+        const RT* rp = ringb + (slot * IWS + gc * CPG * S) * DCB + c;
         float win[WIN];
 #pragma unroll
-        for (int x = 0; x < WIN; ++x) win[x] = rp[x * DCB];
+        for (int x = 0; x < WIN; ++x) {
+          if constexpr (RB) win[x] = bf2f(rp[x * DCB]);
+          else win[x] = rp[x * DCB];
+        }
 #pragma unroll
         for (int p = 0; p < P; ++p) {
           const int kh = ih - p * S;
@@ -1365,6 +1381,12 @@ static int launch_dws(DwArgs g, hipStream_t s) {
   if (!WG && dev_knob(18) == 2) {  // development: two steps in flight (forward)
     EDET_LAUNCH((k_dws<T, K, S, CPG, false, P, 2>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
     return check_launch("edet dwconv (rows)");
+  }
+  if constexpr (!WG && sizeof(T) == 2) {
+    if (dev_knob(19) == 1) {  // development: bf16 ring
+      EDET_LAUNCH((k_dws<T, K, S, CPG, false, P, 1, true>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
+      return check_launch("edet dwconv (rows)");
+    }
   }
   EDET_LAUNCH((k_dws<T, K, S, CPG, WG, P>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
   return check_launch("edet dwconv (rows)");
@@ -1691,8 +1713,9 @@ template <typename T, int K, bool FOLD>
 static int dispatch_dwb_cpg(const DwArgs& g, const edet_bngrad64& fold, hipStream_t s) {
   int wmax = 0;
   for (int i = 0; i < g.pin.nseg; ++i) wmax = std::max(wmax, g.pin.W[i]);
-  if (wmax >= 32) return launch_dwb<T, K, 4, FOLD>(g, fold, s);
-  if (wmax >= 16) return launch_dwb<T, K, 2, FOLD>(g, fold, s);
+  const int force = dev_knob(20);  // development: columns per thread (1, 2, 4)
+  if (force == 4 || (!force && wmax >= 32)) return launch_dwb<T, K, 4, FOLD>(g, fold, s);
+  if (force == 2 || (!force && wmax >= 16)) return launch_dwb<T, K, 2, FOLD>(g, fold, s);
   return launch_dwb<T, K, 1, FOLD>(g, fold, s);
 }
 
