@@ -82,7 +82,7 @@ def algorithmic_bytes(name, args, es):
     if name == "edet_conv1x1_wgrad":
         p, K, N = args[2], args[3], args[6]
         return rows(p) * (K + N) * es
-    if name == "edet_dwconv_fwd":
+    if name in ("edet_dwconv_fwd", "edet_dwconv_fwd_squeeze"):
         pin, C, pout = args[2], args[3], args[8]
         return (rows(pin) + rows(pout)) * C * es
     if name == "edet_dwconv_wgrad":
@@ -152,7 +152,7 @@ def shape_tag(name, args):
             return f"M={rows(args[3])} N={args[4]} K={args[6]} acc={args[9]}"
         if name == "edet_conv1x1_wgrad":
             return f"M={rows(args[2])} K={args[3]} N={args[6]} {lazy(args[1])}"
-        if name in ("edet_dwconv_fwd", "edet_dwconv_wgrad"):
+        if name in ("edet_dwconv_fwd", "edet_dwconv_wgrad", "edet_dwconv_fwd_squeeze"):
             return f"in={rows(args[2])} C={args[3]} k={args[4]} s={args[5]}"
         if name == "edet_dwconv_bwd":
             return f"in={rows(args[2])} C={args[3]} k={args[4]} s={args[5]}" + (" fold" if args[12] else "")
@@ -290,17 +290,15 @@ class ProbeTimer:
                 "achieved_GBps": bpl / avg_us * 1e-3 if avg_us > 0 else None, "clock_khz": khz.value}
 
 
-def probe_roofline(model, data, funcs, kernel, steps, es):
+def probe_roofline(step_fn, funcs, kernel, steps, es):
     """Average launch duration of ``kernel`` (launched from the entry points ``funcs``) over
-    ``steps`` replays of a captured step graph that carries the probes, and its algorithmic
-    bytes per launch."""
+    ``steps`` replays of a captured graph of ``step_fn`` (one eager step) that carries the
+    probes, and its algorithmic bytes per launch."""
     pt = ProbeTimer(funcs, kernel, es)
     with pt:
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            model.train_step(data)
+            step_fn()
     g.replay()  # warm
     torch.cuda.synchronize()
     pt.slots.zero_()
@@ -435,6 +433,71 @@ def cpu_baseline(model, anchors, fwd_runs=10, train_runs=3):
                                      f"loss + backward), 7 GT boxes -> {npos} positive anchors, after 1 warm-up"}}
 
 
+def kernel_tables(step_fn, args, el):
+    """One eager ``step_fn`` under HIP events per library call -> (roofline of the kernel with
+    the most step time, timed by probes in a captured graph of the step; roofline_table of every
+    kernel above 2 % of the kernel time; roofline_step; per-entry-point summary)."""
+    es = 2 if args.dtype == "bf16" else 4
+    roofline = None
+    with KernelTimer(es) as kt:
+        step_fn()
+    agg = kt.summary()
+    kag = kt.summary("kernel")
+    if os.environ.get("EDET_KERNEL_DETAIL"):
+        kt.detail(os.environ["EDET_KERNEL_DETAIL"])
+    total_ms = sum(a[1] for a in agg.values())
+    top = sorted(agg.items(), key=lambda kv: -kv[1][1])
+    kernels = {k: {"calls": a[0], "ms": round(a[1], 4), "GBps": (round(a[2] / (a[1] * 1e6), 1) if a[3] and a[1] > 0 else None)}
+               for k, a in top[:12]}
+    log(f"[bench] instrumented eager step: {total_ms:.2f} ms of kernel time")
+    for k, a in top[:12]:
+        log(f"   {k:28s} calls={a[0]:4d} ms={a[1]:8.3f} share={a[1] / total_ms * 100:5.1f}%"
+            + (f" {a[2] / (a[1] * 1e6):8.1f} GB/s" if a[3] else ""))
+    # per device kernel (base name: a kernel's compile-time cases are one kernel, as rocprof
+    # rows are summed in profiles/): every kernel above 2 % of the step's kernel time
+    ktop = sorted(kag.items(), key=lambda kv: -kv[1][1])
+    table = []
+    for k, a in ktop:
+        if a[1] < 0.02 * total_ms:
+            continue
+        gbs = a[2] / (a[1] * 1e6) if a[3] and a[1] > 0 else None
+        tr = pmc_traffic(k, a[0])
+        mf = pmc_mfma(k, a[0])
+        table.append({"kernel": k, "calls": a[0], "ms": round(a[1], 4), "share": round(a[1] / total_ms, 4),
+                      "avg_us": round(a[1] * 1e3 / a[0], 2),
+                      "bytes_per_launch": round(a[2] / a[0]) if a[3] else None,
+                      "achieved_GBps": None if gbs is None else round(gbs, 1),
+                      "frac": None if gbs is None else round(gbs / HBM_PEAK_GBS, 4),
+                      "pmc_traffic_ratio": (round(tr / (a[2] / a[0]), 3) if (tr and a[3] and a[2]) else None),
+                      "mfma_frac": None if mf is None else round(mf, 4),
+                      "entry_points": sorted(a[4])})
+    known = sum(a[2] for a in kag.values() if a[3])
+    step_level = {"algorithmic_bytes": round(known), "ms_per_step": round(el / args.steps * 1e3, 3),
+                  "achieved_GBps": round(known / (el / args.steps) * 1e-9, 1),
+                  "frac": round(known / (el / args.steps) * 1e-9 / HBM_PEAK_GBS, 4),
+                  "note": "sum of every launch's algorithmic bytes (launches with a formula: "
+                          f"{sum(a[0] for a in kag.values() if a[3])} of {sum(a[0] for a in kag.values())}) "
+                          "over the timed step"}
+    # headline roofline: the kernel with the most time in the step, its launches timed by
+    # wall-clock probes inside the captured step graph
+    dom = next(((k, a) for k, a in ktop if a[3]), None)
+    if dom is not None and args.graph:
+        kname, a = dom
+        pr = probe_roofline(step_fn, a[4], kname, args.steps, es)
+        ach = pr["achieved_GBps"]
+        traffic = pmc_traffic(kname, a[0])
+        roofline = {"bound": "hbm", "kernel": kname, "entry_points": sorted(a[4]), "achieved": round(ach, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                    "traffic": None if traffic is None else round(traffic),
+                    "bytes_per_launch": round(pr["bytes_per_launch"]), "avg_launch_us": round(pr["avg_launch_us"], 2),
+                    "launches": pr["launches"], "share_of_kernel_time": round(a[1] / total_ms, 4),
+                    "timing": "wall-clock probes in the captured step graph, "
+                    f"{args.steps} replays ({pr['ms_per_step']:.2f} ms/step with probes)"}
+        log(f"[bench] roofline {kname}: {pr['launches']} launches, avg {pr['avg_launch_us']:.2f} us, "
+            f"{pr['bytes_per_launch'] / 1e6:.2f} MB/launch -> {ach:.1f} GB/s")
+    return roofline, table, step_level, kernels
+
+
 def bench_backbone(args):
     """BASELINE config 2: EfficientNet-B0 backbone forward (inference BN), 224x224, one GPU,
     B = --batch (64 for the config).  Same timing contract as the train step."""
@@ -467,6 +530,9 @@ def bench_backbone(args):
     el = dp.max_over_ranks(ctx, el, dev)
     value = world * B * args.steps / el
     log(f"[bench] backbone B0@224 B={B}/gpu: {args.steps} steps in {el:.3f}s -> {value:.1f} img/s")
+    roofline = table = step_level = kernels = None
+    if args.kernel_timing and rank == 0:
+        roofline, table, step_level, kernels = kernel_tables(lambda: model.backbone(x, training=False), args, el)
     if rank == 0:
         print(json.dumps({
             "metric": "EfficientNet-B0 backbone forward images/sec", "value": round(value, 2), "unit": "images/s",
@@ -475,7 +541,9 @@ def bench_backbone(args):
             "data": "synthetic",
             "config": {"workload": f"efficientnet-b0 backbone forward 224x224, B={B}/GPU, inference BN",
                        "model": "efficientnet-b0", "global_batch": B * world, "image_size": 224,
-                       "parallelism": f"dp{world}", "graph": bool(args.graph)}}), flush=True)
+                       "parallelism": f"dp{world}", "graph": bool(args.graph)},
+            "roofline": roofline, "roofline_table": table, "roofline_step": step_level, "kernels": kernels}),
+            flush=True)
     dp.shutdown(ctx)
 
 
@@ -556,12 +624,8 @@ def main():
     gnorm = float(model.scalars[3])
     log(f"[bench] {args.steps} steps in {el:.3f}s -> {value:.1f} img/s  loss={loss:.4f} gnorm={gnorm:.4f}")
 
-    roofline = None
-    kernels = None
-    table = None
-    step_level = None
+    roofline = kernels = table = step_level = None
     if args.kernel_timing and rank == 0:
-        es = 2 if args.dtype == "bf16" else 4
         # the instrumented steps below run on rank 0 alone: snapshot the optimizer-visible
         # state and restore it afterwards so rank 0 leaves in step with the other replicas
         P = model.P
@@ -570,63 +634,8 @@ def main():
             model.grad_allreduce = None
             model.npos_allreduce = None
         model.eng.overlap = False  # per-kernel attribution: one stream, no concurrency
-        with KernelTimer(es) as kt:
-            model.train_step(data)
+        roofline, table, step_level, kernels = kernel_tables(lambda: model.train_step(data), args, el)
         model.eng.overlap = bool(args.overlap)
-        agg = kt.summary()
-        kag = kt.summary("kernel")
-        if os.environ.get("EDET_KERNEL_DETAIL"):
-            kt.detail(os.environ["EDET_KERNEL_DETAIL"])
-        total_ms = sum(a[1] for a in agg.values())
-        top = sorted(agg.items(), key=lambda kv: -kv[1][1])
-        kernels = {k: {"calls": a[0], "ms": round(a[1], 4), "GBps": (round(a[2] / (a[1] * 1e6), 1) if a[3] and a[1] > 0 else None)}
-                   for k, a in top[:12]}
-        log(f"[bench] instrumented eager step: {total_ms:.2f} ms of kernel time")
-        for k, a in top[:12]:
-            log(f"   {k:28s} calls={a[0]:4d} ms={a[1]:8.3f} share={a[1] / total_ms * 100:5.1f}%"
-                + (f" {a[2] / (a[1] * 1e6):8.1f} GB/s" if a[3] else ""))
-        # per device kernel (base name: a kernel's compile-time cases are one kernel, as rocprof
-        # rows are summed in profiles/): every kernel above 2 % of the step's kernel time
-        ktop = sorted(kag.items(), key=lambda kv: -kv[1][1])
-        table = []
-        for k, a in ktop:
-            if a[1] < 0.02 * total_ms:
-                continue
-            gbs = a[2] / (a[1] * 1e6) if a[3] and a[1] > 0 else None
-            tr = pmc_traffic(k, a[0])
-            mf = pmc_mfma(k, a[0])
-            table.append({"kernel": k, "calls": a[0], "ms": round(a[1], 4), "share": round(a[1] / total_ms, 4),
-                          "avg_us": round(a[1] * 1e3 / a[0], 2),
-                          "bytes_per_launch": round(a[2] / a[0]) if a[3] else None,
-                          "achieved_GBps": None if gbs is None else round(gbs, 1),
-                          "frac": None if gbs is None else round(gbs / HBM_PEAK_GBS, 4),
-                          "pmc_traffic_ratio": (round(tr / (a[2] / a[0]), 3) if (tr and a[3] and a[2]) else None),
-                          "mfma_frac": None if mf is None else round(mf, 4),
-                          "entry_points": sorted(a[4])})
-        known = sum(a[2] for a in kag.values() if a[3])
-        step_level = {"algorithmic_bytes": round(known), "ms_per_step": round(el / args.steps * 1e3, 3),
-                      "achieved_GBps": round(known / (el / args.steps) * 1e-9, 1),
-                      "frac": round(known / (el / args.steps) * 1e-9 / HBM_PEAK_GBS, 4),
-                      "note": "sum of every launch's algorithmic bytes (launches with a formula: "
-                              f"{sum(a[0] for a in kag.values() if a[3])} of {sum(a[0] for a in kag.values())}) "
-                              "over the timed step"}
-        # headline roofline: the kernel with the most time in the step, its launches timed by
-        # wall-clock probes inside the captured step graph
-        dom = next(((k, a) for k, a in ktop if a[3]), None)
-        if dom is not None and args.graph:
-            kname, a = dom
-            pr = probe_roofline(model, data, a[4], kname, args.steps, es)
-            ach = pr["achieved_GBps"]
-            traffic = pmc_traffic(kname, a[0])
-            roofline = {"bound": "hbm", "kernel": kname, "entry_points": sorted(a[4]), "achieved": round(ach, 1),
-                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                        "traffic": None if traffic is None else round(traffic),
-                        "bytes_per_launch": round(pr["bytes_per_launch"]), "avg_launch_us": round(pr["avg_launch_us"], 2),
-                        "launches": pr["launches"], "share_of_kernel_time": round(a[1] / total_ms, 4),
-                        "timing": "wall-clock probes in the captured step graph, "
-                        f"{args.steps} replays ({pr['ms_per_step']:.2f} ms/step with probes)"}
-            log(f"[bench] roofline {kname}: {pr['launches']} launches, avg {pr['avg_launch_us']:.2f} us, "
-                f"{pr['bytes_per_launch'] / 1e6:.2f} MB/launch -> {ach:.1f} GB/s")
         for t, c in saved:
             t.copy_(c)
         P.refresh_compute_copy()

@@ -165,6 +165,14 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
 int edet_dwconv_fwd(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
                     int stride, const void* w, void* y, const edet_pyramid* pout,
                     const edet_statout* stats, edet_stream_t stream);
+/* inference: edet_dwconv_fwd (no statistics) and the SE squeeze of the output in the same pass,
+ *   s[n][c] += mean_hw v(y)  with v = yv's lazy transform act(bn(y)) (yv->x is ignored; no
+ *   gate) into a zeroed fp64 [B][C] -- edet_se_squeeze over y without its own pass.  In
+ *   call(training=False) y's BN uses moving statistics, so its affine is known before the
+ *   launch (layers/se.py:35-39 on mb_conv_block.py:147-150).  Single tensors (nseg 1). */
+int edet_dwconv_fwd_squeeze(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
+                            int stride, const void* w, void* y, const edet_pyramid* pout,
+                            const edet_lazy* yv, double* s, edet_stream_t stream);
 int edet_dwconv_dgrad(int dtype, const void* dy, const edet_pyramid* pout, int C, int k,
                       int stride, const void* w, void* dx, const edet_pyramid* pin,
                       int accumulate, edet_stream_t stream);

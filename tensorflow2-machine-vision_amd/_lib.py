@@ -15,7 +15,7 @@ import torch  # noqa: F401
 from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
 
 MAX_SEG = 5
-ABI_VERSION = 5  # must equal edet_abi_version() of the loaded library (struct layouts)
+ABI_VERSION = 6  # must equal edet_abi_version() of the loaded library (struct layouts)
 OPT_NORM_BLOCKS = 256  # EDET_OPT_NORM_BLOCKS: edet_opt_norm partial-sum slots per quantity
 F32, BF16 = 0, 1
 ACT_NONE, ACT_SWISH = 0, 1
@@ -90,6 +90,7 @@ SIGNATURES = {
     "edet_dwconv_dgrad": [c_int, P, PPyr, c_int, c_int, c_int, P, P, PPyr, c_int, P],
     "edet_dwconv_wgrad": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, PPyr, P, P],
     "edet_dwconv_bwd": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, PPyr, P, P, c_int, P, PBnG, P],
+    "edet_dwconv_fwd_squeeze": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, P, PPyr, PLazy, P, P],
     "edet_stem_fwd": [c_int, P, c_int, c_int, c_int, P, c_int, P, P, P, P],
     "edet_stem_wgrad": [c_int, P, c_int, c_int, c_int, P, c_int, P, P],
     "edet_lazy_bwd_reduce": [c_int, PLazy, PPyr, c_int, P, P, P, PBnG, P],

@@ -30,6 +30,8 @@ struct DwArgs {
   int C, ncb, accumulate, has_stats;
   int tiles_per_wg, tiles_total;
   float* part;  // wgrad: per-chunk partials [chunks][K*K][C] (null: atomics)
+  edet_lazy yv;  // fwd + squeeze: the output's own lazy transform (inference BN, act)
+  double* sq;    // fwd + squeeze: [batch][C] += mean_hw v(y)  (null: no squeeze)
 };
 
 // tiles over a pyramid's spatial extent (per channel block)
@@ -1013,9 +1015,13 @@ struct DwRaw {  // raw input vectors of a fetch, in registers until their commit
   uint32_t ok;
 };
 
-template <typename T, int K, int S, int CPG, bool WG, int P, int PF = 1, bool RB = false>
+template <typename T, int K, int S, int CPG, bool WG, int P, int PF = 1, bool RB = false, bool SQ = false>
 __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
   static_assert(PF == 1 || (PF == 2 && !WG), "two steps in flight: forward only");
+  // SQ (inference): the SE squeeze of the output's value v(y) = act(bn(y)) in the epilogue --
+  // with moving statistics bn's affine is known before the launch (layers/se.py:36 on
+  // mb_conv_block.py:147-150 in call(training=False)), so the edet_se_squeeze pass is not needed
+  static_assert(!SQ || !WG, "squeeze: forward only");
   // RB: the ring holds the transformed input rounded to bf16 (as the GEMMs stage their lazy A
   // operand) -- half the LDS, so more blocks per CU; forward with bf16 storage only
   static_assert(!RB || (!WG && sizeof(T) == 2), "bf16 ring: bf16 forward only");
@@ -1031,7 +1037,7 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
   constexpr int WORDS = sizeof(T) == 2 ? 1 : 2;
   constexpr int WIN = (CPG - 1) * S + K;
   static_assert(R * IWS >= 8 * K, "wgrad reduction scratch exceeds the ring");
-  static_assert(R * IWS * DCB * sizeof(RT) >= 16 * DCB * sizeof(float), "statistics scratch exceeds the ring");
+  static_assert(R * IWS * DCB * sizeof(RT) >= 24 * DCB * sizeof(float), "statistics scratch exceeds the ring");
   __shared__ __attribute__((aligned(16))) RT ringb[R * IWS * DCB];
   float* ring = reinterpret_cast<float*>(ringb);  // the fp32 view (RB: end-of-block scratch only)
   __shared__ __attribute__((aligned(16))) T ost[WG ? 1 : 2][WG ? 8 : P * TW * DCB];  // fwd output stage
@@ -1077,6 +1083,11 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
     xf[tid] = cc < C ? bn_affine(g.lz.bn, seg, cc, 1.f / (float)seg_rows(g.pin, seg)) : make_float2(1.f, 0.f);
     gt[tid] = (g.lz.gate && cc < C) ? g.lz.gate[(size_t)n * C + cc] : 1.f;
   }
+  float2 ya = make_float2(1.f, 0.f);  // SQ: the output's affine for this thread's channel
+  if constexpr (SQ) {
+    if (cvalid) ya = bn_affine(g.yv.bn, seg, c0 + c, 1.f / (float)seg_rows(g.pout, seg));
+  }
+  float z = 0.f;  // SQ: sum of v(y) over the block's outputs of channel c
 
   // input rows [r0, r0 + nr) of the block (relative to iy0) <-> registers <-> ring slots
   auto fetch = [&](auto& rg, int r0, int nr) {
@@ -1263,8 +1274,14 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
         const bool rowok = j * P + p < nrows;
 #pragma unroll
         for (int t = 0; t < CPG; ++t) {
-          ost[j & 1][(p * TW + gc * CPG + t) * DCB + c] = from_f<T>(o[p][t]);
-          if (rowok && cvalid && ox0 + gc * CPG + t < OW) { s += o[p][t]; q += o[p][t] * o[p][t]; }
+          const T ov = from_f<T>(o[p][t]);
+          ost[j & 1][(p * TW + gc * CPG + t) * DCB + c] = ov;
+          if (rowok && cvalid && ox0 + gc * CPG + t < OW) {
+            s += o[p][t];
+            q += o[p][t] * o[p][t];
+            // the squeeze reads y as stored, as edet_se_squeeze would
+            if constexpr (SQ) z += lazy_apply(to_f<T>(ov), ya, g.yv.act);
+          }
         }
       }
     } else {
@@ -1317,6 +1334,17 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
         for (int k = 0; k < 8; ++k) { ss += red[k * DCB + tid]; qq += red[(8 + k) * DCB + tid]; }
         stat_add(g.stats.sum[seg] + c0 + tid, (double)ss);
         stat_add(g.stats.sq[seg] + c0 + tid, (double)qq);
+      }
+    }
+    if constexpr (SQ) {  // (after the statistics' reads of the scratch: its own rows 16..23)
+      float* red = ring + 16 * DCB;
+      red[gc * DCB + c] = z;
+      __syncthreads();
+      if (tid < DCB && c0 + tid < C) {
+        float zz = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) zz += red[k * DCB + tid];
+        atomicAdd(g.sq + (size_t)n * C + c0 + tid, (double)zz / (double)(OH * OW));
       }
     }
   } else {
@@ -1378,6 +1406,12 @@ static int launch_dws(DwArgs g, hipStream_t s) {
   if (total == 0) return EDET_OK;
   pl.cb_inner = dev_knob(15) != 2;
   EDET_REQUIRE(total < (1L << 31), "dwconv: grid too large");
+  if constexpr (!WG) {
+    if (g.sq) {
+      EDET_LAUNCH((k_dws<T, K, S, CPG, false, P, 1, false, true>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
+      return check_launch("edet dwconv (rows, squeeze)");
+    }
+  }
   if (!WG && dev_knob(18) == 2) {  // development: two steps in flight (forward)
     EDET_LAUNCH((k_dws<T, K, S, CPG, false, P, 2>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
     return check_launch("edet dwconv (rows)");
@@ -1866,6 +1900,30 @@ int edet_dwconv_fwd(int dtype, const edet_lazy* x, const edet_pyramid* pin, int 
   g.has_stats = stats != nullptr;
   if (stats) g.stats = *stats;
   EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_dw<T>(0, k, stride, g, (hipStream_t)stream); });
+}
+
+int edet_dwconv_fwd_squeeze(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
+                            int stride, const void* w, void* y, const edet_pyramid* pout,
+                            const edet_lazy* yv, double* s, edet_stream_t stream) {
+  EDET_REQUIRE(x && w && y && yv && s, "dwconv_fwd_squeeze: null argument");
+  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0, "dwconv_fwd_squeeze: need C%%8==0, ld%%8==0");
+  EDET_REQUIRE(yv->gate == nullptr, "dwconv_fwd_squeeze: the squeezed value is the pre-gate one");
+  EDET_REQUIRE(pin && pin->nseg == 1, "dwconv_fwd_squeeze: single tensors only (the SE is per image)");
+  int rc = check_pyrs(pin, pout, k, stride);
+  if (rc) return rc;
+  if ((k != 3 && k != 5) || (stride != 1 && stride != 2)) {
+    set_error("dwconv_fwd_squeeze: unsupported kernel %d stride %d", k, stride);
+    return EDET_EUNSUPPORTED;
+  }
+  DwArgs g{};
+  g.x = x->x; g.w = w; g.y = y; g.lz = *x; g.pin = *pin; g.pout = *pout; g.C = C;
+  g.yv = *yv; g.sq = s; g.ncb = cdiv(C, DCB);
+  // always the row-streaming form: the only one with the squeeze epilogue
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    const hipStream_t st = (hipStream_t)stream;
+    if (k == 3) return stride == 1 ? dispatch_dws<T, 3, 1, false>(g, st) : dispatch_dws<T, 3, 2, false>(g, st);
+    return stride == 1 ? dispatch_dws<T, 5, 1, false>(g, st) : dispatch_dws<T, 5, 2, false>(g, st);
+  });
 }
 
 int edet_dwconv_dgrad(int dtype, const void* dy, const edet_pyramid* pout, int C, int k,

@@ -58,6 +58,8 @@ class EfficientDetNet:
         self.last_outputs = None
         # SE-gated depthwise outputs written once before the project conv (ops.materialize)
         self.materialize_se = True
+        # inference: SE squeeze in the depthwise epilogue (edet_dwconv_fwd_squeeze)
+        self.fused_squeeze = True
 
     # ------------------------------------------------------------------ parameters
     def _register(self):
@@ -260,9 +262,12 @@ class EfficientDetNet:
         if sp.expand_ratio != 1:
             x = ops.conv1x1(eng, P, x, b["expand_w"], sp.expanded_filters, bns=[b["bn0"]], act=L.ACT_SWISH,
                             name=f"{pre}/expand")
+        # inference: the SE squeeze rides in the depthwise epilogue (BN affine from moving
+        # statistics); training needs the batch statistics of the whole output first
+        svec = None if eng.training or not self.fused_squeeze else eng.zeros64(x.pyr.batch, x.C)
         d = ops.dwconv(eng, P, x, f"{pre}/depthwise_conv2d/depthwise_kernel", sp.kernel_size, sp.stride,
-                       bns=[b["bn1"]], act=L.ACT_SWISH, name=f"{pre}/dw")
-        ops.squeeze_excite(eng, P, d, f"{pre}/se", sp.se_filters)
+                       bns=[b["bn1"]], act=L.ACT_SWISH, name=f"{pre}/dw", squeeze=svec)
+        ops.squeeze_excite(eng, P, d, f"{pre}/se", sp.se_filters, svec=svec)
         if self.materialize_se:
             d = ops.materialize(eng, d, name=f"{pre}/se_out")
         return ops.conv1x1(eng, P, d, b["project_w"], sp.output_filters, bns=[b["bn2"]], name=f"{pre}/project")

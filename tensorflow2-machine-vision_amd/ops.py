@@ -164,14 +164,22 @@ FUSED_DW_BWD = os.environ.get("EDET_FUSED_DW", "1") != "0"
 FOLD_DW_BN = os.environ.get("EDET_FOLD_DW_BN", "1") != "0"
 
 def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
-           bns: Optional[List[BNParam]] = None, act: int = L.ACT_NONE, name: str = "") -> Act:
+           bns: Optional[List[BNParam]] = None, act: int = L.ACT_NONE, name: str = "",
+           squeeze: Optional[torch.Tensor] = None) -> Act:
+    """Depthwise conv.  `squeeze` (inference only): a zeroed fp64 [B][C] that receives the SE
+    squeeze mean_hw act(bn(y)) of the output from the same launch (edet_dwconv_fwd_squeeze)."""
     C = x.C
     x.consume()
     pout = x.pyr.strided(stride)
     y = eng.empty(pout.rows, C)
-    L.call("edet_dwconv_fwd", eng.dt, x.lazy(), x.pyr.c, C, k, stride, vp(P.wcv(wname)), vp(y), pout.c,
-           _stats_out(eng, bns), stream())
     out = Act(y, pout, C, bns, act, training=eng.training, name=name)
+    if squeeze is not None:
+        assert not eng.training, "the fused squeeze needs y's BN affine before the launch (moving statistics)"
+        L.call("edet_dwconv_fwd_squeeze", eng.dt, x.lazy(), x.pyr.c, C, k, stride, vp(P.wcv(wname)), vp(y),
+               pout.c, out.lazy(), vp(squeeze), stream())
+    else:
+        L.call("edet_dwconv_fwd", eng.dt, x.lazy(), x.pyr.c, C, k, stride, vp(P.wcv(wname)), vp(y), pout.c,
+               _stats_out(eng, bns), stream())
 
     def bwd():
         rec = eng.tape.take(out)
@@ -206,14 +214,17 @@ def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
 
 
 # --------------------------------------------------------------------------- SE
-def squeeze_excite(eng: Engine, P: ParamStore, x: Act, prefix: str, R: int):
-    """Attach the SE gate to x (the swish(BN(dw)) value) in place: v -> v * sigmoid(...)."""
+def squeeze_excite(eng: Engine, P: ParamStore, x: Act, prefix: str, R: int,
+                   svec: Optional[torch.Tensor] = None):
+    """Attach the SE gate to x (the swish(BN(dw)) value) in place: v -> v * sigmoid(...).
+    `svec`: the squeeze already taken by the producer (dwconv(..., squeeze=svec))."""
     assert x.pyr.nseg == 1 and x.gate is None
     B, C = x.pyr.batch, x.C
     HW = x.pyr.H * x.pyr.W
     s = stream()
-    svec = eng.zeros64(B, C)  # fp64 squeeze (edet.h)
-    L.call("edet_se_squeeze", eng.dt, x.lazy(), B, HW, C, vp(svec), s)
+    if svec is None:
+        svec = eng.zeros64(B, C)  # fp64 squeeze (edet.h)
+        L.call("edet_se_squeeze", eng.dt, x.lazy(), B, HW, C, vp(svec), s)
     z1 = torch.empty((B, R), dtype=torch.float32, device=eng.device)
     gate = torch.empty((B, C), dtype=torch.float32, device=eng.device)
     w1, b1 = P.view(prefix + "/conv2d/kernel"), P.view(prefix + "/conv2d/bias")

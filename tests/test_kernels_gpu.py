@@ -317,6 +317,48 @@ def test_lazy_backward(dt, C, act, gate, dsq, scale, nseg):
         close(grads[sg][0], ga.grad, dt, scale=n ** 0.5 * 2)
 
 
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("k,s,H,W,C", [(3, 1, 16, 16, 32), (3, 2, 17, 13, 96), (5, 2, 20, 9, 144),
+                                       (5, 1, 11, 12, 40), (3, 1, 8, 9, 480), (5, 1, 10, 11, 1152),
+                                       (3, 1, 6, 7, 2112), (5, 2, 9, 8, 672), (3, 1, 40, 70, 64)])
+def test_dwconv_fwd_squeeze(dt, k, s, H, W, C):
+    """Inference (layers/se.py:36 on mb_conv_block.py:147-150, call(training=False)):
+    edet_dwconv_fwd_squeeze writes y = dwconv(v(x)) and, from the same pass, the SE squeeze
+    mean_hw swish(bn(y)) of y as stored, with y's BN on moving statistics.  y against the fp64
+    stencil; the squeeze against edet_se_squeeze over the y it wrote (same inputs, only the
+    fp32 partial-sum order differs) and against fp64 of that y."""
+    rng = np.random.default_rng(k * 1000 + s * 100 + C)
+    B = 3
+    pin = Pyr(B, [(H, W)])
+    pout = pin.strided(s)
+    OH, OW = pout.sizes[0]
+    x = pyr_data(rng, pin, C, dt)
+    lz = LazyDesc(x, pin, C, bn=make_bn(x, pin, C, rng), act=1)
+    w = g(rnd(rng, k * k, C, scale=0.3), dt)
+    y = torch.empty(pout.rows, C, dtype=TDT[dt], device=DEV)
+    # y's BatchNorm in inference form: sums that give the moving mean / variance over pout.rows
+    n = pout.rows
+    mean, var = rng.normal(0, 0.3, C), rng.uniform(0.2, 2.0, C)
+    ybn = [(torch.tensor(mean * n, dtype=torch.float64, device=DEV),
+            torch.tensor((var + mean * mean) * n, dtype=torch.float64, device=DEV),
+            torch.tensor(rng.uniform(0.5, 1.5, C), dtype=torch.float32, device=DEV),
+            torch.tensor(rng.uniform(-0.5, 0.5, C), dtype=torch.float32, device=DEV))]
+    ylz = LazyDesc(y, pout, C, bn=ybn, act=1)
+    sq = zeros64(B, C)
+    L.call("edet_dwconv_fwd_squeeze", DT[dt], lz.c, pin.c, C, k, s, vp(w), vp(y), pout.c, ylz.c, vp(sq), stream())
+    ref = dw_ref(lz.cpu_value(), pin, k, s, w.double().cpu())
+    close(y, ref, dt)
+    sep = zeros64(B, C)
+    L.call("edet_se_squeeze", DT[dt], ylz.c, B, OH * OW, C, vp(sep), stream())
+    close(sq, sep, "f32", rtol=1e-5, atol=1e-6)
+    close(sq, ylz.cpu_value().view(B, OH * OW, C).mean(1), "f32", rtol=1e-5, atol=1e-5)
+    # a gate on the squeezed value is refused (the squeeze is of the pre-gate value)
+    bad = LazyDesc(y, pout, C, bn=ybn, act=1, gate=zeros(B, C))
+    with pytest.raises(L.EdetError):
+        L.call("edet_dwconv_fwd_squeeze", DT[dt], lz.c, pin.c, C, k, s, vp(w), vp(y), pout.c, bad.c, vp(sq),
+               stream())
+
+
 # ----------------------------------------------------------------- SE
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("C,R", [(96, 4), (1152, 48), (520, 100)])

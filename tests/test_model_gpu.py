@@ -108,6 +108,32 @@ def test_forward_parity_fp32(training):
         assert rel_err(classes[l].cpu(), rc[l].detach()) < 1e-3, l
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_inference_fused_squeeze_equals_separate_pass(dtype):
+    """call(training=False) takes the SE squeeze from the depthwise epilogue
+    (edet_dwconv_fwd_squeeze); the same model with the separate edet_se_squeeze pass gives the
+    same outputs (the two differ only in the fp32 partial-sum order of the squeeze, and in the
+    depthwise form of a few layers: within fp32 rounding, a few bf16 ulp)."""
+    m = EfficientDetNet(efficientnet_b0_blocks(), cfg(), dtype=dtype, seed=3)
+    sd = m.state_dict()
+    rng = np.random.default_rng(8)
+    for k in sd:
+        if k.endswith("moving_mean"):
+            sd[k] = rng.normal(0, 0.3, sd[k].shape).astype(np.float32)
+        elif k.endswith("moving_variance"):
+            sd[k] = rng.uniform(0.5, 2.0, sd[k].shape).astype(np.float32)
+    m.load_state_dict(sd)
+    x = torch.tensor(synth(2)[0]).cuda()
+    outs = []
+    for fused in (True, False):
+        m.fused_squeeze = fused
+        b, c = m.call(x, training=False)
+        outs.append([t.float().cpu().clone() for t in list(b) + list(c)])
+    tol = 1e-4 if dtype == "f32" else 3e-2
+    for a, r in zip(*outs):
+        assert rel_err(a, r) < tol
+
+
 def _train_model(dtype, seed=1):
     c = cfg()
     anchors = Anchors(c.min_level, c.max_level, (SIZE, SIZE), c.num_scales, c.aspect_ratios, c.anchor_scale)
