@@ -520,39 +520,74 @@ __global__ __launch_bounds__(256) void k_se_dz1(int B, int C, int R, const float
   }
 }
 
-// backward, pass 2 (dw2 / dw1: a half-wave per (c, r) over the images; dsq, db2, db1: a thread
-// per element):
+// backward, pass 2 (dw2 / dw1: a block per 32 channels, the images staged in LDS; dsq, db2,
+// db1: a thread per element):
 //   dw2[c][r] += sum_n dz2[n][c] swish(z1[n][r])     dw1[r][c] += sum_n dz1[n][r] s[n][c]
 //   db2[c]    += sum_n dz2[n][c]                     db1[r]    += sum_n dz1[n][r]
 //   dsq[n][c]  = sum_r dz1[n][r] w1[r][c] / HW
+// The weight gradients are (C x B)(B x R) products: the block stages dz2 and s for its 32
+// channels and swish(z1), dz1 for all R, 32 images at a time (coalesced rows), and thread
+// (c, rg) accumulates r = rg, rg + 8, ... in registers (the former half-wave per (c, r) read
+// gate / dgate / s with stride C across its lanes: 12 us per launch at C = 1152, R = 48).
+constexpr int SEW_NB = 32, SEW_C = 32;
+__host__ __device__ inline size_t se_wgrad_lds(int R) { return (size_t)(2 * SEW_NB * SEW_C + 2 * SEW_NB * R) * sizeof(float); }
 __device__ __forceinline__ void k_se_wgrad_body(int B, int C, int R, int HW, int nA, const double* s,
                                                 const float* z1, const float* gate, const double* dgate,
                                                 const float* dz1, const float* w1, float* dw1, float* db1,
                                                 float* dw2, float* db2, float* dsq) {
   if ((int)blockIdx.x < nA) {
-    // dw2[c][r], dw1[r][c]: one half-wave per (c, r), its 32 lanes over the images, then a
-    // 32-lane tree (the per-thread loop over B serialised B dependent load rounds)
-    const int half = threadIdx.x >> 5, ln = threadIdx.x & 31;
-    const int item = blockIdx.x * 8 + half;
-    float a2 = 0.f, a1 = 0.f;
-    const bool live = item < C * R;
-    const int c = live ? item / R : 0, r = live ? item - c * R : 0;
-    if (live)
-      for (int n = ln; n < B; n += 32) {
-        const float gv = gate[(size_t)n * C + c];
-        const float d2 = (float)dgate[(size_t)n * C + c] * gv * (1.f - gv);
-        const float z = z1[(size_t)n * R + r];
-        a2 += d2 * (z * sigmoidf_(z));
-        a1 += dz1[(size_t)n * R + r] * (float)s[(size_t)n * C + c];
+    extern __shared__ float sew[];
+    float* d2s = sew;                     // [NB][32] dz2
+    float* svs = d2s + SEW_NB * SEW_C;    // [NB][32] s
+    float* zss = svs + SEW_NB * SEW_C;    // [NB][R]  swish(z1)
+    float* dzs = zss + SEW_NB * R;        // [NB][R]  dz1
+    const int tid = threadIdx.x, cl = tid & 31, rg = tid >> 5;
+    const int c0 = blockIdx.x * SEW_C, c = c0 + cl;
+    for (int rb = 0; rb < R; rb += 64) {
+      float a2[8], a1[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a2[i] = a1[i] = 0.f;
+      for (int n0 = 0; n0 < B; n0 += SEW_NB) {
+        const int nb = min(SEW_NB, B - n0);
+        __syncthreads();
+        for (int e = tid; e < SEW_NB * SEW_C; e += 256) {  // clamped addresses, values selected
+          const int n = e >> 5, cc = c0 + (e & 31);
+          const bool ok = n < nb && cc < C;
+          const size_t i = ok ? (size_t)(n0 + n) * C + cc : 0;
+          const float gv = gate[i];
+          const double dg = dgate[i], sv = s[i];
+          d2s[e] = ok ? (float)dg * gv * (1.f - gv) : 0.f;
+          svs[e] = ok ? (float)sv : 0.f;
+        }
+        for (int e = tid; e < SEW_NB * R; e += 256) {
+          const int n = e / R;
+          const bool ok = n < nb;
+          const size_t i = ok ? (size_t)n0 * R + e : 0;
+          const float z = z1[i], d = dz1[i];
+          zss[e] = ok ? z * sigmoidf_(z) : 0.f;
+          dzs[e] = ok ? d : 0.f;
+        }
+        __syncthreads();
+        for (int n = 0; n < nb; ++n) {
+          const float d2 = d2s[n * SEW_C + cl], sv = svs[n * SEW_C + cl];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int r = rb + rg + 8 * i;
+            if (r < R) {
+              a2[i] += d2 * zss[n * R + r];
+              a1[i] += dzs[n * R + r] * sv;
+            }
+          }
+        }
       }
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
-      a2 += __shfl_xor(a2, o, 64);
-      a1 += __shfl_xor(a1, o, 64);
-    }
-    if (live && ln == 0) {
-      dw2[(size_t)c * R + r] += a2;
-      dw1[(size_t)r * C + c] += a1;
+      for (int i = 0; i < 8; ++i) {
+        const int r = rb + rg + 8 * i;
+        if (r < R && c < C) {
+          dw2[(size_t)c * R + r] += a2[i];
+          dw1[(size_t)r * C + c] += a1[i];
+        }
+      }
     }
     return;
   }
@@ -886,9 +921,10 @@ int edet_se_bwd_bn(int B, int C, int R, int HW, const double* s, const float* z1
                    acc->dgamma[0] && acc->dbeta[0],
                "se_bwd_bn: null argument");
   hipStream_t st = (hipStream_t)stream;
+  EDET_REQUIRE(se_wgrad_lds(R) <= 64 * 1024, "se_bwd_bn: R = %d too large", R);
   EDET_LAUNCH(k_se_dz1, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, z1, gate, dgate, w2, dz1);
-  const int nA = cdiv(C * R, 8), nB = cdiv(std::max(B * C, std::max(C, R)), 256);
-  EDET_LAUNCH(k_se_wgrad_bn, dim3(nA + nB + cdiv(C, 8)), dim3(256), 0, st, B, C, R, HW, nA, nA + nB, s, z1, gate,
+  const int nA = cdiv(C, SEW_C), nB = cdiv(std::max(B * C, std::max(C, R)), 256);
+  EDET_LAUNCH(k_se_wgrad_bn, dim3(nA + nB + cdiv(C, 8)), dim3(256), se_wgrad_lds(R), st, B, C, R, HW, nA, nA + nB, s, z1, gate,
               dgate, dz1, w1, dw1, db1, dw2, db2, dsq, sums5, acc->dgamma[0], acc->dbeta[0]);
   return check_launch("edet se_bwd_bn");
 }
@@ -900,9 +936,10 @@ int edet_se_bwd(int B, int C, int R, int HW, const double* s, const float* z1,
   EDET_REQUIRE(s && z1 && gate && dgate && w1 && w2 && dw1 && db1 && dw2 && db2 && dsq && dz1,
                "se_bwd: null argument");
   hipStream_t st = (hipStream_t)stream;
+  EDET_REQUIRE(se_wgrad_lds(R) <= 64 * 1024, "se_bwd: R = %d too large", R);
   EDET_LAUNCH(k_se_dz1, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, z1, gate, dgate, w2, dz1);
-  const int nA = cdiv(C * R, 8), nB = cdiv(std::max(B * C, std::max(C, R)), 256);
-  EDET_LAUNCH(k_se_wgrad, dim3(nA + nB), dim3(256), 0, st, B, C, R, HW, nA, s, z1, gate, dgate, dz1, w1,
+  const int nA = cdiv(C, SEW_C), nB = cdiv(std::max(B * C, std::max(C, R)), 256);
+  EDET_LAUNCH(k_se_wgrad, dim3(nA + nB), dim3(256), se_wgrad_lds(R), st, B, C, R, HW, nA, s, z1, gate, dgate, dz1, w1,
                      dw1, db1, dw2, db2, dsq);
   return check_launch("edet se_bwd");
 }

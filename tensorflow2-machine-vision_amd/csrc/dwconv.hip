@@ -34,6 +34,20 @@ struct DwArgs {
   double* sq;    // fwd + squeeze: [batch][C] += mean_hw v(y)  (null: no squeeze)
 };
 
+// The N filter taps of channel ch (stride C between taps) into fp32 registers.  Every load is
+// issued unconditionally from a clamped channel and zeroed after: a select-predicated load is
+// compiled as a branch around it with its own vmcnt(0), i.e. N serial L2 round trips in every
+// block's prologue (25 at k5).
+template <int N, typename T>
+__device__ __forceinline__ void load_taps(float (&wr)[N], const T* w, int C, int ch, bool valid) {
+  const T* p = w + (valid ? ch : 0);
+  T raw[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) raw[i] = p[(size_t)i * C];
+#pragma unroll
+  for (int i = 0; i < N; ++i) wr[i] = valid ? to_f<T>(raw[i]) : 0.f;
+}
+
 // tiles over a pyramid's spatial extent (per channel block)
 __device__ __forceinline__ void locate_tile(const edet_pyramid& p, int id, int& seg, int& n, int& ty, int& tx) {
   seg = 0;
@@ -151,8 +165,7 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
   const bool cvalid = (c0 + c) < g.C;
   float wr[K * K];
   const T* Wp = (const T*)g.w;
-#pragma unroll
-  for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(Wp[(size_t)i * g.C + c0 + c]) : 0.f;
+  load_taps(wr, Wp, g.C, c0 + c, cvalid);
   T* Y = (T*)g.y;
   float s = 0.f, q = 0.f;
   int cur_seg = -1, xf_seg = -1, xf_img = -1;
@@ -288,8 +301,7 @@ __global__ __launch_bounds__(256) void k_dw_dgrad(DwArgs g) {
   float wr[K * K];
   const T* Wp = (const T*)g.w;
   const bool cvalid = (c0 + c) < g.C;
-#pragma unroll
-  for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(Wp[(size_t)i * g.C + c0 + c]) : 0.f;
+  load_taps(wr, Wp, g.C, c0 + c, cvalid);
   __syncthreads();
 
   const int iy = iy0 + r;
@@ -444,8 +456,7 @@ __global__ __launch_bounds__(256) void k_dw3(DwArgs g) {
   float wr[WGRAD ? 1 : K * K];
   if constexpr (!WGRAD) {
     const T* Wp = (const T*)g.w;
-#pragma unroll
-    for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(Wp[(size_t)i * C + c0 + c]) : 0.f;
+    load_taps(wr, Wp, C, c0 + c, cvalid);
   }
   const T* X = (const T*)g.x;
   const T* DY = (const T*)g.dy;
@@ -1074,10 +1085,7 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
   const bool cvalid = c0 + c < C;
 
   float wr[WG ? 1 : K * K];
-  if constexpr (!WG) {
-#pragma unroll
-    for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(((const T*)g.w)[(size_t)i * C + c0 + c]) : 0.f;
-  }
+  if constexpr (!WG) load_taps(wr, (const T*)g.w, C, c0 + c, cvalid);
   if (tid < DCB) {
     const int cc = c0 + tid;
     xf[tid] = cc < C ? bn_affine(g.lz.bn, seg, cc, 1.f / (float)seg_rows(g.pin, seg)) : make_float2(1.f, 0.f);
@@ -1497,8 +1505,7 @@ __global__ __launch_bounds__(256) void k_dwb(DwArgs g, DwsPlan pl, edet_bngrad64
   const bool cvalid = c0 + c < C;
 
   float wr[K * K];
-#pragma unroll
-  for (int i = 0; i < K * K; ++i) wr[i] = cvalid ? to_f<T>(((const T*)g.w)[(size_t)i * C + c0 + c]) : 0.f;
+  load_taps(wr, (const T*)g.w, C, c0 + c, cvalid);
   const float inv = 1.f / (float)seg_rows(g.pin, seg);
   if (tid < DCB) {
     const int cc = c0 + tid;
@@ -1712,17 +1719,265 @@ __global__ __launch_bounds__(256) void k_dwb(DwArgs g, DwsPlan pl, edet_bngrad64
   }
 }
 
+// k_dwb with two output rows per step: every ring row's windows are read from LDS once for both
+// rows (K + 1 ring rows feed 2 outputs instead of K feeding 1), and one barrier serves both.
+// Ring R = K + 3: step j commits rows j+K-1, j+K into the slots of rows j-4, j-3, last read by
+// step j-4, which step j-2's barrier separates from these writes.
+template <typename T, int K, int CPG, bool FOLD>
+__global__ __launch_bounds__(256) void k_dwb2(DwArgs g, DwsPlan pl, edet_bngrad64 fold) {
+  constexpr int P = (K - 1) / 2;
+  constexpr int TW = 8 * CPG, IWS = TW + K - 1;
+  constexpr int R = K + 3;
+  constexpr int RV = IWS * (DCB / 8);
+  constexpr int WORDS = sizeof(T) == 2 ? 1 : 2;
+  constexpr int WIN = CPG + K - 1;
+  constexpr int RINGF = R * IWS * DCB;
+  constexpr int RINGB = RINGF * 4 + R * IWS * DCB * (int)sizeof(T);
+  constexpr int REDB = (K * K + 2) * 8 * DCB * 4;
+  constexpr int LDSB = RINGB > REDB ? RINGB : REDB;
+  __shared__ __attribute__((aligned(16))) char smem[LDSB];
+  float* vring = reinterpret_cast<float*>(smem);
+  T* dring = reinterpret_cast<T*>(smem + RINGF * 4);
+  __shared__ float2 xf[DCB];
+  __shared__ float gt[DCB];
+  const int tid = threadIdx.x, c = tid & 31, gc = tid >> 5;
+
+  int id = xcd_remap(blockIdx.x, gridDim.x), seg = 0;
+  while (seg < g.pout.nseg - 1 && id >= pl.nblk[seg]) id -= pl.nblk[seg++];
+  const int cb = id % g.ncb;
+  id /= g.ncb;
+  const int strip = id % pl.strips[seg];
+  id /= pl.strips[seg];
+  const int rb = id % pl.rowblk[seg];
+  const int n = id / pl.rowblk[seg];
+  const int c0 = cb * DCB, C = g.C;
+  const int H = g.pin.H[seg], W = g.pin.W[seg];
+  const int r0 = rb * pl.TH, x0 = strip * TW;
+  const int nrows = min(pl.TH, H - r0);
+  const T* X = (const T*)g.x + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * g.lz.ld + c0;
+  const T* DY = (const T*)g.dy + ((size_t)g.pout.row_off[seg] + (size_t)n * H * W) * C + c0;
+  T* DX = (T*)g.dx + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * C + c0;
+  const bool cvalid = c0 + c < C;
+
+  float wr[K * K];
+  load_taps(wr, (const T*)g.w, C, c0 + c, cvalid);
+  const float inv = 1.f / (float)seg_rows(g.pin, seg);
+  if (tid < DCB) {
+    const int cc = c0 + tid;
+    xf[tid] = cc < C ? bn_affine(g.lz.bn, seg, cc, inv) : make_float2(1.f, 0.f);
+    gt[tid] = (g.lz.gate && cc < C) ? g.lz.gate[(size_t)n * C + cc] : 1.f;
+  }
+  float2 myaf = make_float2(1.f, 0.f), mymr = make_float2(0.f, 1.f);
+  if constexpr (FOLD) {
+    if (cvalid) {
+      myaf = bn_affine(g.lz.bn, seg, c0 + c, inv);
+      mymr = bn_mean_rstd(g.lz.bn, seg, c0 + c, inv);
+    }
+  }
+
+  // as k_dwb: dy vector e of a fetch -> thread e, x vector e -> thread 255 - e
+  auto fetch = [&](auto& rg, auto& rx, int t0, int nt) {
+    constexpr int NV = std::remove_reference_t<decltype(rg)>::NV;
+    rg.ok = 0;
+    rx.ok = 0;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const int v = (side ? 255 - tid : tid) + u * 256;
+        const int row = v / RV, e = v - row * RV, xx = e >> 2, cv = (e & 3) * 8;
+        const int q = r0 - P + t0 + row, gx = x0 - P + xx;
+        const bool in = row < nt && q >= 0 && q < H && gx >= 0 && gx < W && c0 + cv < C;
+        const uint32_t pix = in ? (uint32_t)(q * W + gx) : 0u;
+        const uint4* src = reinterpret_cast<const uint4*>(side ? X + (size_t)pix * g.lz.ld + (in ? cv : 0)
+                                                               : DY + (size_t)pix * C + (in ? cv : 0));
+        auto& dst = side ? rx : rg;
+        dst.v[u][0] = src[0];
+        if constexpr (WORDS == 2) dst.v[u][1] = src[1];
+        dst.ok |= (uint32_t)in << u;
+      }
+    }
+  };
+  auto commit = [&](const auto& rg, const auto& rx, int t0, int nt) {
+    constexpr int NV = std::remove_reference_t<decltype(rg)>::NV;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int v = tid + u * 256;
+      const int row = v / RV, e = v - row * RV, xx = e >> 2;
+      if (row >= nt) break;
+      const bool in = (rg.ok >> u) & 1;
+      T* d = dring + (((t0 + row) % R) * IWS + xx) * DCB + (e & 3) * 8;
+#pragma unroll
+      for (int w = 0; w < WORDS; ++w) reinterpret_cast<uint4*>(d)[w] = in ? rg.v[u][w] : make_uint4(0, 0, 0, 0);
+    }
+    const int cv0 = ((255 - tid) & 3) * 8;
+    float2 a8[8];
+    float g8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a8[j] = xf[cv0 + j]; g8[j] = gt[cv0 + j]; }
+    const int act = g.lz.act;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int v = 255 - tid + u * 256;
+      const int row = v / RV, e = v - row * RV, xx = e >> 2;
+      if (row >= nt) break;
+      float vals[8];
+      if constexpr (WORDS == 1) {
+        const uint32_t w4[4] = {rx.v[u][0].x, rx.v[u][0].y, rx.v[u][0].z, rx.v[u][0].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          vals[2 * i] = __uint_as_float(w4[i] << 16);
+          vals[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+        }
+      } else {
+        const uint32_t w8[8] = {rx.v[u][0].x, rx.v[u][0].y, rx.v[u][0].z, rx.v[u][0].w,
+                                rx.v[u][1].x, rx.v[u][1].y, rx.v[u][1].z, rx.v[u][1].w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vals[i] = __uint_as_float(w8[i]);
+      }
+      const float m = ((rx.ok >> u) & 1) ? 1.f : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vals[j] = lazy_apply(vals[j], a8[j], act) * (g8[j] * m);
+      float* d = vring + (((t0 + row) % R) * IWS + xx) * DCB + cv0;
+      reinterpret_cast<float4*>(d)[0] = make_float4(vals[0], vals[1], vals[2], vals[3]);
+      reinterpret_cast<float4*>(d)[1] = make_float4(vals[4], vals[5], vals[6], vals[7]);
+    }
+  };
+
+  constexpr int NV2 = (2 * RV + 255) / 256;
+  DwRaw<NV2, WORDS> rs, rsx;
+  {  // prologue: rows 0 .. K-2, two at a time
+    DwRaw<NV2, WORDS> rp, rpx;
+    fetch(rp, rpx, 0, K - 1 < 2 ? K - 1 : 2);
+    __syncthreads();  // xf / gt
+#pragma unroll
+    for (int t = 0; t < K - 1; t += 2) {
+      commit(rp, rpx, t, K - 1 - t < 2 ? K - 1 - t : 2);
+      if (t + 2 < K - 1) fetch(rp, rpx, t + 2, K - 1 - (t + 2) < 2 ? K - 1 - (t + 2) : 2);
+    }
+  }
+  fetch(rs, rsx, K - 1, 2);
+
+  float acc[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
+  float fs = 0.f, fq = 0.f;
+  const int act = g.lz.act;
+  for (int j = 0; j < nrows; j += 2) {
+    // this step's global reads (fold x of both rows, cache-hot; dx for an accumulating store)
+    // before the next rows' prefetch (vmcnt counts in issue order)
+    T xr[2][CPG], dold[2][CPG];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < CPG; ++i) {
+        const int col = x0 + gc * CPG + i, r = r0 + j + p;
+        const bool ok = col < W && cvalid && j + p < nrows;
+        if constexpr (FOLD) xr[p][i] = X[ok ? (size_t)(r * W + col) * g.lz.ld + c : 0];
+        if (g.accumulate) dold[p][i] = DX[ok ? (size_t)(r * W + col) * C + c : 0];
+      }
+    commit(rs, rsx, j + K - 1, 2);
+    fetch(rs, rsx, j + K + 1, 2);  // unconditional (rows past the block: real or predicated off)
+    __syncthreads();
+
+    float dxv[2][CPG], dyc[2][CPG];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < CPG; ++i) {
+        dxv[p][i] = 0.f;
+        // an odd block's last step has no second row: its dy (a real row of the next block or
+        // padding) must not reach the filter gradient
+        const float live = j + p < nrows ? 1.f : 0.f;
+        dyc[p][i] = to_f<T>(dring[(((j + p + P) % R) * IWS + gc * CPG + i + P) * DCB + c]) * live;
+      }
+#pragma unroll
+    for (int rr = 0; rr <= K; ++rr) {
+      const int slot = (j + rr) % R;
+      float dwin[WIN], vwin[WIN];
+#pragma unroll
+      for (int x = 0; x < WIN; ++x) {
+        dwin[x] = to_f<T>(dring[(slot * IWS + gc * CPG + x) * DCB + c]);
+        vwin[x] = vring[(slot * IWS + gc * CPG + x) * DCB + c];
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int kh = rr - p;
+        if (kh < 0 || kh >= K) continue;
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) {
+          const float wv = wr[(K - 1 - kh) * K + kw];
+          float a = 0.f;
+#pragma unroll
+          for (int i = 0; i < CPG; ++i) {
+            dxv[p][i] += dwin[i + 2 * P - kw] * wv;
+            a += dyc[p][i] * vwin[i + kw];
+          }
+          acc[kh * K + kw] += a;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int i = 0; i < CPG; ++i) {
+        const int col = x0 + gc * CPG + i, r = r0 + j + p;
+        if (col < W && cvalid && j + p < nrows) {
+          DX[(size_t)(r * W + col) * C + c] = from_f<T>(g.accumulate ? to_f<T>(dold[p][i]) + dxv[p][i] : dxv[p][i]);
+          if constexpr (FOLD) {
+            const float xv = to_f<T>(xr[p][i]);
+            const float du = act ? dxv[p][i] * dswishf_(xv * myaf.x + myaf.y) : dxv[p][i];
+            fs += du;
+            fq += du * ((xv - mymr.x) * mymr.y);
+          }
+        }
+      }
+  }
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) red[(i * 8 + gc) * DCB + c] = acc[i];
+  if constexpr (FOLD) {
+    red[(K * K * 8 + gc) * DCB + c] = fs;
+    red[((K * K + 1) * 8 + gc) * DCB + c] = fq;
+  }
+  __syncthreads();
+  constexpr int NOUT = (K * K + (FOLD ? 2 : 0)) * DCB;
+  for (int e = tid; e < NOUT; e += 256) {
+    const int i = e / DCB, cc = e - i * DCB;
+    if (c0 + cc >= C) continue;
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sum += red[(i * 8 + k) * DCB + cc];
+    if (i < K * K) atomicAdd(g.dw + (size_t)i * C + c0 + cc, sum);
+    else if constexpr (FOLD) stat_add((i == K * K ? fold.dbeta[seg] : fold.dgamma[seg]) + c0 + cc, (double)sum);
+  }
+}
+
 template <typename T, int K, int CPG, bool FOLD>
 static int launch_dwb(DwArgs g, const edet_bngrad64& fold, hipStream_t s) {
   // rows in flight ahead of the one committed (development slot 17 = 2 selects two)
   const int pf = dev_knob(17) == 2 ? 2 : 1;
   constexpr int TW = 8 * CPG;
   int hmax = 0;
-  for (int i = 0; i < g.pin.nseg; ++i) hmax = std::max(hmax, g.pin.H[i]);
+  long rows_in = 0;
+  for (int i = 0; i < g.pin.nseg; ++i) {
+    hmax = std::max(hmax, g.pin.H[i]);
+    rows_in += (long)g.pin.batch * g.pin.H[i] * g.pin.W[i];
+  }
+  // plan per shape (tools/dw_bwd_probe.py over the D0 b32 stride-1 layers, r03k): two output
+  // rows per step (k_dwb2) everywhere but the C = 64 BiFPN / head layers (their short rows keep
+  // the 1-row ring: 44 vs 45 us pyramid, 32 vs 35 us at 64^2); 512 blocks at k5 (C = 240 / 480:
+  // 143 -> 138, 88 -> 78 us), 2048 for the large k3 layers (256^2 x 32: 191 -> 174, 128^2 x 144:
+  // 220 -> 209 us).  Development slots: 16 = block target, 25 = rows per step (1 or 2)
+  const int rows_per_step = dev_knob(25) ? dev_knob(25) : (g.C <= 64 ? 1 : 2);
   DwsPlan pl{};
   pl.cb_inner = 1;
   long total = 0;
   int target = DWS_BLOCKS;
+  if (K == 5) target = DWS_BLOCKS / 2;
+  else if (rows_in >= 524288) target = 2 * DWS_BLOCKS;
   if (dev_knob(16) > 0) target = dev_knob(16);
   for (int TH = 256; TH >= 2; TH /= 2) {
     if (TH > 2 * hmax && TH > 2) continue;
@@ -1738,7 +1993,8 @@ static int launch_dwb(DwArgs g, const edet_bngrad64& fold, hipStream_t s) {
   }
   if (total == 0) return EDET_OK;
   EDET_REQUIRE(total < (1L << 31), "dwconv_bwd: grid too large");
-  if (pf == 2) EDET_LAUNCH((k_dwb<T, K, CPG, FOLD, 2>), dim3((unsigned)total), dim3(256), 0, s, g, pl, fold);
+  if (rows_per_step == 2) EDET_LAUNCH((k_dwb2<T, K, CPG, FOLD>), dim3((unsigned)total), dim3(256), 0, s, g, pl, fold);
+  else if (pf == 2) EDET_LAUNCH((k_dwb<T, K, CPG, FOLD, 2>), dim3((unsigned)total), dim3(256), 0, s, g, pl, fold);
   else EDET_LAUNCH((k_dwb<T, K, CPG, FOLD, 1>), dim3((unsigned)total), dim3(256), 0, s, g, pl, fold);
   return check_launch("edet dwconv bwd");
 }

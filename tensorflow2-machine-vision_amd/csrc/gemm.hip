@@ -32,28 +32,52 @@ struct GemmArgs {
   int accumulate, has_stats, ntm, ntn;
 };
 
-// raw copy of 8 elements global -> LDS with zero fill past n valid
-template <typename T>
-__device__ __forceinline__ void cp8(T* dst, const T* src, int n) {
-  if (n >= 8) {
-    if constexpr (sizeof(T) == 2) {
-      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
-    } else {
-      reinterpret_cast<float4*>(dst)[0] = reinterpret_cast<const float4*>(src)[0];
-      reinterpret_cast<float4*>(dst)[1] = reinterpret_cast<const float4*>(src)[1];
-    }
-  } else {
+// W 16-byte words from p (a valid address: callers clamp it), zero when !ok.  Loaded
+// unconditionally and selected after: `ok ? p[w] : 0` is compiled as a branch around the load
+// with its own vmcnt(0) inside, one memory round trip per vector.
+template <int W, typename V>
+__device__ __forceinline__ void ld_or_zero(V (&dst)[W], const V* p, bool ok) {
+  V t[W];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) dst[i] = (i < n) ? src[i] : T(0);
-  }
+  for (int w = 0; w < W; ++w) t[w] = p[w];
+#pragma unroll
+  for (int w = 0; w < W; ++w) dst[w] = ok ? t[w] : V{};
 }
+
+// Rows [0, nrows) of a row-major [.][ld] matrix, columns [0, KP) (KP % 8 == 0), into LDS
+// [nrows][lds_ld]: 8 16-byte vectors per thread in flight before any is stored (a per-vector
+// conditional copy waited for each load inside its branch, one round trip per vector); rows
+// with row >= nvalid and elements at or past K are written as zeros.
 template <typename T>
-__device__ __forceinline__ void zero8(T* dst) {
-  if constexpr (sizeof(T) == 2) {
-    *reinterpret_cast<uint4*>(dst) = make_uint4(0, 0, 0, 0);
-  } else {
-    reinterpret_cast<float4*>(dst)[0] = make_float4(0, 0, 0, 0);
-    reinterpret_cast<float4*>(dst)[1] = make_float4(0, 0, 0, 0);
+__device__ __forceinline__ void stage_rows(T* lds, int lds_ld, const T* src, int ld, int nrows, int nvalid,
+                                           int K, int KP) {
+  using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
+  constexpr int VW = sizeof(T) == 2 ? 1 : 2, U = 8;
+  const int kv8 = KP / 8, total = nrows * kv8;
+  for (int v0 = 0; v0 < total; v0 += 256 * U) {
+    V t[U][VW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v = v0 + threadIdx.x + u * 256;
+      const int n = v / kv8, kv = (v - n * kv8) * 8;
+      const bool ok = v < total && n < nvalid && kv < K;
+      ld_or_zero<VW>(t[u], reinterpret_cast<const V*>(src + (ok ? (size_t)n * ld + kv : 0)), ok);
+      if (ok && K - kv < 8) {  // tail vector: zero the elements at or past K
+        T* e = reinterpret_cast<T*>(&t[u][0]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j >= K - kv) e[j] = T(0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v = v0 + threadIdx.x + u * 256;
+      if (v < total) {
+        const int n = v / kv8, kv = (v - n * kv8) * 8;
+#pragma unroll
+        for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(lds + (size_t)n * lds_ld + kv)[w] = t[u][w];
+      }
+    }
   }
 }
 
@@ -134,25 +158,15 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     for (int u = 0; u < AV; ++u) {
       const int v = tid + u * 256;
       const int r = v / KV, kv = (v % KV) * 8, grow = row0 + r, gk = k0 + kv;
-#pragma unroll
-      for (int w = 0; w < VW; ++w) R.ra[u][w] = V{};
-      if (v < BM * KV && grow < g.M && gk < g.K) {
-        const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + gk);
-#pragma unroll
-        for (int w = 0; w < VW; ++w) R.ra[u][w] = src[w];
-      }
+      const bool ok = v < BM * KV && grow < g.M && gk < g.K;
+      ld_or_zero<VW>(R.ra[u], reinterpret_cast<const V*>(A + (ok ? (size_t)grow * g.lda + gk : 0)), ok);
     }
 #pragma unroll
     for (int u = 0; u < BV; ++u) {
       const int v = tid + u * 256;
       const int n = v / KV, kv = (v % KV) * 8, gn = col0 + n, gk = k0 + kv;
-#pragma unroll
-      for (int w = 0; w < VW; ++w) R.rb[u][w] = V{};
-      if (v < BN * KV && gn < g.N && gk < g.K) {
-        const V* src = reinterpret_cast<const V*>(B + (size_t)gn * g.ldb + gk);
-#pragma unroll
-        for (int w = 0; w < VW; ++w) R.rb[u][w] = src[w];
-      }
+      const bool ok = v < BN * KV && gn < g.N && gk < g.K;
+      ld_or_zero<VW>(R.rb[u], reinterpret_cast<const V*>(B + (ok ? (size_t)gn * g.ldb + gk : 0)), ok);
     }
   };
   // registers -> LDS buffer, lazy transform of A on the way
@@ -323,13 +337,13 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 constexpr int RNB = 64;
 
 template <typename T, int BM, bool LAZY>
-__global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, int cps, int LDC) {
+__global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, int cps, int LDC, int bpmax) {
   constexpr int WM = BM / 2, FM = WM / 16, FN = 2;
   const int LDA = KP + 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // B chunks are double-buffered and fetched one chunk ahead when a chunk is at most 4
   // vectors per thread (KP <= 128); wider K keeps one buffer and loads each chunk in place
-  const bool bpipe = KP <= 128;
+  const bool bpipe = KP <= bpmax;
   T* As = reinterpret_cast<T*>(smem);
   T* Bs = As + BM * LDA;                                  // [bpipe ? 2 : 1][RNB][LDA]
   T* Cs = Bs + (bpipe ? 2 : 1) * RNB * LDA;               // [BM][LDC] (this split's columns)
@@ -370,9 +384,7 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
       const int r = v / kv8, kv = (v - r * kv8) * 8;
       const int grow = tmt * BM + r;
       const bool ok = v < BM * kv8 && grow < g.M && kv < K;  // K % 8 == 0: whole vectors
-      const V* src = reinterpret_cast<const V*>(A + (ok ? (size_t)grow * g.lda + kv : 0));
-#pragma unroll
-      for (int w = 0; w < VW; ++w) raw[u][w] = ok ? src[w] : V{};
+      ld_or_zero<VW>(raw[u], reinterpret_cast<const V*>(A + (ok ? (size_t)grow * g.lda + kv : 0)), ok);
     }
   };
   auto commit_a = [&](const V (&raw)[UNR][VW], int v0, int row0, int seg_off, int hw, bool gate_lds, int n_lo) {
@@ -412,16 +424,10 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   const bool bres = ch_end - ch_begin == 1;  // this split's B chunk stays in LDS for every tile
   const T* B = (const T*)g.b;
   using VB = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
-  constexpr int VWB = sizeof(T) == 2 ? 1 : 2, NBV = 4;
+  constexpr int VWB = sizeof(T) == 2 ? 1 : 2, NBV = sizeof(T) == 2 ? 8 : 4;
   VB rb[NBV][VWB];
   auto load_b = [&](int ch, T* bs) {  // in place (global -> LDS)
-    for (int v = tid; v < RNB * kv8; v += 256) {
-      const int n = v / kv8, kv = (v - n * kv8) * 8;
-      const int gn = ch * RNB + n, nk = K - kv;
-      T* dst = &bs[n * LDA + kv];
-      if (gn < N && nk > 0) cp8(dst, B + (size_t)gn * g.ldb + kv, nk);
-      else zero8(dst);
-    }
+    stage_rows(bs, LDA, B + (size_t)ch * RNB * g.ldb, g.ldb, RNB, N - ch * RNB, K, KP);
   };
   auto fetch_b = [&](int ch) {  // registers, every load issued before any use (K % 8 == 0)
 #pragma unroll
@@ -430,9 +436,7 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
       const int n = v / kv8, kv = (v - n * kv8) * 8;
       const int gn = ch * RNB + n;
       const bool ok = v < RNB * kv8 && gn < N && kv < K;
-      const VB* src = reinterpret_cast<const VB*>(B + (ok ? (size_t)gn * g.ldb + kv : 0));
-#pragma unroll
-      for (int w = 0; w < VWB; ++w) rb[u][w] = ok ? src[w] : VB{};
+      ld_or_zero<VWB>(rb[u], reinterpret_cast<const VB*>(B + (ok ? (size_t)gn * g.ldb + kv : 0)), ok);
     }
   };
   auto commit_b = [&](T* bs) {
@@ -812,27 +816,15 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
       const int sg = seg_of_row(g.pyr, row);
       const bool live = row < m_end && row < g.pyr.row_off[sg] + seg_rows(g.pyr, sg);
       S.rseg[h] = live ? sg : -1;
-      const int nn = g.N - (n0 + lc), nk = g.K - (kk0 + lc);
-      S.rd[h] = make_uint4(0, 0, 0, 0);
-      S.rx[h] = make_uint4(0, 0, 0, 0);
-      if (live && nn >= 8) S.rd[h] = *reinterpret_cast<const uint4*>(DY + (size_t)row * g.lddy + n0 + lc);
-      else if (live && nn > 0) {
-        float v[8];
-        ld8m(DY + (size_t)row * g.lddy + n0 + lc, nn, v);
-        uint16_t t[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) t[j] = from_f<uint16_t>(v[j]);
-        S.rd[h] = *reinterpret_cast<uint4*>(t);
-      }
-      if (live && nk >= 8) S.rx[h] = *reinterpret_cast<const uint4*>(A + (size_t)row * g.lda + kk0 + lc);
-      else if (live && nk > 0) {
-        float v[8];
-        ld8m(A + (size_t)row * g.lda + kk0 + lc, nk, v);
-        uint16_t t[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) t[j] = from_f<uint16_t>(v[j]);
-        S.rx[h] = *reinterpret_cast<uint4*>(t);
-      }
+      // whole 16-byte vectors from clamped addresses, zeroed when dead (a load in a branch is
+      // waited for inside it: every stage's four loads went one round trip at a time).  A
+      // vector that starts below N (K) lies inside the row (ld % 8 == 0); its columns past N
+      // (K) only reach outputs that are never written
+      const bool okd = live && n0 + lc < g.N, okx = live && kk0 + lc < g.K;
+      const uint4 vd = *reinterpret_cast<const uint4*>(DY + (okd ? (size_t)row * g.lddy + n0 + lc : 0));
+      const uint4 vx = *reinterpret_cast<const uint4*>(A + (okx ? (size_t)row * g.lda + kk0 + lc : 0));
+      S.rd[h] = okd ? vd : make_uint4(0, 0, 0, 0);
+      S.rx[h] = okx ? vx : make_uint4(0, 0, 0, 0);
     }
   };
   // SE gate of this thread's 8 columns, cached per image (the image changes every hw rows)
@@ -1208,12 +1200,8 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
   {
     const T* B = (const T*)g.b;
     const int kvb = p.KP / 8;
-    for (int v = tid; v < p.NG * kvb; v += 256) {
-      const int n = v / kvb, kv = (v - n * kvb) * 8, gn = col_base + n;
-      T* dst = Bs + (size_t)n * p.LDB + kv;
-      if (gn < N && kv < K) cp8(dst, B + (size_t)gn * g.ldb + kv, K - kv);
-      else zero8(dst);
-    }
+    (void)kvb;
+    stage_rows(Bs, p.LDB, B + (size_t)col_base * g.ldb, g.ldb, p.NG, N - col_base, K, p.KP);
     for (int c = tid; c < 4 * p.NGtot; c += 256) red[c] = 0.f;
     if constexpr (LAZY) {
       for (int s = 0; s < g.pyr.nseg; ++s) {
@@ -1239,16 +1227,10 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
 #pragma unroll
     for (int u = 0; u < PW_NV; ++u) {
       const int v = tid + u * 256;
-#pragma unroll
-      for (int ww = 0; ww < VW; ++ww) ra[u][ww] = V{};
       const int r = v / KV, kv = (v - r * KV) * 8;
       const int grow = rbase + r, gk = kc * p.KC + kv;
       const bool live = v < nvec && grow < M && gk < K;
-      if (live) {
-        const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + gk);
-#pragma unroll
-        for (int ww = 0; ww < VW; ++ww) ra[u][ww] = src[ww];
-      }
+      ld_or_zero<VW>(ra[u], reinterpret_cast<const V*>(A + (live ? (size_t)grow * g.lda + gk : 0)), live);
       if constexpr (LAZY) {
         if (has_gate && live) {
           const float4* gp = reinterpret_cast<const float4*>(g.lz.gate + (size_t)((grow - seg_off) / hw) * K + gk);
@@ -1784,9 +1766,14 @@ static int launch_gemm(GemmArgs g, hipStream_t s) {
   return check_launch("edet gemm");
 }
 
+// B chunks double-buffered and fetched a chunk ahead up to this K (one register round of NBV
+// vectors per thread; development slot 24 = 1: up to 256 for bf16)
+template <typename T>
+static int gemm_r_bpmax() { return (sizeof(T) == 2 && dev_knob(24) == 1) ? 256 : 128; }
+
 template <typename T, int BM, bool LAZY>
 static size_t gemm_r_lds(int K, int KP, int LDC) {
-  return (size_t)(BM + (KP <= 128 ? 2 : 1) * RNB) * (KP + 8) * sizeof(T) + (size_t)BM * LDC * sizeof(T) +
+  return (size_t)(BM + (KP <= gemm_r_bpmax<T>() ? 2 : 1) * RNB) * (KP + 8) * sizeof(T) + (size_t)BM * LDC * sizeof(T) +
          4 * (size_t)LDC * sizeof(float) +
          (LAZY ? (size_t)K * (sizeof(float2) + 2 * sizeof(float)) : 0);
 }
@@ -1810,7 +1797,8 @@ static int launch_gemm_r(GemmArgs g, hipStream_t s) {
   // resident blocks per CU from the LDS image; the row-tile workers per split fill that once
   const int per_cu = max(1, min(8, (int)((160 * 1024) / lds)));
   const int G = min(ntm, max(1, cdiv(256 * per_cu, nsplit)));
-  EDET_LAUNCH((k_gemm_r<T, BM, LAZY>), dim3(G * nsplit), dim3(256), lds, s, g, KP, nsplit, cps, LDC);
+  EDET_LAUNCH((k_gemm_r<T, BM, LAZY>), dim3(G * nsplit), dim3(256), lds, s, g, KP, nsplit, cps, LDC,
+              gemm_r_bpmax<T>());
   return check_launch("edet gemm_r");
 }
 
@@ -1857,7 +1845,7 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
   // lazy A with K >= 112 into N > 320 (the stage 5-7 expand convs): the A-resident form walks
   // its column chunks one dependent B load at a time with 2 blocks per CU; the pipelined
   // K loop over 128-column tiles measured 1.3-1.4x faster (8192x192x1152, 32768x112x672)
-  if (LAZY && g.K >= 112 && g.N > 320) return dispatch_gemm_kloop<T, LAZY>(g, s);
+  if (LAZY && g.K >= 112 && g.N > 320 && dev_knob(23) != 1) return dispatch_gemm_kloop<T, LAZY>(g, s);
   if (g.K <= 512) {
     // the largest row tile that still gives >= 256 (row tile, column chunk) blocks: at M = 8192
     // the 128-row tiles left 64 blocks for 256 CUs (8192 x 320 -> 64: 21 us)

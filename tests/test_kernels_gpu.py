@@ -361,10 +361,12 @@ def test_dwconv_fwd_squeeze(dt, k, s, H, W, C):
 
 # ----------------------------------------------------------------- SE
 @pytest.mark.parametrize("dt", DTS)
-@pytest.mark.parametrize("C,R", [(96, 4), (1152, 48), (520, 100)])
-def test_squeeze_excite(dt, C, R):
+@pytest.mark.parametrize("C,R,B", [(96, 4, 3), (1152, 48, 3), (520, 100, 3), (200, 70, 40)])
+def test_squeeze_excite(dt, C, R, B):
+    """SE forward and backward (layers/se.py:35-39) against fp64 autograd; R > 64 and B > 32
+    take the weight-gradient tiles' r-batch and image-chunk loops."""
     rng = np.random.default_rng(5 + C)
-    B, H, W = 3, 9, 7
+    H, W = 9, 7
     pyr = Pyr(B, [(H, W)])
     x = pyr_data(rng, pyr, C, dt)
     bn = make_bn(x, pyr, C, rng)
