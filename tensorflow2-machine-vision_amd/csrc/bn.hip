@@ -525,69 +525,54 @@ __global__ __launch_bounds__(256) void k_se_dz1(int B, int C, int R, const float
 //   dw2[c][r] += sum_n dz2[n][c] swish(z1[n][r])     dw1[r][c] += sum_n dz1[n][r] s[n][c]
 //   db2[c]    += sum_n dz2[n][c]                     db1[r]    += sum_n dz1[n][r]
 //   dsq[n][c]  = sum_r dz1[n][r] w1[r][c] / HW
-// The weight gradients are (C x B)(B x R) products: the block stages dz2 and s for its 32
-// channels and swish(z1), dz1 for all R, 32 images at a time (coalesced rows), and thread
-// (c, rg) accumulates r = rg, rg + 8, ... in registers (the former half-wave per (c, r) read
+// The weight gradients are (C x B)(B x R) products: a block per 32 channels x 8 r stages dz2
+// and s of its channels and swish(z1), dz1 of its r, 32 images at a time (coalesced rows), and
+// thread (c, r) accumulates both products over the images (the former half-wave per (c, r) read
 // gate / dgate / s with stride C across its lanes: 12 us per launch at C = 1152, R = 48).
-constexpr int SEW_NB = 32, SEW_C = 32;
-__host__ __device__ inline size_t se_wgrad_lds(int R) { return (size_t)(2 * SEW_NB * SEW_C + 2 * SEW_NB * R) * sizeof(float); }
+constexpr int SEW_NB = 32, SEW_C = 32, SEW_R = 8;
+__host__ __device__ inline int se_wgrad_blocks(int C, int R) { return cdiv(C, SEW_C) * cdiv(R, SEW_R); }
 __device__ __forceinline__ void k_se_wgrad_body(int B, int C, int R, int HW, int nA, const double* s,
                                                 const float* z1, const float* gate, const double* dgate,
                                                 const float* dz1, const float* w1, float* dw1, float* db1,
                                                 float* dw2, float* db2, float* dsq) {
   if ((int)blockIdx.x < nA) {
-    extern __shared__ float sew[];
-    float* d2s = sew;                     // [NB][32] dz2
-    float* svs = d2s + SEW_NB * SEW_C;    // [NB][32] s
-    float* zss = svs + SEW_NB * SEW_C;    // [NB][R]  swish(z1)
-    float* dzs = zss + SEW_NB * R;        // [NB][R]  dz1
-    const int tid = threadIdx.x, cl = tid & 31, rg = tid >> 5;
-    const int c0 = blockIdx.x * SEW_C, c = c0 + cl;
-    for (int rb = 0; rb < R; rb += 64) {
-      float a2[8], a1[8];
+    __shared__ float d2s[SEW_NB][SEW_C], svs[SEW_NB][SEW_C], zss[SEW_NB][SEW_R], dzs[SEW_NB][SEW_R];
+    const int tid = threadIdx.x, cl = tid & 31, rl = tid >> 5;
+    const int nrt = cdiv(R, SEW_R);
+    const int c0 = ((int)blockIdx.x / nrt) * SEW_C, r0 = ((int)blockIdx.x % nrt) * SEW_R;
+    const int c = c0 + cl, r = r0 + rl;
+    float a2 = 0.f, a1 = 0.f;
+    for (int n0 = 0; n0 < B; n0 += SEW_NB) {
+      const int nb = min(SEW_NB, B - n0);
+      __syncthreads();
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a2[i] = a1[i] = 0.f;
-      for (int n0 = 0; n0 < B; n0 += SEW_NB) {
-        const int nb = min(SEW_NB, B - n0);
-        __syncthreads();
-        for (int e = tid; e < SEW_NB * SEW_C; e += 256) {  // clamped addresses, values selected
-          const int n = e >> 5, cc = c0 + (e & 31);
-          const bool ok = n < nb && cc < C;
-          const size_t i = ok ? (size_t)(n0 + n) * C + cc : 0;
-          const float gv = gate[i];
-          const double dg = dgate[i], sv = s[i];
-          d2s[e] = ok ? (float)dg * gv * (1.f - gv) : 0.f;
-          svs[e] = ok ? (float)sv : 0.f;
-        }
-        for (int e = tid; e < SEW_NB * R; e += 256) {
-          const int n = e / R;
-          const bool ok = n < nb;
-          const size_t i = ok ? (size_t)n0 * R + e : 0;
-          const float z = z1[i], d = dz1[i];
-          zss[e] = ok ? z * sigmoidf_(z) : 0.f;
-          dzs[e] = ok ? d : 0.f;
-        }
-        __syncthreads();
-        for (int n = 0; n < nb; ++n) {
-          const float d2 = d2s[n * SEW_C + cl], sv = svs[n * SEW_C + cl];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int r = rb + rg + 8 * i;
-            if (r < R) {
-              a2[i] += d2 * zss[n * R + r];
-              a1[i] += dzs[n * R + r] * sv;
-            }
-          }
-        }
+      for (int u = 0; u < SEW_NB * SEW_C / 256; ++u) {  // clamped addresses, values selected
+        const int e = tid + u * 256, n = e >> 5, cc = c0 + (e & 31);
+        const bool ok = n < nb && cc < C;
+        const size_t i = ok ? (size_t)(n0 + n) * C + cc : 0;
+        const float gv = gate[i];
+        const double dg = dgate[i], sv = s[i];
+        d2s[n][e & 31] = ok ? (float)dg * gv * (1.f - gv) : 0.f;
+        svs[n][e & 31] = ok ? (float)sv : 0.f;
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = rb + rg + 8 * i;
-        if (r < R && c < C) {
-          dw2[(size_t)c * R + r] += a2[i];
-          dw1[(size_t)r * C + c] += a1[i];
-        }
+      {
+        const int n = tid >> 3, rr = r0 + (tid & 7);
+        const bool ok = n < nb && rr < R;
+        const size_t i = ok ? (size_t)(n0 + n) * R + rr : 0;
+        const float z = z1[i], d = dz1[i];
+        zss[n][tid & 7] = ok ? z * sigmoidf_(z) : 0.f;
+        dzs[n][tid & 7] = ok ? d : 0.f;
       }
+      __syncthreads();
+#pragma unroll 8
+      for (int n = 0; n < nb; ++n) {
+        a2 += d2s[n][cl] * zss[n][rl];
+        a1 += dzs[n][rl] * svs[n][cl];
+      }
+    }
+    if (r < R && c < C) {
+      dw2[(size_t)c * R + r] += a2;
+      dw1[(size_t)r * C + c] += a1;
     }
     return;
   }
@@ -921,10 +906,9 @@ int edet_se_bwd_bn(int B, int C, int R, int HW, const double* s, const float* z1
                    acc->dgamma[0] && acc->dbeta[0],
                "se_bwd_bn: null argument");
   hipStream_t st = (hipStream_t)stream;
-  EDET_REQUIRE(se_wgrad_lds(R) <= 64 * 1024, "se_bwd_bn: R = %d too large", R);
   EDET_LAUNCH(k_se_dz1, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, z1, gate, dgate, w2, dz1);
-  const int nA = cdiv(C, SEW_C), nB = cdiv(std::max(B * C, std::max(C, R)), 256);
-  EDET_LAUNCH(k_se_wgrad_bn, dim3(nA + nB + cdiv(C, 8)), dim3(256), se_wgrad_lds(R), st, B, C, R, HW, nA, nA + nB, s, z1, gate,
+  const int nA = se_wgrad_blocks(C, R), nB = cdiv(std::max(B * C, std::max(C, R)), 256);
+  EDET_LAUNCH(k_se_wgrad_bn, dim3(nA + nB + cdiv(C, 8)), dim3(256), 0, st, B, C, R, HW, nA, nA + nB, s, z1, gate,
               dgate, dz1, w1, dw1, db1, dw2, db2, dsq, sums5, acc->dgamma[0], acc->dbeta[0]);
   return check_launch("edet se_bwd_bn");
 }
@@ -936,10 +920,9 @@ int edet_se_bwd(int B, int C, int R, int HW, const double* s, const float* z1,
   EDET_REQUIRE(s && z1 && gate && dgate && w1 && w2 && dw1 && db1 && dw2 && db2 && dsq && dz1,
                "se_bwd: null argument");
   hipStream_t st = (hipStream_t)stream;
-  EDET_REQUIRE(se_wgrad_lds(R) <= 64 * 1024, "se_bwd: R = %d too large", R);
   EDET_LAUNCH(k_se_dz1, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, z1, gate, dgate, w2, dz1);
-  const int nA = cdiv(C, SEW_C), nB = cdiv(std::max(B * C, std::max(C, R)), 256);
-  EDET_LAUNCH(k_se_wgrad, dim3(nA + nB), dim3(256), se_wgrad_lds(R), st, B, C, R, HW, nA, s, z1, gate, dgate, dz1, w1,
+  const int nA = se_wgrad_blocks(C, R), nB = cdiv(std::max(B * C, std::max(C, R)), 256);
+  EDET_LAUNCH(k_se_wgrad, dim3(nA + nB), dim3(256), 0, st, B, C, R, HW, nA, s, z1, gate, dgate, dz1, w1,
                      dw1, db1, dw2, db2, dsq);
   return check_launch("edet se_bwd");
 }

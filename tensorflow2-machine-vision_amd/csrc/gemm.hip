@@ -337,13 +337,13 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 constexpr int RNB = 64;
 
 template <typename T, int BM, bool LAZY>
-__global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, int cps, int LDC, int bpmax) {
+__global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, int cps, int LDC) {
   constexpr int WM = BM / 2, FM = WM / 16, FN = 2;
   const int LDA = KP + 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // B chunks are double-buffered and fetched one chunk ahead when a chunk is at most 4
   // vectors per thread (KP <= 128); wider K keeps one buffer and loads each chunk in place
-  const bool bpipe = KP <= bpmax;
+  const bool bpipe = KP <= 128;
   T* As = reinterpret_cast<T*>(smem);
   T* Bs = As + BM * LDA;                                  // [bpipe ? 2 : 1][RNB][LDA]
   T* Cs = Bs + (bpipe ? 2 : 1) * RNB * LDA;               // [BM][LDC] (this split's columns)
@@ -424,7 +424,7 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   const bool bres = ch_end - ch_begin == 1;  // this split's B chunk stays in LDS for every tile
   const T* B = (const T*)g.b;
   using VB = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
-  constexpr int VWB = sizeof(T) == 2 ? 1 : 2, NBV = sizeof(T) == 2 ? 8 : 4;
+  constexpr int VWB = sizeof(T) == 2 ? 1 : 2, NBV = 4;
   VB rb[NBV][VWB];
   auto load_b = [&](int ch, T* bs) {  // in place (global -> LDS)
     stage_rows(bs, LDA, B + (size_t)ch * RNB * g.ldb, g.ldb, RNB, N - ch * RNB, K, KP);
@@ -1766,14 +1766,9 @@ static int launch_gemm(GemmArgs g, hipStream_t s) {
   return check_launch("edet gemm");
 }
 
-// B chunks double-buffered and fetched a chunk ahead up to this K (one register round of NBV
-// vectors per thread; development slot 24 = 1: up to 256 for bf16)
-template <typename T>
-static int gemm_r_bpmax() { return (sizeof(T) == 2 && dev_knob(24) == 1) ? 256 : 128; }
-
 template <typename T, int BM, bool LAZY>
 static size_t gemm_r_lds(int K, int KP, int LDC) {
-  return (size_t)(BM + (KP <= gemm_r_bpmax<T>() ? 2 : 1) * RNB) * (KP + 8) * sizeof(T) + (size_t)BM * LDC * sizeof(T) +
+  return (size_t)(BM + (KP <= 128 ? 2 : 1) * RNB) * (KP + 8) * sizeof(T) + (size_t)BM * LDC * sizeof(T) +
          4 * (size_t)LDC * sizeof(float) +
          (LAZY ? (size_t)K * (sizeof(float2) + 2 * sizeof(float)) : 0);
 }
@@ -1797,8 +1792,7 @@ static int launch_gemm_r(GemmArgs g, hipStream_t s) {
   // resident blocks per CU from the LDS image; the row-tile workers per split fill that once
   const int per_cu = max(1, min(8, (int)((160 * 1024) / lds)));
   const int G = min(ntm, max(1, cdiv(256 * per_cu, nsplit)));
-  EDET_LAUNCH((k_gemm_r<T, BM, LAZY>), dim3(G * nsplit), dim3(256), lds, s, g, KP, nsplit, cps, LDC,
-              gemm_r_bpmax<T>());
+  EDET_LAUNCH((k_gemm_r<T, BM, LAZY>), dim3(G * nsplit), dim3(256), lds, s, g, KP, nsplit, cps, LDC);
   return check_launch("edet gemm_r");
 }
 
@@ -1845,7 +1839,7 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
   // lazy A with K >= 112 into N > 320 (the stage 5-7 expand convs): the A-resident form walks
   // its column chunks one dependent B load at a time with 2 blocks per CU; the pipelined
   // K loop over 128-column tiles measured 1.3-1.4x faster (8192x192x1152, 32768x112x672)
-  if (LAZY && g.K >= 112 && g.N > 320 && dev_knob(23) != 1) return dispatch_gemm_kloop<T, LAZY>(g, s);
+  if (LAZY && g.K >= 112 && g.N > 320) return dispatch_gemm_kloop<T, LAZY>(g, s);
   if (g.K <= 512) {
     // the largest row tile that still gives >= 256 (row tile, column chunk) blocks: at M = 8192
     // the 128-row tiles left 64 blocks for 256 CUs (8192 x 320 -> 64: 21 us)
