@@ -29,7 +29,16 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--dev", default="", help="edet_dev_set slots for the timed replays, e.g. 7=1")
     ap.add_argument("--seq", default="", help="also write every call's us in launch order")
+    ap.add_argument("--abi-any", action="store_true",
+                    help="A/B against an older build (EDET_LIB): accept its ABI version, drop entry points it lacks")
     args = ap.parse_args()
+    if args.abi_any:
+        import ctypes
+        from tf2mv_amd import _lib as L0
+        d = ctypes.CDLL(L0.LIB_PATH)
+        for name in [n for n in L0.SIGNATURES if not hasattr(d, n)]:
+            del L0.SIGNATURES[name]
+        L0.ABI_VERSION = d.edet_abi_version()
 
     from tf2mv_amd import _lib as L
     from tf2mv_amd.anchors import Anchors

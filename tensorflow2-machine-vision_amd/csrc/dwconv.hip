@@ -376,13 +376,16 @@ __global__ __launch_bounds__(256) void k_dw_wgrad(DwArgs g) {
     // this tile's dy values go out with the halo loads (select-predicated), not after commit
     const int oy = oy0 + r;
     const size_t obase = (size_t)g.pout.row_off[seg] + (size_t)n * OH * OW;
+    // (a zero select on the loaded value let the compiler branch around each conversion with a
+    // vmcnt(0) inside, draining the halo loads eight times per tile: zeroed by a multiply)
     T dyr[DTS];
+    float dym[DTS];
 #pragma unroll
     for (int j = 0; j < DTS; ++j) {
       const int ox = ox0 + j;
       const bool in = oy < OH && ox < OW && cvalid;
       dyr[j] = DY[in ? (obase + (size_t)oy * OW + ox) * g.C + c0 + c : 0];
-      if (!in) dyr[j] = from_f<T>(0.f);
+      dym[j] = in ? 1.f : 0.f;
     }
     if (seg != xf_seg || (g.lz.gate && n != xf_img)) {  // block-uniform, as in k_dw_fwd
       prep_xf(g, xf, gt, seg, n, c0);
@@ -393,7 +396,7 @@ __global__ __launch_bounds__(256) void k_dw_wgrad(DwArgs g) {
     st.commit(g, lds, xf, gt);
     float dyv[DTS];
 #pragma unroll
-    for (int j = 0; j < DTS; ++j) dyv[j] = to_f<T>(dyr[j]);
+    for (int j = 0; j < DTS; ++j) dyv[j] = to_f<T>(dyr[j]) * dym[j];
     __syncthreads();
 #pragma unroll
     for (int kh = 0; kh < K; ++kh)

@@ -32,52 +32,28 @@ struct GemmArgs {
   int accumulate, has_stats, ntm, ntn;
 };
 
-// W 16-byte words from p (a valid address: callers clamp it), zero when !ok.  Loaded
-// unconditionally and selected after: `ok ? p[w] : 0` is compiled as a branch around the load
-// with its own vmcnt(0) inside, one memory round trip per vector.
-template <int W, typename V>
-__device__ __forceinline__ void ld_or_zero(V (&dst)[W], const V* p, bool ok) {
-  V t[W];
-#pragma unroll
-  for (int w = 0; w < W; ++w) t[w] = p[w];
-#pragma unroll
-  for (int w = 0; w < W; ++w) dst[w] = ok ? t[w] : V{};
-}
-
-// Rows [0, nrows) of a row-major [.][ld] matrix, columns [0, KP) (KP % 8 == 0), into LDS
-// [nrows][lds_ld]: 8 16-byte vectors per thread in flight before any is stored (a per-vector
-// conditional copy waited for each load inside its branch, one round trip per vector); rows
-// with row >= nvalid and elements at or past K are written as zeros.
+// raw copy of 8 elements global -> LDS with zero fill past n valid
 template <typename T>
-__device__ __forceinline__ void stage_rows(T* lds, int lds_ld, const T* src, int ld, int nrows, int nvalid,
-                                           int K, int KP) {
-  using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
-  constexpr int VW = sizeof(T) == 2 ? 1 : 2, U = 8;
-  const int kv8 = KP / 8, total = nrows * kv8;
-  for (int v0 = 0; v0 < total; v0 += 256 * U) {
-    V t[U][VW];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int v = v0 + threadIdx.x + u * 256;
-      const int n = v / kv8, kv = (v - n * kv8) * 8;
-      const bool ok = v < total && n < nvalid && kv < K;
-      ld_or_zero<VW>(t[u], reinterpret_cast<const V*>(src + (ok ? (size_t)n * ld + kv : 0)), ok);
-      if (ok && K - kv < 8) {  // tail vector: zero the elements at or past K
-        T* e = reinterpret_cast<T*>(&t[u][0]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j >= K - kv) e[j] = T(0);
-      }
+__device__ __forceinline__ void cp8(T* dst, const T* src, int n) {
+  if (n >= 8) {
+    if constexpr (sizeof(T) == 2) {
+      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+    } else {
+      reinterpret_cast<float4*>(dst)[0] = reinterpret_cast<const float4*>(src)[0];
+      reinterpret_cast<float4*>(dst)[1] = reinterpret_cast<const float4*>(src)[1];
     }
+  } else {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int v = v0 + threadIdx.x + u * 256;
-      if (v < total) {
-        const int n = v / kv8, kv = (v - n * kv8) * 8;
-#pragma unroll
-        for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(lds + (size_t)n * lds_ld + kv)[w] = t[u][w];
-      }
-    }
+    for (int i = 0; i < 8; ++i) dst[i] = (i < n) ? src[i] : T(0);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void zero8(T* dst) {
+  if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<uint4*>(dst) = make_uint4(0, 0, 0, 0);
+  } else {
+    reinterpret_cast<float4*>(dst)[0] = make_float4(0, 0, 0, 0);
+    reinterpret_cast<float4*>(dst)[1] = make_float4(0, 0, 0, 0);
   }
 }
 
@@ -158,15 +134,25 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     for (int u = 0; u < AV; ++u) {
       const int v = tid + u * 256;
       const int r = v / KV, kv = (v % KV) * 8, grow = row0 + r, gk = k0 + kv;
-      const bool ok = v < BM * KV && grow < g.M && gk < g.K;
-      ld_or_zero<VW>(R.ra[u], reinterpret_cast<const V*>(A + (ok ? (size_t)grow * g.lda + gk : 0)), ok);
+#pragma unroll
+      for (int w = 0; w < VW; ++w) R.ra[u][w] = V{};
+      if (v < BM * KV && grow < g.M && gk < g.K) {
+        const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + gk);
+#pragma unroll
+        for (int w = 0; w < VW; ++w) R.ra[u][w] = src[w];
+      }
     }
 #pragma unroll
     for (int u = 0; u < BV; ++u) {
       const int v = tid + u * 256;
       const int n = v / KV, kv = (v % KV) * 8, gn = col0 + n, gk = k0 + kv;
-      const bool ok = v < BN * KV && gn < g.N && gk < g.K;
-      ld_or_zero<VW>(R.rb[u], reinterpret_cast<const V*>(B + (ok ? (size_t)gn * g.ldb + gk : 0)), ok);
+#pragma unroll
+      for (int w = 0; w < VW; ++w) R.rb[u][w] = V{};
+      if (v < BN * KV && gn < g.N && gk < g.K) {
+        const V* src = reinterpret_cast<const V*>(B + (size_t)gn * g.ldb + gk);
+#pragma unroll
+        for (int w = 0; w < VW; ++w) R.rb[u][w] = src[w];
+      }
     }
   };
   // registers -> LDS buffer, lazy transform of A on the way
@@ -384,7 +370,9 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
       const int r = v / kv8, kv = (v - r * kv8) * 8;
       const int grow = tmt * BM + r;
       const bool ok = v < BM * kv8 && grow < g.M && kv < K;  // K % 8 == 0: whole vectors
-      ld_or_zero<VW>(raw[u], reinterpret_cast<const V*>(A + (ok ? (size_t)grow * g.lda + kv : 0)), ok);
+      const V* src = reinterpret_cast<const V*>(A + (ok ? (size_t)grow * g.lda + kv : 0));
+#pragma unroll
+      for (int w = 0; w < VW; ++w) raw[u][w] = ok ? src[w] : V{};
     }
   };
   auto commit_a = [&](const V (&raw)[UNR][VW], int v0, int row0, int seg_off, int hw, bool gate_lds, int n_lo) {
@@ -427,7 +415,13 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   constexpr int VWB = sizeof(T) == 2 ? 1 : 2, NBV = 4;
   VB rb[NBV][VWB];
   auto load_b = [&](int ch, T* bs) {  // in place (global -> LDS)
-    stage_rows(bs, LDA, B + (size_t)ch * RNB * g.ldb, g.ldb, RNB, N - ch * RNB, K, KP);
+    for (int v = tid; v < RNB * kv8; v += 256) {
+      const int n = v / kv8, kv = (v - n * kv8) * 8;
+      const int gn = ch * RNB + n, nk = K - kv;
+      T* dst = &bs[n * LDA + kv];
+      if (gn < N && nk > 0) cp8(dst, B + (size_t)gn * g.ldb + kv, nk);
+      else zero8(dst);
+    }
   };
   auto fetch_b = [&](int ch) {  // registers, every load issued before any use (K % 8 == 0)
 #pragma unroll
@@ -436,7 +430,9 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
       const int n = v / kv8, kv = (v - n * kv8) * 8;
       const int gn = ch * RNB + n;
       const bool ok = v < RNB * kv8 && gn < N && kv < K;
-      ld_or_zero<VWB>(rb[u], reinterpret_cast<const VB*>(B + (ok ? (size_t)gn * g.ldb + kv : 0)), ok);
+      const VB* src = reinterpret_cast<const VB*>(B + (ok ? (size_t)gn * g.ldb + kv : 0));
+#pragma unroll
+      for (int w = 0; w < VWB; ++w) rb[u][w] = ok ? src[w] : VB{};
     }
   };
   auto commit_b = [&](T* bs) {
@@ -816,15 +812,27 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
       const int sg = seg_of_row(g.pyr, row);
       const bool live = row < m_end && row < g.pyr.row_off[sg] + seg_rows(g.pyr, sg);
       S.rseg[h] = live ? sg : -1;
-      // whole 16-byte vectors from clamped addresses, zeroed when dead (a load in a branch is
-      // waited for inside it: every stage's four loads went one round trip at a time).  A
-      // vector that starts below N (K) lies inside the row (ld % 8 == 0); its columns past N
-      // (K) only reach outputs that are never written
-      const bool okd = live && n0 + lc < g.N, okx = live && kk0 + lc < g.K;
-      const uint4 vd = *reinterpret_cast<const uint4*>(DY + (okd ? (size_t)row * g.lddy + n0 + lc : 0));
-      const uint4 vx = *reinterpret_cast<const uint4*>(A + (okx ? (size_t)row * g.lda + kk0 + lc : 0));
-      S.rd[h] = okd ? vd : make_uint4(0, 0, 0, 0);
-      S.rx[h] = okx ? vx : make_uint4(0, 0, 0, 0);
+      const int nn = g.N - (n0 + lc), nk = g.K - (kk0 + lc);
+      S.rd[h] = make_uint4(0, 0, 0, 0);
+      S.rx[h] = make_uint4(0, 0, 0, 0);
+      if (live && nn >= 8) S.rd[h] = *reinterpret_cast<const uint4*>(DY + (size_t)row * g.lddy + n0 + lc);
+      else if (live && nn > 0) {
+        float v[8];
+        ld8m(DY + (size_t)row * g.lddy + n0 + lc, nn, v);
+        uint16_t t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = from_f<uint16_t>(v[j]);
+        S.rd[h] = *reinterpret_cast<uint4*>(t);
+      }
+      if (live && nk >= 8) S.rx[h] = *reinterpret_cast<const uint4*>(A + (size_t)row * g.lda + kk0 + lc);
+      else if (live && nk > 0) {
+        float v[8];
+        ld8m(A + (size_t)row * g.lda + kk0 + lc, nk, v);
+        uint16_t t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = from_f<uint16_t>(v[j]);
+        S.rx[h] = *reinterpret_cast<uint4*>(t);
+      }
     }
   };
   // SE gate of this thread's 8 columns, cached per image (the image changes every hw rows)
@@ -1200,8 +1208,12 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
   {
     const T* B = (const T*)g.b;
     const int kvb = p.KP / 8;
-    (void)kvb;
-    stage_rows(Bs, p.LDB, B + (size_t)col_base * g.ldb, g.ldb, p.NG, N - col_base, K, p.KP);
+    for (int v = tid; v < p.NG * kvb; v += 256) {
+      const int n = v / kvb, kv = (v - n * kvb) * 8, gn = col_base + n;
+      T* dst = Bs + (size_t)n * p.LDB + kv;
+      if (gn < N && kv < K) cp8(dst, B + (size_t)gn * g.ldb + kv, K - kv);
+      else zero8(dst);
+    }
     for (int c = tid; c < 4 * p.NGtot; c += 256) red[c] = 0.f;
     if constexpr (LAZY) {
       for (int s = 0; s < g.pyr.nseg; ++s) {
@@ -1227,10 +1239,16 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
 #pragma unroll
     for (int u = 0; u < PW_NV; ++u) {
       const int v = tid + u * 256;
+#pragma unroll
+      for (int ww = 0; ww < VW; ++ww) ra[u][ww] = V{};
       const int r = v / KV, kv = (v - r * KV) * 8;
       const int grow = rbase + r, gk = kc * p.KC + kv;
       const bool live = v < nvec && grow < M && gk < K;
-      ld_or_zero<VW>(ra[u], reinterpret_cast<const V*>(A + (live ? (size_t)grow * g.lda + gk : 0)), live);
+      if (live) {
+        const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + gk);
+#pragma unroll
+        for (int ww = 0; ww < VW; ++ww) ra[u][ww] = src[ww];
+      }
       if constexpr (LAZY) {
         if (has_gate && live) {
           const float4* gp = reinterpret_cast<const float4*>(g.lz.gate + (size_t)((grow - seg_off) / hw) * K + gk);
