@@ -1423,7 +1423,9 @@ static int launch_dws(DwArgs g, hipStream_t s) {
       return check_launch("edet dwconv (rows, squeeze)");
     }
   }
-  if (!WG && dev_knob(18) == 2) {  // development: two steps in flight (forward)
+  // forward: two steps in flight (dw_bwd_probe r03o: 488 -> 480 us over the D0 stride-1 layers;
+  // development slot 18 = 1 selects one)
+  if (!WG && dev_knob(18) != 1) {
     EDET_LAUNCH((k_dws<T, K, S, CPG, false, P, 2>), dim3((unsigned)total), dim3(256), 0, s, g, pl);
     return check_launch("edet dwconv (rows)");
   }

@@ -1833,6 +1833,7 @@ static int dispatch_gemm_kloop(GemmArgs g, hipStream_t s) {
     if (NP <= 320) return launch_gemm<T, 64, 320, LAZY>(g, s);
   }
   // wider outputs (EfficientDet-D4+ project convs: K = 1632 -> N = 448): 128-column tiles
+  // (r03p sweep: 64-deep K chunks, 256-column tiles or both were 1.15-1.8x slower)
   if (cdiv(g.M, 64) < 512) return launch_gemm<T, 32, 128, LAZY>(g, s);
   return launch_gemm<T, 64, 128, LAZY>(g, s);
 }
