@@ -57,6 +57,47 @@ __device__ __forceinline__ void zero8(T* dst) {
   }
 }
 
+// Rows [0, nrows) of a row-major [.][ld] matrix, columns [0, KP) (KP % 8 == 0), into LDS
+// [nrows][lds_ld] with 8 16-byte vectors per thread in flight before any is stored (cp8 per
+// vector waits for each load inside its branch: one round trip per vector, 7 per 64-row chunk at
+// K = 224); rows at or past nvalid and elements at or past K are written as zeros.
+template <typename T>
+__device__ __forceinline__ void stage_rows(T* lds, int lds_ld, const T* src, int ld, int nrows, int nvalid,
+                                           int K, int KP) {
+  using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
+  constexpr int VW = sizeof(T) == 2 ? 1 : 2, U = 8;
+  const int kv8 = KP / 8, total = nrows * kv8;
+  for (int v0 = 0; v0 < total; v0 += 256 * U) {
+    V t[U][VW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v = v0 + threadIdx.x + u * 256;
+      const int n = v / kv8, kv = (v - n * kv8) * 8;
+      const bool ok = v < total && n < nvalid && kv < K;
+      const V* p = reinterpret_cast<const V*>(src + (ok ? (size_t)n * ld + kv : 0));
+#pragma unroll
+      for (int w = 0; w < VW; ++w) t[u][w] = p[w];
+#pragma unroll
+      for (int w = 0; w < VW; ++w) t[u][w] = ok ? t[u][w] : V{};
+      if (ok && K - kv < 8) {  // tail vector: zero the elements at or past K
+        T* e = reinterpret_cast<T*>(&t[u][0]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j >= K - kv) e[j] = T(0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int v = v0 + threadIdx.x + u * 256;
+      if (v < total) {
+        const int n = v / kv8, kv = (v - n * kv8) * 8;
+#pragma unroll
+        for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(lds + (size_t)n * lds_ld + kv)[w] = t[u][w];
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ bf16x8_t lds_frag_bf16(const uint16_t* p) {
   uint4 v = *reinterpret_cast<const uint4*>(p);
   return __builtin_bit_cast(bf16x8_t, v);
@@ -323,7 +364,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 constexpr int RNB = 64;
 
 template <typename T, int BM, bool LAZY>
-__global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, int cps, int LDC) {
+__global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, int cps, int LDC, int bstage) {
   constexpr int WM = BM / 2, FM = WM / 16, FN = 2;
   const int LDA = KP + 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -415,6 +456,10 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   constexpr int VWB = sizeof(T) == 2 ? 1 : 2, NBV = 4;
   VB rb[NBV][VWB];
   auto load_b = [&](int ch, T* bs) {  // in place (global -> LDS)
+    if (bstage) {
+      stage_rows(bs, LDA, B + (size_t)ch * RNB * g.ldb, g.ldb, RNB, N - ch * RNB, K, KP);
+      return;
+    }
     for (int v = tid; v < RNB * kv8; v += 256) {
       const int n = v / kv8, kv = (v - n * kv8) * 8;
       const int gn = ch * RNB + n, nk = K - kv;
@@ -1523,7 +1568,11 @@ static int dispatch_pwb(const GemmArgs& g, hipStream_t s, bool& done) {
   // column group and loses
   const int KP = cdiv(g.K, 32) * 32;
   const bool lazy_in = LAZY;
-  if (ks || !(lazy_in ? (g.N >= 192 && KP <= 96) : (g.N >= 128 && KP <= 192))) return EDET_OK;
+  // D4+ (224-channel BiFPN and heads): K = 224 into N >= 192 also wins B-resident (the A-resident
+  // form holds one block per CU there and re-stages B per row tile: D4 conv1x1 18.9 -> 17.7 ms per
+  // step in kbench, r03t; wherever the plan fits, D0 lost 0.5 ms)
+  const bool wide224 = g.N >= 192 && KP > 192 && KP <= 224;
+  if (!wide224 && (ks || !(lazy_in ? (g.N >= 192 && KP <= 96) : (g.N >= 128 && KP <= 192)))) return EDET_OK;
   // except the stage-6 expand dgrad (8192 x 192 -> 1152): the A-resident form is faster there
   // (90 -> 63 us for its three calls, kbench round 2)
   if (g.M <= 8192 && g.N >= 1024) return EDET_OK;
@@ -1810,7 +1859,10 @@ static int launch_gemm_r(GemmArgs g, hipStream_t s) {
   // resident blocks per CU from the LDS image; the row-tile workers per split fill that once
   const int per_cu = max(1, min(8, (int)((160 * 1024) / lds)));
   const int G = min(ntm, max(1, cdiv(256 * per_cu, nsplit)));
-  EDET_LAUNCH((k_gemm_r<T, BM, LAZY>), dim3(G * nsplit), dim3(256), lds, s, g, KP, nsplit, cps, LDC);
+  // in-place B chunk loads batched (stage_rows) for K > 128: D4 (K = 224 BiFPN / head convs)
+  // conv1x1 19.5 -> 18.9 ms per step in kbench, D0 even (r03r); development slot 24 = 2: cp8 loop
+  const int bstage = dev_knob(24) != 2;
+  EDET_LAUNCH((k_gemm_r<T, BM, LAZY>), dim3(G * nsplit), dim3(256), lds, s, g, KP, nsplit, cps, LDC, bstage);
   return check_launch("edet gemm_r");
 }
 
