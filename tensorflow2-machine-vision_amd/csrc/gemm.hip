@@ -1801,6 +1801,13 @@ static int launch_gemm_s_n(const GemmArgs& g, hipStream_t s) {
   }
 }
 
+template <typename T, bool LAZY, int KS>
+static int launch_gemm_s_nf(const GemmArgs& g, int nf, hipStream_t s) {  // N <= 48
+  if (nf <= 1) return launch_gemm_s<T, LAZY, 1, KS>(g, s);
+  if (nf == 2) return launch_gemm_s<T, LAZY, 2, KS>(g, s);
+  return launch_gemm_s<T, LAZY, 3, KS>(g, s);
+}
+
 // K <= 32 and N <= 160 (a lazy A on one segment), and 32 < K <= 64, N <= 96 for a plain A
 // (the 1x1 dgrads and the BiFPN / head pointwise convs), with BN statistics per segment on
 // pyramids: rows between segments are padding, only ever written
@@ -1817,6 +1824,24 @@ static int dispatch_gemm_s(const GemmArgs& g, hipStream_t s, bool& done) {
   if (!LAZY && g.K <= 64 && g.N <= 96) {
     done = true;
     return launch_gemm_s_n<T, LAZY, 2>(g, s);
+  }
+  // narrow outputs (N <= 48) over a deeper plain A (K <= 256): 2M x 96 -> 16 dgrad 259 -> 94 us,
+  // 524288 x 144 -> 24 fwd 97 -> 33 us, dgrad 84 -> 29 us, 131072 x 240 -> 40 fwd 33 -> 24 us
+  // (kbench r03w / r03x: conv1x1 4.86 -> 4.45 ms per step; the A-resident form staged the A tile
+  // through LDS for a 16- to 40-column product).  Development slot 23 = 2: off
+  if constexpr (!LAZY && sizeof(T) == 2) {
+    if (dev_knob(23) != 2 && g.K <= 256 && g.N <= 48) {
+      done = true;
+      const int nf = cdiv(g.N, 16);
+      switch (cdiv(g.K, 32)) {
+        case 3: return launch_gemm_s_nf<T, LAZY, 3>(g, nf, s);
+        case 4: return launch_gemm_s_nf<T, LAZY, 4>(g, nf, s);
+        case 5: return launch_gemm_s_nf<T, LAZY, 5>(g, nf, s);
+        case 6: return launch_gemm_s_nf<T, LAZY, 6>(g, nf, s);
+        case 7: return launch_gemm_s_nf<T, LAZY, 7>(g, nf, s);
+        default: return launch_gemm_s_nf<T, LAZY, 8>(g, nf, s);
+      }
+    }
   }
   return EDET_OK;
 }

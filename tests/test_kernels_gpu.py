@@ -35,7 +35,10 @@ def pyr_data(rng, pyr, C, dt, scale=1.0):
                                             (600, 16, 96, 1, 1), (300, 1152, 320, 1, 1), (260, 320, 1152, 0, 1),
                                             (640, 672, 112, 0, 1),
                                             # D4's 224-channel BiFPN / head convs (B-resident form)
-                                            (900, 224, 224, 3, 2), (1100, 224, 224, 0, 1), (500, 224, 729, 3, 1)])
+                                            (900, 224, 224, 3, 2), (1100, 224, 224, 0, 1), (500, 224, 729, 3, 1),
+                                            # narrow outputs over a deeper plain A (wave-streaming form)
+                                            (2000, 96, 16, 0, 1), (1500, 144, 24, 0, 1), (900, 160, 32, 0, 2),
+                                            (700, 240, 40, 0, 1)])
 def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
     rng = np.random.default_rng(M + K + N)
     pyr = Pyr(2, [(13, 11), (7, 5)]) if nseg == 2 else Pyr(1, [(M, 1)])
@@ -59,7 +62,7 @@ def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("M,N,K,ldy", [(300, 40, 24, 40), (777, 729, 64, 736), (2048, 1152, 192, 1152),
                                        (500, 320, 1152, 320), (300, 36, 64, 40), (1000, 224, 224, 224),
-                                       (600, 729, 224, 736)])
+                                       (600, 729, 224, 736), (2000, 96, 16, 96), (1500, 144, 24, 144)])
 def test_conv1x1_dgrad(dt, M, N, K, ldy):
     rng = np.random.default_rng(M * 7 + N)
     pyr = Pyr(1, [(M, 1)])
