@@ -1821,6 +1821,12 @@ static int dispatch_gemm_s(const GemmArgs& g, hipStream_t s, bool& done) {
     done = true;
     return launch_gemm_s_n<T, LAZY, 1>(g, s);
   }
+  // a lazy A up to K = 64 into N <= 64 on one segment (131072 x 40 -> 64 with BN + swish: 43 ->
+  // 25 us; route sweep r03y)
+  if (LAZY && g.K <= 64 && g.N <= 64 && g.pyr.nseg == 1) {
+    done = true;
+    return launch_gemm_s_n<T, LAZY, 2>(g, s);
+  }
   if (!LAZY && g.K <= 64 && g.N <= 96) {
     done = true;
     return launch_gemm_s_n<T, LAZY, 2>(g, s);
@@ -1917,11 +1923,55 @@ static int dispatch_gemm_kloop(GemmArgs g, hipStream_t s) {
 
 template <typename T, bool LAZY>
 static int dispatch_gemm(GemmArgs g, hipStream_t s) {
+  const int KP0 = cdiv(g.K, 32) * 32;
+#ifdef EDET_DEV
+  // development slot 26: force a kernel family where it applies (1 = wave-streaming, 2 =
+  // B-resident, 3 = A-resident, 4 = K loop) for route sweeps; otherwise the production rules
+  if (const int route = dev_knob(26)) {
+    const int KP = cdiv(g.K, 32) * 32, LDCf = cdiv(g.N, 8) * 8;
+    if (route == 1 && sizeof(T) == 2 && g.K % 8 == 0 && g.N % 8 == 0 && !g.accumulate && g.ldc % 8 == 0 &&
+        g.lda % 8 == 0 && g.ldb % 8 == 0 && g.K <= 256 && g.N <= 160 && (!LAZY || g.pyr.nseg == 1)) {
+      switch (cdiv(g.K, 32)) {
+        case 1: return launch_gemm_s_n<T, LAZY, 1>(g, s);
+        case 2: return launch_gemm_s_n<T, LAZY, 2>(g, s);
+        case 3: return launch_gemm_s_n<T, LAZY, 3>(g, s);
+        case 4: return launch_gemm_s_n<T, LAZY, 4>(g, s);
+        case 5: return launch_gemm_s_n<T, LAZY, 5>(g, s);
+        case 6: return launch_gemm_s_n<T, LAZY, 6>(g, s);
+        case 7: return launch_gemm_s_n<T, LAZY, 7>(g, s);
+        default: return launch_gemm_s_n<T, LAZY, 8>(g, s);
+      }
+    }
+    if (route == 2 && g.ldc % 8 == 0 && g.lda % 8 == 0 && g.K % 8 == 0 && g.M > 0) {
+      PwPlan p;
+      int FN;
+      bool ks;
+      if (pw_plan(g, LAZY, sizeof(T), p, FN, ks)) {
+        if (!ks) return launch_pwb<T, 2, false, LAZY>(g, p, s);
+        if (FN == 2) return launch_pwb<T, 2, true, LAZY>(g, p, s);
+        return launch_pwb<T, 1, true, LAZY>(g, p, s);
+      }
+    }
+    if (route == 3 && g.K <= 512) {
+      if (gemm_r_lds<T, 128, LAZY>(g.K, KP, LDCf) <= 96 * 1024) return launch_gemm_r<T, 128, LAZY>(g, s);
+      if (gemm_r_lds<T, 64, LAZY>(g.K, KP, LDCf) <= 96 * 1024) return launch_gemm_r<T, 64, LAZY>(g, s);
+      if (gemm_r_lds<T, 32, LAZY>(g.K, KP, LDCf) <= 96 * 1024) return launch_gemm_r<T, 32, LAZY>(g, s);
+    }
+    if (route == 4) return dispatch_gemm_kloop<T, LAZY>(g, s);
+  }
+#endif
   {
     bool done = false;
     const int rc = dispatch_gemm_s<T, LAZY>(g, s, done);
     if (done || rc) return rc;
   }
+  // route sweep over every D0 conv1x1 launch (r03y, development slot 26): past the
+  // wave-streaming shapes, the pipelined K loop beats the B- and A-resident forms for a plain A
+  // without BN statistics (the 1x1 dgrads and the box predict: 32768 x 112 -> 672 dgrad 93 -> 47
+  // us, 174592 x 64 -> 36 38 -> 14 us; about -150 us per step), and for a lazy A with K > 64 into
+  // N > 320 (32768 x 80 -> 480: 106 -> 87 us).  D4's K = 224 convs stay B-resident (below).
+  const bool wide224 = g.N >= 192 && KP0 > 192 && KP0 <= 224;
+  if ((!LAZY && !g.has_stats && !wide224) || (LAZY && g.K > 64 && g.N > 320)) return dispatch_gemm_kloop<T, LAZY>(g, s);
   {
     bool done = false;
     const int rc = dispatch_pwb<T, LAZY>(g, s, done);
@@ -1932,10 +1982,9 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
   const int KP = cdiv(g.K, 32) * 32;
   const int LDCf = cdiv(g.N, 8) * 8;
   constexpr size_t BUDGET = 96 * 1024;
-  // lazy A with K >= 112 into N > 320 (the stage 5-7 expand convs): the A-resident form walks
-  // its column chunks one dependent B load at a time with 2 blocks per CU; the pipelined
-  // K loop over 128-column tiles measured 1.3-1.4x faster (8192x192x1152, 32768x112x672)
-  if (LAZY && g.K >= 112 && g.N > 320) return dispatch_gemm_kloop<T, LAZY>(g, s);
+  // (lazy A with K > 64 into N > 320 took the K loop above: the A-resident form walks its
+  // column chunks one dependent B load at a time with 2 blocks per CU; 8192x192x1152,
+  // 32768x112x672 measured 1.3-1.4x faster on the K loop)
   if (g.K <= 512) {
     // the largest row tile that still gives >= 256 (row tile, column chunk) blocks: at M = 8192
     // the 128-row tiles left 64 blocks for 256 CUs (8192 x 320 -> 64: 21 us)

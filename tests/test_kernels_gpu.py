@@ -38,8 +38,14 @@ def pyr_data(rng, pyr, C, dt, scale=1.0):
                                             (900, 224, 224, 3, 2), (1100, 224, 224, 0, 1), (500, 224, 729, 3, 1),
                                             # narrow outputs over a deeper plain A (wave-streaming form)
                                             (2000, 96, 16, 0, 1), (1500, 144, 24, 0, 1), (900, 160, 32, 0, 2),
-                                            (700, 240, 40, 0, 1)])
+                                            (700, 240, 40, 0, 1),
+                                            # route rules of round 3: lazy K <= 64 into N <= 64 (wave
+                                            # streaming), lazy K > 64 into N > 320 (K loop), plain without
+                                            # statistics (K loop; the stats-free call is below)
+                                            (1000, 40, 64, 1, 1), (700, 80, 480, 3, 1)])
 def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
+    """conv1x1 forward with BN statistics (and without them for plain inputs: the stats-free
+    route) against fp64."""
     rng = np.random.default_rng(M + K + N)
     pyr = Pyr(2, [(13, 11), (7, 5)]) if nseg == 2 else Pyr(1, [(M, 1)])
     x = pyr_data(rng, pyr, K, dt)
@@ -57,6 +63,10 @@ def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
         close(y[sl], ref[sl], dt)
         close(st[s][0], ref[sl].sum(0), dt, scale=pyr.seg_rows(s) ** 0.5 * 4)
         close(st[s][1], (ref[sl] ** 2).sum(0), dt, scale=pyr.seg_rows(s) ** 0.5 * 8, rtol=5e-2 if dt == "bf16" else 1e-4)
+    if not lazy:  # the same product without statistics (box / class predict convs) takes another route
+        y2 = torch.empty_like(y)
+        L.call("edet_conv1x1_fwd", DT[dt], lz.c, pyr.c, K, vp(w), N, vp(b), vp(y2), N, 0, None, stream())
+        close(y2, ref, dt)
 
 
 @pytest.mark.parametrize("dt", DTS)
