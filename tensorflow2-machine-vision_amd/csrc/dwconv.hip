@@ -2034,6 +2034,11 @@ constexpr int DW_GRID_FWD = 2048, DW_GRID_WGRAD = 4096;
 
 static DwForm dw_form_prod(int which, int K, int S, int C, int nseg);
 static DwForm dw_form(int which, int K, int S, int C, int nseg, long rows_in) {
+#ifdef EDET_DEV
+  // development slot 27: force a form (1 TILE, 2 DW3, 3 DIRECT, 4 DW4, 5 ROWS) for route sweeps;
+  // launch_dw falls back to a form the direction implements
+  if (const int f = dev_knob(27)) return (DwForm)(f - 1);
+#endif
   const bool direct_ok = C <= 2048;
   const bool dw4_ok = C % 8 == 0;  // channel rows split over blockIdx.y past 256 vectors
   if (which == 0) {
@@ -2047,9 +2052,13 @@ static DwForm dw_form(int which, int K, int S, int C, int nseg, long rows_in) {
     // round-2 form sweep (kbench --dev): the 8x8 tiles for the C = 64 heads / BiFPN levels at
     // 32x32 and the pyramid (209 -> 192 us for the 8 head calls), rows for k3 s1 at
     // 32768 x 480 (63 -> 57 us)
-    if (K == 3 && S == 1 && C == 64 && (nseg > 1 || rows_in <= 32768)) return DW_TILE;
-    if (K == 3 && S == 1 && C == 480 && rows_in <= 32768) return DW_ROWS;
-    if (C <= 2048 && (K == 5 || (S == 1 && C <= 144) || (S == 2 && C >= 192))) return DW_ROWS;
+    // round-3 form sweep (development slot 27, r03aa; the rows kernels lost their serial
+    // filter-tap prologue this round): rows for the C = 64 pyramid (189 -> 174 us), k3 s2 at
+    // C = 96 (166 -> 159) and k3 s1 at C >= 480 (16^2 x 1152: 24 -> 20); the 8x8 tiles keep the
+    // single C = 64 BiFPN levels from 4096 to 32768 rows (43 vs 51 us at 32768)
+    if (K == 3 && S == 1 && C == 64 && nseg == 1 && rows_in >= 4096 && rows_in <= 32768) return DW_TILE;
+    if (K == 3 && S == 1 && C >= 480 && C <= 2048) return DW_ROWS;
+    if (C <= 2048 && (K == 5 || (S == 1 && C <= 144) || (S == 2 && C >= 96))) return DW_ROWS;
     if ((K == 3 && S == 2 && C >= 192) || (S == 1 && C == 240) || C > 2048) return DW_DW3;
     return DW_TILE;
   }
@@ -2065,7 +2074,8 @@ static DwForm dw_form(int which, int K, int S, int C, int nseg, long rows_in) {
   if (S == 1 && C == 64 && nseg == 1 && rows_in <= 8192) return DW_DW3;
   if (S == 1 && C == 64 && nseg > 1) return DW_ROWS;
   if (K == 5 && S == 1 && C == 1152) return DW_ROWS;
-  if (nseg == 1 && C <= 672 && (K == 5 || S == 1 || C >= 192)) return DW_ROWS;
+  // (k3 s2 at C = 240 took the rows form until round 3: 8x8 tiles 30 vs 32 us, r03aa)
+  if (nseg == 1 && C <= 672 && (K == 5 || S == 1)) return DW_ROWS;
   return (S == 1 && (C <= 64 || (K == 5 && C == 240))) ? DW_DW3 : DW_TILE;
 }
 
