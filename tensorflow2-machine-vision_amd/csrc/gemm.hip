@@ -2096,8 +2096,13 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
     // 2048 x 320 -> 64: 10.6 -> 7.7); >= 16 stages for many tiles over M <= 32768 (32768 x 112
     // -> 672: 36.8 -> 32.1 us), the class predict (106 -> 100) and M >= 524288 (38 -> 35)
     // (profiles/r02b_wgrad_plan_sweep.txt)
+    // The BiFPN 64 -> 64 convs (one tile, M <= 32768) want ~8192 blocks of >= 2 stages (512 x 64
+    // -> 64: 23.5 -> 18.0 us per step, 2048: 47.5 -> 37.2, 32768: 74.7 -> 66.9); a few tiles over
+    // M <= 8192 >= 4 stages (8192 x 320 -> 64: 33.9 -> 28.5) (profiles/r03ab_wgrad_plan_sweep.txt)
     int target = 2048, min_stages = 8;
-    if (tiles == 1 || g.M <= 4096) target = 4096, min_stages = 4;
+    if (tiles == 1 && g.M <= 32768) target = 8192, min_stages = 2;
+    else if (tiles == 1 || g.M <= 4096) target = 4096, min_stages = 4;
+    else if (tiles <= 8 && g.M <= 8192) min_stages = 4;
     else if ((tiles >= 22 && g.M <= 32768) || (tiles >= 12 && g.M >= 131072) || g.M >= 524288) min_stages = 16;
     if (dev_knob(0) > 0) target = dev_knob(0);
     if (dev_knob(1) > 0) min_stages = dev_knob(1);

@@ -93,7 +93,8 @@ def test_conv1x1_dgrad(dt, M, N, K, ldy):
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("K,N,lazy,nseg", [(24, 40, 0, 1), (96, 144, 1, 1), (64, 729, 0, 2), (40, 64, 2, 2),
                                            (16, 96, 0, 1), (32, 16, 0, 1), (144, 24, 0, 1), (1152, 320, 0, 1),
-                                           (112, 672, 0, 1), (64, 36, 0, 2), (240, 40, 0, 1), (40, 240, 0, 2)])
+                                           (112, 672, 0, 1), (64, 36, 0, 2), (240, 40, 0, 1), (40, 240, 0, 2),
+                                           (64, 64, 1, 1), (64, 64, 2, 2), (320, 64, 0, 1)])
 def test_conv1x1_wgrad(dt, K, N, lazy, nseg):
     rng = np.random.default_rng(K * 13 + N)
     pyr = Pyr(3, [(17, 9), (5, 3)]) if nseg == 2 else Pyr(2, [(37, 29)])
