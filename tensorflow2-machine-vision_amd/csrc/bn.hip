@@ -788,11 +788,18 @@ int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, i
   // (scripts/row_probe.py: -20..-30 % on the C >= 240 and C = 16 layers, equal elsewhere).
   // 32 passes for the wide layers (kbench sweep, round 2: 524288 x 144 60 -> 52 us, 32768 x 480
   // 24 -> 21 us)
-  g.geo = row_geom(C, dev_knob(10) > 0 ? dev_knob(10) : (C >= 144 && p->nseg == 1 ? 32 : 16));
+  // Round 3 (profiles/r03ad_bn_plan_sweep.txt): short rows want shorter chunks, 8 passes for
+  // C <= 64 and 16 for C >= 144 at M <= 8192 (8192 x 192: 36.2 -> 29.9 us per step, the BiFPN
+  // 2048 x 64: 43.3 -> 37.1), and the narrow C <= 24 tensors 256 blocks (2M x 16: 31.5 -> 28.0)
+  const int M = pyr_valid_rows(*p);
+  int passes = C >= 144 && p->nseg == 1 ? 32 : 16;
+  if (M <= 8192 && C < 1024) passes = C <= 64 ? 8 : 16;  // D4's 8192 x 2688 keeps 32 (46.6 vs 64.0 us)
+  g.geo = row_geom(C, dev_knob(10) > 0 ? dev_knob(10) : passes);
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 2 * C * sizeof(float2) + 2 * (size_t)g.geo.R * C * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    const int rcap = dev_knob(11) > 0 ? dev_knob(11) : 512;  // persistent blocks (r01h sweep: 1.51 -> 1.43 ms/step against 1024)
+    // persistent blocks (r01h sweep: 1.51 -> 1.43 ms/step against 1024)
+    const int rcap = dev_knob(11) > 0 ? dev_knob(11) : (C <= 24 ? 256 : 512);
     const int grid = nb < rcap ? nb : rcap;
     const int f = (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0);
     if (nb) launch_reduce<T>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
@@ -816,7 +823,17 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
   g.dsq = dsq; g.C = C; g.accumulate = accumulate;
   // short chunks (persistent grid): 2.25 -> 2.21 ms/step against 8-16 passes; 8 from C = 480 up
   // (fewer, longer-lived blocks: M = 8192, C = 1152: 25 -> 21 us; kbench sweep, round 2)
-  g.geo = row_geom(C, dev_knob(8) > 0 ? dev_knob(8) : (C >= 480 ? 8 : 4));
+  // Round 3 (profiles/r03ad_bn_plan_sweep.txt): the BiFPN C = 64 levels at M <= 8192 2 passes
+  // (8192 x 64 +sw: 26.5 -> 22.8 us per step), SE-gated 96 <= C < 480 8 (524288 x 96: 63.8 ->
+  // 59.3, 32768 x 240: 15.0 -> 12.9), C >= 672 over M >= 32768 16 (32768 x 672: 84.8 -> 79.8),
+  // C < 1024 over M <= 8192 4 (8192 x 672: 13.9 -> 12.4)
+  const int M = pyr_valid_rows(*p);
+  int passes = C >= 480 ? 8 : 4;
+  if (C <= 64 && M <= 8192) passes = 2;
+  else if (x->gate && C >= 96 && C < 480) passes = 8;
+  else if (C >= 672 && M >= 32768) passes = 16;
+  else if (C >= 480 && C < 1024 && M <= 8192) passes = 4;
+  g.geo = row_geom(C, dev_knob(8) > 0 ? dev_knob(8) : passes);
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 3 * C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {
@@ -954,7 +971,11 @@ int edet_lazy_materialize(int dtype, const edet_lazy* x, const edet_pyramid* p, 
   LArgs g{};
   g.lz = *x; g.p = *p; g.dx = out; g.C = C;
   // 0.60 -> 0.56 ms/step against ~8 passes; 8 for C >= 1024 (M = 8192, C = 1152: 15 -> 13 us)
-  g.geo = row_geom(C, dev_knob(13) > 0 ? dev_knob(13) : (C >= 1024 ? 8 : 4));
+  // and 8 for 144 <= C over 32768 <= M <= 131072 (32768 x 480: 42.4 -> 40.5 us per step,
+  // profiles/r03ad_bn_plan_sweep.txt)
+  const int M = pyr_valid_rows(*p);
+  const bool mid = C >= 144 && M >= 32768 && M <= 131072;
+  g.geo = row_geom(C, dev_knob(13) > 0 ? dev_knob(13) : (C >= 1024 || mid ? 8 : 4));
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {

@@ -184,6 +184,11 @@ __host__ __device__ __forceinline__ int seg_of_row(const edet_pyramid& p, int ro
     if (row >= p.row_off[i]) s = i;
   return s;
 }
+__host__ __device__ __forceinline__ int pyr_valid_rows(const edet_pyramid& p) {
+  int n = 0;
+  for (int i = 0; i < p.nseg; ++i) n += seg_rows(p, i);
+  return n;
+}
 __host__ __device__ __forceinline__ int pyr_total_rows(const edet_pyramid& p) {
   return p.row_off[p.nseg - 1] + seg_rows(p, p.nseg - 1);
 }

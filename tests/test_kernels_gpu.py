@@ -287,11 +287,15 @@ def test_dwconv_long_blocks(k, s, B, H, C):
 # ----------------------------------------------------------------- lazy backward (BN train bwd)
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("C,act,gate,dsq,scale,nseg", [(40, 0, 0, 0, 0, 1), (96, 1, 1, 1, 0, 1), (64, 1, 0, 0, 1, 2),
-                                                        (144, 1, 0, 0, 0, 1)])
+                                                        (144, 1, 0, 0, 0, 1), (24, 0, 0, 0, 0, 1), (240, 1, 1, 0, 0, 1),
+                                                        (672, 1, 1, 1, 0, 1), (672, 1, 0, 0, 0, 1)])
 def test_lazy_backward(dt, C, act, gate, dsq, scale, nseg):
     rng = np.random.default_rng(C + act * 7 + nseg)
     B = 3
     pyr = Pyr(B, [(11, 7), (6, 4)]) if nseg == 2 else Pyr(B, [(9, 10)])
+    if C == 672:  # M = 32768: the long-chunk plans of the wide layers
+        B = 32
+        pyr = Pyr(B, [(32, 32)])
     x = pyr_data(rng, pyr, C, dt, scale=2.0)
     bn = make_bn(x, pyr, C, rng)
     gt = g(torch.rand(B, C) + 0.5, "f32") if gate else None
