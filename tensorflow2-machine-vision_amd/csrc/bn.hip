@@ -832,7 +832,7 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
   if (C <= 64 && M <= 8192) passes = 2;
   else if (x->gate && C >= 96 && C < 480) passes = 8;
   else if (C >= 672 && M >= 32768) passes = 16;
-  else if (C >= 480 && C < 1024 && M <= 8192) passes = 4;
+  else if (C >= 480 && C <= 672 && M <= 8192) passes = 4;  // not D4's 8192 x 960 (15.3 vs 17.6 us)
   g.geo = row_geom(C, dev_knob(8) > 0 ? dev_knob(8) : passes);
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 3 * C * sizeof(float2);

@@ -981,6 +981,9 @@ static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s) {
   long rows_in = 0;
   for (int i = 0; i < g.pin.nseg; ++i) rows_in += (long)g.pin.batch * g.pin.H[i] * g.pin.W[i];
   if (K == 5) cap = rows_in <= 8192 ? 1024 : 2048;
+  // round 3 (profiles/r03af_launch_size_sweep.txt): 1024 up to 32768 input rows at k5 (8192 x 672
+  // out: 29.9 -> 24.1 us) and up to 131072 at k3 (32768 x 240 out: 21.1 -> 17.8 us)
+  if ((K == 5 && rows_in <= 32768) || (K == 3 && rows_in <= 131072)) cap = 1024;
   if (dev_knob(14) > 0) cap = dev_knob(14);
   const int grid = (int)std::max<long>(1, std::min<long>(cap, (patches + geo.R - 1) / geo.R));
   if (patches) EDET_LAUNCH((k_dw4_dgrad<T, K, S, CPT, 2, 2>), dim3(grid * ncs), dim3(geo.TPR * geo.R), 0, s, g, geo);
@@ -1399,6 +1402,9 @@ static int launch_dws(DwArgs g, hipStream_t s) {
   } else {
     if (rows_in <= 32768 && g.C >= 256) target = DWS_BLOCKS / 2;
     else if (K == 3 && S == 1 && rows_in >= 524288) target = 2 * DWS_BLOCKS;
+    // the 256^2 stride-2 k3 forward: 4096 blocks (151.3 -> 140.8 us per step,
+    // profiles/r03af_launch_size_sweep.txt)
+    else if (S == 2 && rows_in >= 2097152) target = 4 * DWS_BLOCKS;
   }
   if (dev_knob(6) > 0) target = dev_knob(6);
   // rows per block: the most that still leaves >= target blocks, at least 2
@@ -1983,6 +1989,11 @@ static int launch_dwb(DwArgs g, const edet_bngrad64& fold, hipStream_t s) {
   int target = DWS_BLOCKS;
   if (K == 5) target = DWS_BLOCKS / 2;
   else if (rows_in >= 524288) target = 2 * DWS_BLOCKS;
+  // round 3 (profiles/r03af_launch_size_sweep.txt): the single-level BiFPN C = 64 layers and the
+  // 32 x 32 k5 C = 480 layer want longer strips (32768 x 64: 116.7 -> 92.6 us per step at 512,
+  // 8192 x 64: 71.6 -> 63.1 at 256, 32768 x 480 k5: 73.5 -> 69.3 at 256)
+  if (g.C <= 64 && g.pin.nseg == 1 && rows_in <= 32768) target = rows_in <= 8192 ? 256 : 512;
+  else if (K == 5 && g.C <= 480 && rows_in <= 32768) target = 256;
   if (dev_knob(16) > 0) target = dev_knob(16);
   for (int TH = 256; TH >= 2; TH /= 2) {
     if (TH > 2 * hmax && TH > 2) continue;
