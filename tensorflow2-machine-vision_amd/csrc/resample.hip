@@ -566,29 +566,31 @@ __global__ __launch_bounds__(256) void k_fuse_fwd(FuseArgs g) {
     load_affine(g.in[i].v, g.C, 1.f / (float)(g.B * g.in[i].H * g.in[i].W), aft + i * g.C);
   __syncthreads();
   const int nv = g.C / 8;
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long)g.B * g.H * g.W * nv) return;
-  const int cv = (int)(idx % nv);
-  const long pix = idx / nv;
-  const int n = (int)(pix / ((long)g.H * g.W));
-  const int rem = (int)(pix - (long)n * g.H * g.W);
-  const int h = rem / g.W, w = rem - h * g.W;
+  const long total = (long)g.B * g.H * g.W * nv;
   const float den = fuse_denom(g.w, g.n_in);
-  float o[8];
-  for (int i = 0; i < g.n_in; ++i) {
-    const edet_fuse_input& fi = g.in[i];
-    float2 af[8];
-    affine8_lds(aft + i * g.C, cv * 8, af);
-    float v[8];
-    fuse_input_value<T>(fi, af, n, h, w, g.H, g.W, cv * 8, v, (size_t)pix, g.C, true);
-    const float wn = g.w[i] / den;  // one division per input, not per element
+  // grid-stride over the vectors: a capped grid amortises the per-block affine tables
+  for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const int cv = (int)(idx % nv);
+    const long pix = idx / nv;
+    const int n = (int)(pix / ((long)g.H * g.W));
+    const int rem = (int)(pix - (long)n * g.H * g.W);
+    const int h = rem / g.W, w = rem - h * g.W;
+    float o[8];
+    for (int i = 0; i < g.n_in; ++i) {
+      const edet_fuse_input& fi = g.in[i];
+      float2 af[8];
+      affine8_lds(aft + i * g.C, cv * 8, af);
+      float v[8];
+      fuse_input_value<T>(fi, af, n, h, w, g.H, g.W, cv * 8, v, (size_t)pix, g.C, true);
+      const float wn = g.w[i] / den;  // one division per input, not per element
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float t = v[j] * wn;
-      o[j] = (i == 0) ? t : o[j] + t;
+      for (int j = 0; j < 8; ++j) {
+        const float t = v[j] * wn;
+        o[j] = (i == 0) ? t : o[j] + t;
+      }
     }
+    st8((T*)g.out + (size_t)pix * g.C + cv * 8, o);
   }
-  st8((T*)g.out + (size_t)pix * g.C + cv * 8, o);
 }
 
 template <typename T>
@@ -817,7 +819,9 @@ int edet_bifpn_fuse_fwd(int dtype, int n_in, const edet_fuse_input* ins, const f
   EDET_REQUIRE(out, "bifpn_fuse_fwd: null out");
   g.out = out;
   const long n = (long)B * H * W * (C / 8);
-  const int nb = (int)((n + 255) / 256);
+  int nb = (int)((n + 255) / 256);
+  // development slot 28: grid cap (the kernel strides over the remaining vectors)
+  if (dev_knob(28) > 0 && nb > dev_knob(28)) nb = dev_knob(28);
   EDET_DTYPE_DISPATCH(dtype, T, {
     if (nb) EDET_LAUNCH(k_fuse_fwd<T>, dim3(nb), dim3(256), n_in * C * sizeof(float2), (hipStream_t)stream, g);
     return check_launch("edet bifpn_fuse_fwd");
