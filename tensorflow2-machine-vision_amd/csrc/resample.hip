@@ -820,8 +820,11 @@ int edet_bifpn_fuse_fwd(int dtype, int n_in, const edet_fuse_input* ins, const f
   g.out = out;
   const long n = (long)B * H * W * (C / 8);
   int nb = (int)((n + 255) / 256);
-  // development slot 28: grid cap (the kernel strides over the remaining vectors)
-  if (dev_knob(28) > 0 && nb > dev_knob(28)) nb = dev_knob(28);
+  // at most 2048 blocks striding over the vectors, so each block's affine tables serve more
+  // than 32 pixels (D4 1605 -> 1401 us, D0 282 -> 271 us per step; profiles/r03ah_fuse_grid.txt).
+  // Development slot 28 overrides the cap.
+  const int cap = dev_knob(28) > 0 ? dev_knob(28) : 2048;
+  if (nb > cap) nb = cap;
   EDET_DTYPE_DISPATCH(dtype, T, {
     if (nb) EDET_LAUNCH(k_fuse_fwd<T>, dim3(nb), dim3(256), n_in * C * sizeof(float2), (hipStream_t)stream, g);
     return check_launch("edet bifpn_fuse_fwd");

@@ -458,9 +458,10 @@ def test_maxpool(dt, H, W):
 
 
 @pytest.mark.parametrize("dt", DTS)
-def test_bifpn_fuse(dt):
+@pytest.mark.parametrize("B,H,W", [(2, 8, 8), (4, 136, 136)])  # the second exceeds the forward's 2048-block grid
+def test_bifpn_fuse(dt, B, H, W):
     rng = np.random.default_rng(11)
-    B, C, H, W = 2, 64, 8, 8
+    C = 64
     ins = []
     specs = [((H, W), L.MODE_SAME), ((H // 2, W // 2), L.MODE_UPSAMPLE), ((H * 2, W * 2), L.MODE_MAXPOOL)]
     descs = []
