@@ -312,14 +312,26 @@ def probe_roofline(step_fn, funcs, kernel, steps, es):
     return r
 
 
+# workload key of this run ("efficientdet-d0 train B=32 S=512 bf16"); a PMC summary made from
+# another workload (scripts/pmc_*.py --workload) is not evidence about this one
+WORKLOAD_KEY = None
+
+
+def workload_key(model, kind, B, S, dtype):
+    return f"{model} {kind} B={B} S={S} {dtype}"
+
+
 def _pmc_entry(fname, kernel, calls_per_step):
     """``kernel``'s entry of a committed rocprofv3 PMC summary under profiles/, or None when
-    absent or stale: the profiled run's dispatches per step must equal the launches this
-    step makes (a summary from an older tree counts other launches)."""
+    absent or stale: the summary's workload key must be this run's, and the profiled run's
+    dispatches per step must equal the launches this step makes (a summary from an older tree
+    counts other launches)."""
     path = os.path.join(ROOT, "profiles", fname)
     try:
         with open(path) as f:
             d = json.load(f)
+        if WORKLOAD_KEY is None or d.get("workload") != WORKLOAD_KEY:
+            return None
         k = d.get("kernels", {}).get(kernel)
         if k is None:
             return None
@@ -512,6 +524,8 @@ def bench_backbone(args):
     world, rank = ctx.world, ctx.rank
     cfg = get_efficientdet_config("efficientdet-d0", {"image_size": 224})
     B = args.batch
+    global WORKLOAD_KEY
+    WORKLOAD_KEY = workload_key("efficientnet-b0", "backbone", B, 224, args.dtype)
     model = EfficientDetNet(efficientnet_b0_blocks(), cfg, dtype=args.dtype, device=dev, seed=0)
     rng = np.random.default_rng(1000 + rank)
     x = torch.tensor(rng.random((B, 224, 224, 3), dtype=np.float32), device=dev).to(model.eng.tdtype)
@@ -584,6 +598,8 @@ def main():
 
     cfg = get_efficientdet_config(args.model)
     S, B = cfg.image_size, args.batch
+    global WORKLOAD_KEY
+    WORKLOAD_KEY = workload_key(args.model, "train", B, S, args.dtype)
     anchors = Anchors(cfg.min_level, cfg.max_level, (S, S), cfg.num_scales, cfg.aspect_ratios, cfg.anchor_scale, device=dev)
     ar = dp.make_allreduce(ctx)
     model = EfficientDetNetTrain(efficientnet_b0_blocks(), cfg, anchors, dtype=args.dtype, device=dev, seed=0,

@@ -119,7 +119,9 @@ typedef struct edet_sched {
   int32_t warmup_steps, total_steps;
   float momentum, ema_decay, clip_norm, l2_weight;
   float fixed_lr;       /* >0: constant learning rate instead of the cosine schedule */
-  int32_t pad;
+  int32_t skip_nonfinite; /* 1: a step whose gradient norm is NaN / Inf leaves w, v, ema, the
+                             compute copy and the step counter unchanged (scalars[6] = 1); 0 (the
+                             reference's behaviour, efficientdet_net_train.py:129-130): applied */
 } edet_sched;
 
 /* ---- library ---- */
@@ -314,6 +316,7 @@ int edet_detect_nms(int dtype, const float* boxes, const void* cls, int ldc, con
 
 /* ---- optimizer: L2 + clip_by_global_norm + SGD momentum + EMA, fused ----
  * scalars: [0] loss  [1] sum g^2  [2] sum w^2 (L2 params)  [3] gnorm  [4] lr  [5] npos
+ *          [6] 1 when edet_opt_apply skipped a non-finite step (sched->skip_nonfinite), else 0
  * step: device int32 step counter (incremented by edet_opt_apply). */
 /* norm pass: writes EDET_OPT_NORM_BLOCKS per-block partial sums of (g + l2*w)^2 and of
  * w^2 over the L2 prefix to partials[0..255] / partials[256..511] (fp64, device; no atomics);
@@ -325,10 +328,11 @@ int edet_opt_norm(const float* w, const float* g, int64_t n, int64_t n_l2,
 /* apply pass: folds the partials in one fixed order (bit-identical gnorm on every data-parallel
  * replica), clip, SGD momentum, EMA; writes the `dtype` compute copy of w (nullable),
  * scalars[1] = sum g^2, scalars[2] = sum w^2, scalars[3] = gnorm (pre-clip),
- * scalars[0] += l2 * sum w^2 / 2. */
+ * scalars[0] += l2 * sum w^2 / 2, scalars[6] = skipped (0/1).  `step` (nullable): the counter
+ * edet_opt_norm advanced, stepped back when the update is skipped (ABI 7). */
 int edet_opt_apply(float* w, const float* g, float* v, float* ema, int64_t n, int64_t n_l2,
                    const edet_sched* sched, float* scalars, const double* partials, int dtype, void* wcompute,
-                   edet_stream_t stream);
+                   int32_t* step, edet_stream_t stream);
 int edet_cast_f32(int dtype, const float* src, void* dst, int64_t n, edet_stream_t stream);
 /* fp32 [N][K] 1x1 kernels -> `dtype` [K][roundup(N,8)] copies; table[e] = {src_off, dst_off, N, K}
  * (int64, device memory); grid = max_tiles (32x32 tiles of the largest entry) x n_entries */

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--workload", default="efficientdet-d0 train B=32 S=512 bf16",
+                    help="workload key of the profiled command (bench.py workload_key()); bench.py ignores a "
+                         "summary whose key differs from the run it reports")
     a = ap.parse_args()
     files = glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -46,7 +49,7 @@ def main():
                 acc[k]["grbm"] += float(row["Counter_Value"])
             acc[k]["ids"].add(did)
     out = {"source": "rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE; mfma_busy_frac = MFMA busy cycles / "
-                     "(1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)", "tag": a.tag, "steps": a.steps, "kernels": {}}
+                     "(1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)", "tag": a.tag, "workload": a.workload, "steps": a.steps, "kernels": {}}
     for k, v in acc.items():
         n = len(v["ids"])
         if not n or v["grbm"] <= 0:

@@ -47,12 +47,15 @@ def main():
                     help="train steps the profiled command ran (bench.py --steps 3 --warmup 1 --graph 0: 2 eager "
                          "warm-ups + 1 + 3); bench.py uses dispatches / steps to reject a stale entry")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--workload", default="efficientdet-d0 train B=32 S=512 bf16",
+                    help="workload key of the profiled command (bench.py workload_key()); bench.py ignores a "
+                         "summary whose key differs from the run it reports")
     a = ap.parse_args()
     fe = per_kernel(a.fetch, "FETCH_SIZE")
     wr = per_kernel(a.write, "WRITE_SIZE")
     out = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), KiB per dispatch; "
                      "read bytes = 2 x FETCH_SIZE (gfx950 correction), write bytes = WRITE_SIZE",
-           "tag": a.tag, "steps": a.steps, "kernels": {}}
+           "tag": a.tag, "workload": a.workload, "steps": a.steps, "kernels": {}}
     for k in sorted(set(fe) | set(wr)):
         f_kib, nf = fe.get(k, (0.0, 0))
         w_kib, nw = wr.get(k, (0.0, 0))

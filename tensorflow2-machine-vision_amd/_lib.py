@@ -15,7 +15,7 @@ import torch  # noqa: F401
 from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
 
 MAX_SEG = 5
-ABI_VERSION = 6  # must equal edet_abi_version() of the loaded library (struct layouts)
+ABI_VERSION = 7  # must equal edet_abi_version() of the loaded library (struct layouts)
 OPT_NORM_BLOCKS = 256  # EDET_OPT_NORM_BLOCKS: edet_opt_norm partial-sum slots per quantity
 F32, BF16 = 0, 1
 ACT_NONE, ACT_SWISH = 0, 1
@@ -65,7 +65,7 @@ class Sched(ctypes.Structure):
     _fields_ = [("adjusted_lr", c_float), ("warmup_init", c_float), ("warmup_steps", c_int32),
                 ("total_steps", c_int32), ("momentum", c_float), ("ema_decay", c_float),
                 ("clip_norm", c_float), ("l2_weight", c_float), ("fixed_lr", c_float),
-                ("pad", c_int32)]
+                ("skip_nonfinite", c_int32)]
 
 
 P = c_void_p
@@ -117,7 +117,7 @@ SIGNATURES = {
     "edet_decode_boxes": [c_int, P, PPyr, c_int, P, c_int, P, P],
     "edet_detect_nms": [c_int, P, P, c_int, PPyr, c_int, c_int, c_int, c_float, c_float, P, P, P, P, P, P],
     "edet_opt_norm": [P, P, c_int64, c_int64, PSched, P, P, P, P],
-    "edet_opt_apply": [P, P, P, P, c_int64, c_int64, PSched, P, P, c_int, P, P],
+    "edet_opt_apply": [P, P, P, P, c_int64, c_int64, PSched, P, P, c_int, P, P, P],
     "edet_cast_f32": [c_int, P, P, c_int64, P],
     "edet_transpose_cast": [c_int, P, P, P, c_int, c_int, P],
     "edet_bn_inference_stats": [c_int64, P, P, P, P, P, P],

@@ -4,6 +4,8 @@
 //   v = m v - lr g'; w += v                           (Keras SGD momentum, train.py:114-115)
 //   ema -= (1 - d)(ema - w)                           (tfa MovingAverage, train.py:117-119)
 //   lr  = CosineLrSchedule(step)                      (train.py:35-63)
+//   optional: a non-finite gradient norm skips the update (SURVEY §5 failure detection; off by
+//   default, the reference applies it)
 // plus the fp32 -> compute-dtype weight cast, drop-connect masks and device step counter.
 #include <algorithm>
 
@@ -74,9 +76,21 @@ __device__ double2 fold_partials(const double* partials) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_opt_apply(float* w, const float* g, float* v, float* ema, int64_t n,
                                                    int64_t n_l2, edet_sched sc, float* scalars,
-                                                   const double* partials, T* wc) {
+                                                   const double* partials, T* wc, int32_t* step) {
   const double2 sums = fold_partials(partials);
   const float gnorm = (float)sqrt(sums.x);
+  // every block folds the same partials, so every block takes the same branch
+  if (sc.skip_nonfinite && !isfinite(sums.x)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      scalars[1] = (float)sums.x;
+      scalars[2] = (float)sums.y;
+      scalars[3] = gnorm;
+      scalars[0] += (float)((double)sc.l2_weight * 0.5 * sums.y);
+      scalars[6] = 1.f;
+      if (step) *step -= 1;  // the learning-rate schedule does not advance over a skipped step
+    }
+    return;
+  }
   const float clip = sc.clip_norm / fmaxf(gnorm, sc.clip_norm);
   const float lr = scalars[4];
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
@@ -96,6 +110,7 @@ __global__ __launch_bounds__(256) void k_opt_apply(float* w, const float* g, flo
     scalars[2] = (float)sums.y;
     scalars[3] = gnorm;
     scalars[0] += (float)((double)sc.l2_weight * 0.5 * sums.y);
+    scalars[6] = 0.f;
   }
 }
 
@@ -171,11 +186,11 @@ int edet_opt_norm(const float* w, const float* g, int64_t n, int64_t n_l2,
 
 int edet_opt_apply(float* w, const float* g, float* v, float* ema, int64_t n, int64_t n_l2,
                    const edet_sched* sched, float* scalars, const double* partials, int dtype, void* wcompute,
-                   edet_stream_t stream) {
+                   int32_t* step, edet_stream_t stream) {
   EDET_REQUIRE(w && g && v && sched && scalars && partials && n_l2 <= n, "opt_apply: bad argument");
   EDET_DTYPE_DISPATCH(dtype, T, {
     EDET_LAUNCH(k_opt_apply<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, w, g, v, ema, n,
-                       n_l2, *sched, scalars, partials, (T*)wcompute);
+                       n_l2, *sched, scalars, partials, (T*)wcompute, step);
     return check_launch("edet opt_apply");
   });
 }

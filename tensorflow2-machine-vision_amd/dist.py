@@ -126,6 +126,12 @@ def graphed_train_step(model, data, allreduce: Optional[Callable[[torch.Tensor],
     from the capture pool.  Capture runs on torch.cuda.graph's own side stream."""
     if getattr(model, "steps_run", 0) < 1:
         raise RuntimeError("graphed_train_step: run one eager model.train_step(data) first (warm-up)")
+    # the warm-up must have run on these shapes: an eager step at another batch or image size
+    # would leave the persistent buffers sized for it and capture would allocate the rest
+    sig = model.shape_signature(data)
+    if getattr(model, "last_step_signature", None) != sig:
+        raise RuntimeError(f"graphed_train_step: the last eager step ran on {model.last_step_signature}, "
+                           f"not on this data's {sig}; run one eager model.train_step(data) first")
     if allreduce is None:
         # the single graph captures model.train_step, which would call the hooks inside capture
         if model.grad_allreduce is not None or model.npos_allreduce is not None:

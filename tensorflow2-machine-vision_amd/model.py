@@ -440,7 +440,7 @@ class EfficientDetNetTrain(EfficientDetNet):
     def __init__(self, blocks_args=None, global_params: Optional[Config] = None, anchors: Optional[Anchors] = None,
                  name: str = "", min_lr: float = 1e-6, dtype: str = "bf16", device="cuda", seed: int = 0,
                  lr_schedule: Optional[Dict] = None, world_size: int = 1, grad_allreduce=None,
-                 npos_allreduce=None, drop_seed: int = 1234, rank: int = 0):
+                 npos_allreduce=None, drop_seed: int = 1234, rank: int = 0, skip_nonfinite: bool = False):
         super().__init__(blocks_args, global_params, name, dtype, device, seed)
         cfg = self.cfg
         self.anchors = anchors
@@ -468,9 +468,14 @@ class EfficientDetNetTrain(EfficientDetNet):
         sc.clip_norm = s.get("clip_norm", 10.0)
         sc.l2_weight = s.get("l2_weight", 4e-5)
         sc.fixed_lr = s.get("fixed_lr", 0.0)
+        # SURVEY §5 failure detection: a step with a NaN / Inf gradient norm leaves the weights,
+        # optimizer slots and step counter unchanged and reports it in scalars[6] (off by default:
+        # the reference applies every step, efficientdet_net_train.py:129-130)
+        sc.skip_nonfinite = int(bool(skip_nonfinite))
         self.sched = sc
         self.drop_masks = None
         self.steps_run = 0  # compute_step calls (graphed_train_step needs one eager warm-up)
+        self.last_step_signature = None  # shape_signature of the last compute_step's data
         self.fixed_masks = None  # test hook: {'class_net': [rep-1, nseg, B], 'box_net': ...}
 
     # ------------------------------------------------------------------ data
@@ -546,7 +551,15 @@ class EfficientDetNetTrain(EfficientDetNet):
         eng.tape = None
         eng.training = False
         self.steps_run += 1
+        self.last_step_signature = self.shape_signature(data)
         return t
+
+    @staticmethod
+    def shape_signature(data):
+        """(shape, dtype) of the step's input image batch: the persistent buffers of an eager step
+        are sized by it (dist.graphed_train_step checks its warm-up ran on the same shapes)."""
+        x = data[0]
+        return (tuple(x.shape), str(x.dtype))
 
     def forward_backward(self, data):
         """Zero accumulators, targets, N+ (all-reduced when data-parallel), forward, loss,
@@ -562,7 +575,7 @@ class EfficientDetNetTrain(EfficientDetNet):
         L.call("edet_opt_norm", vp(P.w), vp(P.g), P.numel, P.n_l2, self.sched, vp(self.scalars),
                vp(self.norm_partials), vp(self.step_counter), s)
         L.call("edet_opt_apply", vp(P.w), vp(P.g), vp(P.v), vp(P.ema), P.numel, P.n_l2, self.sched, vp(self.scalars),
-               vp(self.norm_partials), self.eng.dt, vp(P.wc) if P.wc is not P.w else None, s)
+               vp(self.norm_partials), self.eng.dt, vp(P.wc) if P.wc is not P.w else None, vp(self.step_counter), s)
         P.refresh_compute_copy(cast=False)  # transposed 1x1 copies for the next dgrad
         cfg = self.cfg
         L.call("edet_bn_update_moving", P.n_bn, vp(P.bn_tstats[0]), vp(P.bn_tstats[1]), vp(P.bn_count),
@@ -617,4 +630,7 @@ class EfficientDetNetTrain(EfficientDetNet):
         if self.grad_allreduce is not None:
             self.grad_allreduce(self.P.g)
         self.apply_gradients()
-        return {"loss": self.scalars[0], "gnorm": self.scalars[3]}
+        out = {"loss": self.scalars[0], "gnorm": self.scalars[3]}
+        if self.sched.skip_nonfinite:
+            out["skipped"] = self.scalars[6]
+        return out

@@ -162,6 +162,9 @@ def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optio
 # input's BatchNorm when this op is the input's only consumer
 FUSED_DW_BWD = os.environ.get("EDET_FUSED_DW", "1") != "0"
 FOLD_DW_BN = os.environ.get("EDET_FOLD_DW_BN", "1") != "0"
+# every switch that takes a BN-backward reduce into the kernel producing the gradient (the test
+# of the folds flips them all: tests/test_model_gpu.py::test_bn_backward_folds_equal_unfused_path)
+FOLD_SWITCHES = ("FUSED_DW_BWD", "FOLD_DW_BN")
 
 def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
            bns: Optional[List[BNParam]] = None, act: int = L.ACT_NONE, name: str = "",

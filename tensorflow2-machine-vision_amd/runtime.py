@@ -415,6 +415,9 @@ class Tape:
         rec = self.g.get(act)
         if rec is not None:
             assert rec.scale is None and rec.ld == act.C, "cannot accumulate into a scaled/strided grad"
+            # a folded gradient already carries its BN-backward sums: a later contribution would
+            # not be in them (a forward op that sends a gradient into `act` skipped consume())
+            assert rec.bn_sums is None, f"gradient of {act} was folded; a later consumer cannot accumulate into it"
             return rec.t, 1
         t = self.eng.empty(act.pyr.rows, act.C)
         self.g[act] = GradRec(t, act.C)

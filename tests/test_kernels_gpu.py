@@ -699,7 +699,7 @@ def test_optimizer_step(steps, start, clip):
         W0 = W.clone()
         L.call("edet_opt_norm", vp(w), vp(gr), n, n_l2, sc, vp(scal), vp(parts), vp(step), stream())
         L.call("edet_opt_apply", vp(w), vp(gr), vp(v), vp(ema), n, n_l2, sc, vp(scal), vp(parts), L.BF16, vp(wc),
-               stream())
+               vp(step), stream())
         gg = G0.clone()
         gg[:n_l2] += 4e-5 * W0[:n_l2]
         gn = gg.norm()
@@ -735,11 +735,52 @@ def test_optimizer_norm_is_bit_reproducible():
         step = torch.zeros(1, dtype=torch.int32, device=DEV)
         L.call("edet_opt_norm", vp(w), vp(gr), n, n_l2, sc, vp(scal), vp(parts), vp(step), stream())
         L.call("edet_opt_apply", vp(w), vp(gr), vp(v), vp(ema), n, n_l2, sc, vp(scal), vp(parts), L.F32, None,
-               stream())
+               vp(step), stream())
         outs.append((scal.clone(), w))
     assert float(outs[0][0][3]) > 10 * sc.clip_norm  # clipping active
     for s, w in outs[1:]:
         assert torch.equal(s[3], outs[0][0][3]) and torch.equal(w, outs[0][1])
+
+
+@pytest.mark.parametrize("bad", [float("nan"), float("inf")])
+def test_optimizer_skips_nonfinite_step(bad):
+    """SURVEY §5 failure detection: with sched.skip_nonfinite a step whose gradient norm is not
+    finite leaves w, v, ema, the compute copy and the step counter unchanged and reports
+    scalars[6] = 1; the next finite step applies normally (scalars[6] = 0).  Without the flag the
+    update is applied as the reference does (the weights become non-finite)."""
+    rng = np.random.default_rng(11)
+    n, n_l2 = 5000, 3000
+    sc = L.Sched()
+    sc.fixed_lr, sc.momentum, sc.ema_decay, sc.clip_norm, sc.l2_weight = 0.01, 0.9, 0.9998, 10.0, 4e-5
+    for flag in (1, 0):
+        sc.skip_nonfinite = flag
+        w, v, ema = g(rnd(rng, n)), g(rnd(rng, n) * 0.1), g(rnd(rng, n))
+        wc = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        L.call("edet_cast_f32", L.BF16, vp(w), vp(wc), n, stream())
+        w0, v0, e0, c0 = w.clone(), v.clone(), ema.clone(), wc.clone()
+        scal = zeros(8)
+        parts = torch.zeros(2 * L.OPT_NORM_BLOCKS, dtype=torch.float64, device=DEV)
+        step = torch.tensor([7], dtype=torch.int32, device=DEV)
+        gr = g(rnd(rng, n))
+        gr[1234] = bad
+        L.call("edet_opt_norm", vp(w), vp(gr), n, n_l2, sc, vp(scal), vp(parts), vp(step), stream())
+        L.call("edet_opt_apply", vp(w), vp(gr), vp(v), vp(ema), n, n_l2, sc, vp(scal), vp(parts), L.BF16, vp(wc),
+               vp(step), stream())
+        torch.cuda.synchronize()
+        assert not math.isfinite(float(scal[3]))
+        if flag:
+            assert float(scal[6]) == 1.0 and int(step.item()) == 7
+            assert torch.equal(w, w0) and torch.equal(v, v0) and torch.equal(ema, e0) and torch.equal(wc, c0)
+            gr = g(rnd(rng, n))  # a finite step afterwards is applied and clears the flag
+            L.call("edet_opt_norm", vp(w), vp(gr), n, n_l2, sc, vp(scal), vp(parts), vp(step), stream())
+            L.call("edet_opt_apply", vp(w), vp(gr), vp(v), vp(ema), n, n_l2, sc, vp(scal), vp(parts), L.BF16,
+                   vp(wc), vp(step), stream())
+            torch.cuda.synchronize()
+            assert float(scal[6]) == 0.0 and int(step.item()) == 8 and not torch.equal(w, w0)
+            assert bool(torch.isfinite(w).all())
+        else:
+            assert float(scal[6]) == 0.0 and int(step.item()) == 8
+            assert not bool(torch.isfinite(w).all())
 
 
 def test_bn_moving_update_and_inference_stats():

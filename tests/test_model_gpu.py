@@ -172,6 +172,40 @@ def test_train_step_parity_fp32():
         np.testing.assert_allclose(sd1[k], v.numpy(), rtol=1e-3, atol=1e-5, err_msg=k)
 
 
+def test_bn_backward_folds_equal_unfused_path():
+    """the BN-backward folds (the input BatchNorm's sums taken inside the kernel that
+    produces its gradient) must give the gradients of the unfused path (reduce + apply passes)
+    on the whole model.  Same weights, inputs, masks and batch statistics; per-tensor gradients
+    within fp32 summation-order noise."""
+    from tf2mv_amd import ops
+    m, anchors = _train_model("f32")
+    x, boxes, cls, n = synth(5)
+    t, *_ = make_targets(m, anchors, boxes, cls, n)
+    m.fixed_masks = {"class_net": torch.tensor(fixed_masks(m)[0]).cuda(), "box_net": torch.tensor(fixed_masks(m)[1]).cuda()}
+    xd = torch.tensor(x).cuda()
+    saved = {k: getattr(ops, k) for k in ops.FOLD_SWITCHES}
+    grads = []
+    try:
+        for on in (True, False):
+            for k in ops.FOLD_SWITCHES:
+                setattr(ops, k, on)
+            m.forward_backward((xd, t))
+            torch.cuda.synchronize()
+            grads.append(m.P.g.clone())
+    finally:
+        for k, v in saved.items():
+            setattr(ops, k, v)
+    a, b = grads
+    gn = float(b.norm())
+    bad = []
+    for k, sp in m.P.specs.items():
+        ga, gb = a[sp.offset: sp.offset + sp.size].double(), b[sp.offset: sp.offset + sp.size].double()
+        err = float((ga - gb).norm())
+        if err > 1e-3 * float(gb.norm()) + 1e-6 * gn:
+            bad.append((k, err, float(gb.norm())))
+    assert not bad, bad[:10]
+
+
 def test_train_step_reference_format_equals_compact():
     m, anchors = _train_model("f32")
     x, boxes, cls, n = synth(4)

@@ -1,4 +1,4 @@
-"""Same-box A/B of two kbench tables per entry point and per launch (tools/gpu_r03n.sh writes
+"""Same-box A/B of two kbench tables per entry point and per launch (tools/gpu_run.sh kbench writes
 kb_<i>_old.txt / kb_<i>_new.txt): python tools/ab_kbench.py DIR"""
 import collections
 import glob

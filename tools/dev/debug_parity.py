@@ -1,6 +1,6 @@
 """Layer-by-layer product vs oracle comparison (forward values or backward d(value)).
 
-    python scripts/debug_parity.py MODEL SIZE BATCH NC DTYPE MODE [TRAINING]
+    python tools/dev/debug_parity.py MODEL SIZE BATCH NC DTYPE MODE [TRAINING]
       MODE fwd : every single-segment activation's value after call(training)
       MODE grad: every activation's d(value) from the tape trace of one forward_backward
 Prints, in execution order, name / relative error (norm of difference over norm of the oracle)

@@ -1,4 +1,4 @@
-"""Per-launch table of a kbench plan sweep (tools/gpu_r03*.sh writes DIR/kb_<variant>_<rep>.txt):
+"""Per-launch table of a kbench plan sweep (tools/gpu_run.sh kbench writes DIR/kb_<variant>_<rep>.txt):
 python tools/sweep_table.py DIR BASELINE_VARIANT [--min-gain 0.05]"""
 import collections
 import glob
