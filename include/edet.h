@@ -97,6 +97,13 @@ typedef struct edet_segout {
   float* b[EDET_MAX_SEG];
 } edet_segout;
 
+/* per-segment fp64 BN-backward sums (dgamma = sum du * xhat, dbeta = sum du), see
+ * edet_lazy_bwd_reduce */
+typedef struct edet_bngrad64 {
+  double* dgamma[EDET_MAX_SEG];
+  double* dbeta[EDET_MAX_SEG];
+} edet_bngrad64;
+
 /* per-segment fp64 BN statistics outputs of a producer: sum and sum of squares */
 typedef struct edet_statout {
   double* sum[EDET_MAX_SEG];
@@ -158,6 +165,16 @@ int edet_conv1x1_fwd(int dtype, const edet_lazy* a, const edet_pyramid* rows, in
 int edet_conv1x1_dgrad(int dtype, const void* dy, int lddy, const edet_pyramid* rows, int N,
                        const void* wkn, int K, void* dx, int lddx, int accumulate,
                        edet_stream_t stream);
+/* edet_conv1x1_dgrad (accumulate = 0) with the BN-backward fold of the value dx is the gradient
+ * of (ABI 7): xv is that value's lazy descriptor (raw x [rows][xv->ld], BN enabled, act, no gate)
+ * and, per segment s and channel k over the valid rows,
+ *   du = dx * act'(bn(x)),  fold->dbeta[s][k] += sum du,  fold->dgamma[s][k] += sum du * xhat
+ * (fp64, caller-zeroed) -- the sums edet_lazy_bwd_reduce(xv, dv = dx) would take, from the stored
+ * dx, in the GEMM's epilogue instead of a pass over (x, dx).  Replaces the reduce of
+ * mb_conv_block.py:143-154's BatchNormalization backward behind the expand conv's dgrad. */
+int edet_conv1x1_dgrad_fold(int dtype, const void* dy, int lddy, const edet_pyramid* rows, int N,
+                            const void* wkn, int K, void* dx, int lddx, const edet_lazy* xv,
+                            const edet_bngrad64* fold, edet_stream_t stream);
 /* dwt[n][k] += sum_m dy[m][n] * v(a)[m][k];  dbias[n] += sum_m dy[m][n]  (valid rows only) */
 int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, int K,
                        const void* dy, int lddy, int N, float* dwt, float* dbias,
@@ -197,10 +214,6 @@ int edet_stem_wgrad(int dtype, const void* x, int B, int H, int W, const void* d
  * apply : dx = scale * (du - dbeta/M - xhat * dgamma/M)   (or du when BN is off);
  *         block 0 also adds the fp32 parameter gradients grads->a[s] += dgamma,
  *         grads->b[s] += dbeta when `grads` is non-NULL */
-typedef struct edet_bngrad64 {
-  double* dgamma[EDET_MAX_SEG];
-  double* dbeta[EDET_MAX_SEG];
-} edet_bngrad64;
 int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, int C,
                          const void* dv, const float* dv_scale, const float* dsq,
                          const edet_bngrad64* acc, edet_stream_t stream);

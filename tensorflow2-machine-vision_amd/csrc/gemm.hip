@@ -27,10 +27,25 @@ struct GemmArgs {
   const float* bias;
   edet_lazy lz;
   edet_pyramid pyr;
-  edet_statout stats;
+  edet_statout stats;  // BN statistics of y, or (FOLD) the folded sums: sum <- dbeta, sq <- dgamma
+  edet_lazy fx;        // FOLD: the value whose gradient y is (raw x, BN, act; no gate)
   int lda, ldb, ldc, M, K, N;
   int accumulate, has_stats, ntm, ntn;
 };
+
+// BN-backward fold (dgrad epilogues): the output y = d(value) of a lazy value v = act(bn(x)) is
+// turned into the two per-channel sums edet_lazy_bwd_reduce would take in its own pass,
+//   du = y * act'(bn(x)),  dbeta += du,  dgamma += du * xhat,
+// from the stored (storage-rounded) y, so the apply pass that later reads y uses sums of exactly
+// the values it applies them to.  Per channel: (bn scale, bn shift, mean, rstd).
+__device__ __forceinline__ float4 fold_table(const edet_bn& bn, int seg, int c, float inv_count) {
+  const float2 af = bn_affine(bn, seg, c, inv_count), mr = bn_mean_rstd(bn, seg, c, inv_count);
+  return make_float4(af.x, af.y, mr.x, mr.y);
+}
+__device__ __forceinline__ void fold_terms(float y, float x, const float4& t, int act, float& du, float& dux) {
+  du = act ? y * dswishf_(x * t.x + t.y) : y;
+  dux = du * ((x - t.z) * t.w);
+}
 
 // raw copy of 8 elements global -> LDS with zero fill past n valid
 template <typename T>
@@ -108,7 +123,7 @@ __device__ __forceinline__ bf16x8_t lds_frag_bf16(const uint16_t* p) {
 // pipelined: chunk k+1 is fetched global -> registers while chunk k's MFMAs run, LDS is
 // double-buffered, one barrier per chunk (the unpipelined loop exposed the full load latency
 // 36 times per tile: 150 GB/s at M = 8192).  B is the [N][K] weight (k contiguous).
-template <typename T, int BM, int BN, int KC, bool LAZY>
+template <typename T, int BM, int BN, int KC, bool LAZY, bool FOLD = false>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   constexpr int KV = KC / 8, LDK = KC + 8;
@@ -116,12 +131,16 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
   constexpr int VW = sizeof(T) == 2 ? 1 : 2;  // 16-byte words per 8 elements
   // A / B chunk buffers, reused after the K loop as the C tile staged for 16-byte row stores
+  // (FOLD: and the folded value's raw x tile behind it)
   constexpr int LDC_S = BN + 8;
-  constexpr int AB_BYTES = 2 * (BM + BN) * LDK * (int)sizeof(T), C_BYTES = BM * LDC_S * (int)sizeof(T);
+  constexpr int AB_BYTES = 2 * (BM + BN) * LDK * (int)sizeof(T);
+  constexpr int C_BYTES = (FOLD ? 2 : 1) * BM * LDC_S * (int)sizeof(T);
   __shared__ __attribute__((aligned(16))) char smem_ab[AB_BYTES > C_BYTES ? AB_BYTES : C_BYTES];
   T (*As)[BM * LDK] = reinterpret_cast<T (*)[BM * LDK]>(smem_ab);
   T (*Bs)[BN * LDK] = reinterpret_cast<T (*)[BN * LDK]>(smem_ab + 2 * BM * LDK * sizeof(T));
   T* Cs = reinterpret_cast<T*>(smem_ab);
+  T* Xs = Cs + BM * LDC_S;         // FOLD
+  __shared__ float4 ftab[FOLD ? BN : 1];
   __shared__ float red[2][2][BN];  // [sum|sq][wm][col]: one writer each, summed in fixed order
   extern __shared__ float2 xf[];   // [K] lazy affine per input channel, then [2][K] gate rows
   float* gts = reinterpret_cast<float*>(xf + (LAZY ? g.K : 0));
@@ -137,6 +156,11 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   const int seg_off = g.pyr.row_off[seg];
   const int seg_end = seg_off + seg_rows(g.pyr, seg);
   const int hw = g.pyr.H[seg] * g.pyr.W[seg];
+  if constexpr (FOLD) {
+    const float inv = 1.f / (float)seg_rows(g.pyr, seg);
+    for (int c = tid; c < BN; c += 256)
+      ftab[c] = col0 + c < g.N ? fold_table(g.fx.bn, seg, col0 + c, inv) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
 
   // SE gate rows of the (at most two, hw >= BM) images this tile spans, staged in LDS once:
   // the per-element global gate loads sat on the chunk loop's critical path
@@ -299,6 +323,23 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   // the chunk buffers), then written as 16-byte row vectors (the MFMA layout's per-lane 2-byte
   // stores left 32-byte pieces of lines: 8192 x 192 -> 1152 ran at 0.65 TB/s)
   T* C = (T*)g.c;
+  constexpr int VPR = BN / 8;  // 8-element vectors per tile row
+  // FOLD: the x tile's vectors are requested before the C tile is staged (their latency overlaps
+  // the staging), then parked in LDS next to it
+  constexpr int NXV = FOLD ? (BM * VPR + 255) / 256 : 1;
+  V xr[NXV][VW];
+  if constexpr (FOLD) {
+    const T* X = (const T*)g.fx.x;
+#pragma unroll
+    for (int u = 0; u < NXV; ++u) {
+      const int e = tid + u * 256, rl = e / VPR, cv = (e - rl * VPR) * 8;
+      const int row = row0 + rl, col = col0 + cv;
+      const bool ok = e < BM * VPR && row < g.M && col < g.N;  // N % 8 == 0: whole vectors
+      const V* src = reinterpret_cast<const V*>(X + (ok ? (size_t)row * g.fx.ld + col : 0));
+#pragma unroll
+      for (int w = 0; w < VW; ++w) xr[u][w] = ok ? src[w] : V{};
+    }
+  }
   float ssum[FN], ssq[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) { ssum[j] = 0.f; ssq[j] = 0.f; }
@@ -313,13 +354,42 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         const int rl = wm * WM + i * 16 + (lane >> 4) * 4 + r, row = row0 + rl;
         const float v = acc[i][j][r] + bv;
         Cs[rl * LDC_S + cl] = from_f<T>(v);
-        if (row < g.M && col < g.N && row < seg_end) { ssum[j] += v; ssq[j] += v * v; }
+        if (!FOLD && row < g.M && col < g.N && row < seg_end) { ssum[j] += v; ssq[j] += v * v; }
+      }
+    }
+  }
+  if constexpr (FOLD) {
+#pragma unroll
+    for (int u = 0; u < NXV; ++u) {
+      const int e = tid + u * 256, rl = e / VPR, cv = (e - rl * VPR) * 8;
+      if (e < BM * VPR) {
+#pragma unroll
+        for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(Xs + rl * LDC_S + cv)[w] = xr[u][w];
       }
     }
   }
   __syncthreads();
+  if constexpr (FOLD) {  // sums of the stored (rounded) values, in the statistics' layout
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int cl = wn * WN + j * 16 + (lane & 15), col = col0 + cl;
+      const float4 t = ftab[cl];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rl = wm * WM + i * 16 + (lane >> 4) * 4 + r, row = row0 + rl;
+          if (row < g.M && col < g.N && row < seg_end) {
+            float du, dux;
+            fold_terms(to_f<T>(Cs[rl * LDC_S + cl]), to_f<T>(Xs[rl * LDC_S + cl]), t, g.fx.act, du, dux);
+            ssum[j] += du;
+            ssq[j] += dux;
+          }
+        }
+      }
+    }
+  }
   {
-    constexpr int VPR = BN / 8;  // 8-element vectors per tile row
     for (int e = tid; e < BM * VPR; e += 256) {
       const int rl = e / VPR, cv = (e - rl * VPR) * 8;
       const int row = row0 + rl, col = col0 + cv;
@@ -1593,11 +1663,13 @@ static int dispatch_pwb(const GemmArgs& g, hipStream_t s, bool& done) {
 // stores, whole rows written by one wave back to back.  BN statistics stay in registers per
 // lane until the end (one lane tree, one LDS pass and one fp64 atomic per channel per block).
 constexpr int GS_PF = 2;  // row groups in flight ahead of the one being computed
-template <typename T, int NF, int KS, bool LAZY>
+template <typename T, int NF, int KS, bool LAZY, bool FOLD = false>
 __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   // BN statistics: per wave and segment (a wave's groups ascend, so it meets each segment
-  // once), summed over the block's waves in a fixed order at the end
+  // once), summed over the block's waves in a fixed order at the end.  FOLD (one segment): the
+  // same machinery carries the BN-backward sums (du, du * xhat) of the value y is the gradient of
   __shared__ float red[EDET_MAX_SEG][2][4][NF * 16];
+  __shared__ float4 ftab[FOLD ? NF * 16 : 1];
   constexpr int LDW = NF * 16 + 8;  // wave-private output staging row (bf16), padded
   __shared__ __attribute__((aligned(16))) uint16_t stg[4][16 * LDW];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1643,6 +1715,11 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
     for (int r = 0; r < 4; ++r) { ss[f][r] = 0.f; sq[f][r] = 0.f; }
   if (g.has_stats)
     for (int i = threadIdx.x; i < EDET_MAX_SEG * 2 * 4 * NF * 16; i += 256) (&red[0][0][0][0])[i] = 0.f;
+  if constexpr (FOLD) {
+    const float inv = 1.f / (float)seg_rows(g.pyr, 0);
+    for (int c = threadIdx.x; c < NF * 16; c += 256)
+      ftab[c] = c < N ? fold_table(g.fx.bn, 0, c, inv) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   int cur_seg = -1, seg_end = g.has_stats ? 0 : M;
   // lanes sharing (lane >> 4) hold the same 4 channels of 16 different rows
   auto wflush = [&](int sg) {
@@ -1670,7 +1747,10 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   const int g_begin = blockIdx.x * gpb, g_end = min(ngroups, g_begin + gpb);
   // the next groups' A rows are fetched before this group's stores are issued (vmcnt
   // counts loads and stores in order: a load issued after the stores would wait for them)
-  auto fetch = [&](int grp, uint4* v) {
+  // FOLD: the folded value's raw x at this lane's output positions (row, 4 channels per
+  // fragment), fetched with the group's A rows
+  const T* X = (const T*)g.fx.x;
+  auto fetch = [&](int grp, uint4* v, uint2* xv) {
     const int row = grp * 16 + (lane & 15);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -1678,10 +1758,20 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
       v[ks] = make_uint4(0, 0, 0, 0);
       if (k < K && grp < g_end) v[ks] = *reinterpret_cast<const uint4*>(A + (size_t)(row < M ? row : 0) * g.lda + k);
     }
+    if constexpr (FOLD) {
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int n0 = 16 * f + 4 * (lane >> 4);
+        const bool ok = n0 < N && grp < g_end && row < M;
+        const uint2 t = *reinterpret_cast<const uint2*>(X + (ok ? (size_t)row * g.fx.ld + n0 : 0));
+        xv[f] = ok ? t : make_uint2(0, 0);
+      }
+    }
   };
   uint4 pre[GS_PF][KS];
+  uint2 prex[GS_PF][FOLD ? NF : 1];
 #pragma unroll
-  for (int u = 0; u < GS_PF; ++u) fetch(g_begin + wave + u * 4, pre[u]);
+  for (int u = 0; u < GS_PF; ++u) fetch(g_begin + wave + u * 4, pre[u], prex[u]);
   for (int grp = g_begin + wave; grp < g_end; grp += 4) {
     const int row = grp * 16 + (lane & 15);
     if (g.has_stats && grp * 16 >= seg_end) {  // wave-uniform; segments start on 128-row multiples
@@ -1694,13 +1784,19 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
     }
     const bool live = row < M && row < seg_end;
     uint4 raw[KS];
+    uint2 xcur[FOLD ? NF : 1];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) raw[ks] = pre[0][ks];
 #pragma unroll
-    for (int u = 0; u + 1 < GS_PF; ++u)
+    for (int f = 0; f < (FOLD ? NF : 1); ++f) xcur[f] = prex[0][f];
+#pragma unroll
+    for (int u = 0; u + 1 < GS_PF; ++u) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) pre[u][ks] = pre[u + 1][ks];
-    fetch(grp + GS_PF * 4, pre[GS_PF - 1]);
+#pragma unroll
+      for (int f = 0; f < (FOLD ? NF : 1); ++f) prex[u][f] = prex[u + 1][f];
+    }
+    fetch(grp + GS_PF * 4, pre[GS_PF - 1], prex[GS_PF - 1]);
     bf16x8_t bfrag[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -1737,7 +1833,16 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         v[r] = d[r] + bias[f][r];
-        if (live) { ss[f][r] += v[r]; sq[f][r] += v[r] * v[r]; }
+        if constexpr (FOLD) {
+          const float xf_ = __uint_as_float(r & 1 ? ((r < 2 ? xcur[f].x : xcur[f].y) & 0xffff0000u)
+                                                  : ((r < 2 ? xcur[f].x : xcur[f].y) << 16));
+          float du, dux;
+          fold_terms(bf2f(f2bf(v[r])), xf_, ftab[n0 + r], g.fx.act, du, dux);
+          if (live && n0 + r < N) { ss[f][r] += du; sq[f][r] += dux; }
+        } else if (live) {
+          ss[f][r] += v[r];
+          sq[f][r] += v[r] * v[r];
+        }
       }
       *reinterpret_cast<uint2*>(cw + (lane & 15) * LDW + n0) =
           make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
@@ -1770,7 +1875,7 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
     }
 }
 
-template <typename T, bool LAZY, int NF, int KS>
+template <typename T, bool LAZY, int NF, int KS, bool FOLD = false>
 static int launch_gemm_s(const GemmArgs& g, hipStream_t s) {
   const int ngroups = (g.M + 15) / 16;
   // 512 blocks (2 per CU): measured best over 512..2048 in the D0 step; 256 for the BiFPN /
@@ -1781,7 +1886,7 @@ static int launch_gemm_s(const GemmArgs& g, hipStream_t s) {
   else if (g.M >= (1 << 21)) cap = 1024;
   if (dev_knob(7) > 0) cap = dev_knob(7);
   const int grid = std::max(1, std::min(cdiv(ngroups, 4), cap));
-  EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY>), dim3(grid), dim3(256), 0, s, g);
+  EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY, FOLD>), dim3(grid), dim3(256), 0, s, g);
   return check_launch("edet gemm_s");
 }
 
@@ -1801,11 +1906,11 @@ static int launch_gemm_s_n(const GemmArgs& g, hipStream_t s) {
   }
 }
 
-template <typename T, bool LAZY, int KS>
+template <typename T, bool LAZY, int KS, bool FOLD = false>
 static int launch_gemm_s_nf(const GemmArgs& g, int nf, hipStream_t s) {  // N <= 48
-  if (nf <= 1) return launch_gemm_s<T, LAZY, 1, KS>(g, s);
-  if (nf == 2) return launch_gemm_s<T, LAZY, 2, KS>(g, s);
-  return launch_gemm_s<T, LAZY, 3, KS>(g, s);
+  if (nf <= 1) return launch_gemm_s<T, LAZY, 1, KS, FOLD>(g, s);
+  if (nf == 2) return launch_gemm_s<T, LAZY, 2, KS, FOLD>(g, s);
+  return launch_gemm_s<T, LAZY, 3, KS, FOLD>(g, s);
 }
 
 // K <= 32 and N <= 160 (a lazy A on one segment), and 32 < K <= 64, N <= 96 for a plain A
@@ -1853,14 +1958,14 @@ static int dispatch_gemm_s(const GemmArgs& g, hipStream_t s, bool& done) {
 }
 
 // ------------------------------------------------------------------ launch helpers
-template <typename T, int BM, int BN, bool LAZY, int KC = 32>
+template <typename T, int BM, int BN, bool LAZY, int KC = 32, bool FOLD = false>
 static int launch_gemm(GemmArgs g, hipStream_t s) {
   g.ntm = cdiv(g.M, BM);
   g.ntn = cdiv(g.N, BN);
   const int nwg = g.ntm * g.ntn;
   if (nwg == 0) return EDET_OK;
   const size_t dyn = LAZY ? (size_t)g.K * (sizeof(float2) + 2 * sizeof(float)) : 0;
-  EDET_LAUNCH((k_gemm<T, BM, BN, KC, LAZY>), dim3(nwg), dim3(256), dyn, s, g);
+  EDET_LAUNCH((k_gemm<T, BM, BN, KC, LAZY, FOLD>), dim3(nwg), dim3(256), dyn, s, g);
   return check_launch("edet gemm");
 }
 
@@ -1898,27 +2003,62 @@ static int launch_gemm_r(GemmArgs g, hipStream_t s) {
 }
 
 // K > 512 with one full-N tile (N <= 320): streaming K loop
-template <typename T, bool LAZY>
+template <typename T, bool LAZY, bool FOLD = false>
 static int dispatch_gemm_kloop(GemmArgs g, hipStream_t s) {
   const int NP = cdiv(g.N, 32) * 32;
-  // BM = 32 when 64-row tiles would leave the chip under-filled
-  if (cdiv(g.M, 64) < 512) {
-    if (NP <= 64) return launch_gemm<T, 32, 64, LAZY>(g, s);
-    if (NP <= 96) return launch_gemm<T, 32, 96, LAZY>(g, s);
-    if (NP <= 128) return launch_gemm<T, 32, 128, LAZY>(g, s);
-    if (NP <= 192) return launch_gemm<T, 32, 192, LAZY>(g, s);
-    if (NP <= 320) return launch_gemm<T, 32, 320, LAZY>(g, s);
-  } else {
-    if (NP <= 64) return launch_gemm<T, 64, 64, LAZY>(g, s);
-    if (NP <= 96) return launch_gemm<T, 64, 96, LAZY>(g, s);
-    if (NP <= 128) return launch_gemm<T, 64, 128, LAZY>(g, s);
-    if (NP <= 192) return launch_gemm<T, 64, 192, LAZY>(g, s);
-    if (NP <= 320) return launch_gemm<T, 64, 320, LAZY>(g, s);
+  // BM = 32 when 64-row tiles would leave the chip under-filled (and for the fp32 fold, whose
+  // staged C and x tiles at 64 x 320 would not fit the LDS)
+  constexpr bool only32 = FOLD && sizeof(T) == 4;
+  if (only32 || cdiv(g.M, 64) < 512) {
+    if (NP <= 64) return launch_gemm<T, 32, 64, LAZY, 32, FOLD>(g, s);
+    if (NP <= 96) return launch_gemm<T, 32, 96, LAZY, 32, FOLD>(g, s);
+    if (NP <= 128) return launch_gemm<T, 32, 128, LAZY, 32, FOLD>(g, s);
+    if (NP <= 192) return launch_gemm<T, 32, 192, LAZY, 32, FOLD>(g, s);
+    if (NP <= 320) return launch_gemm<T, 32, 320, LAZY, 32, FOLD>(g, s);
+  } else if constexpr (!only32) {
+    if (NP <= 64) return launch_gemm<T, 64, 64, LAZY, 32, FOLD>(g, s);
+    if (NP <= 96) return launch_gemm<T, 64, 96, LAZY, 32, FOLD>(g, s);
+    if (NP <= 128) return launch_gemm<T, 64, 128, LAZY, 32, FOLD>(g, s);
+    if (NP <= 192) return launch_gemm<T, 64, 192, LAZY, 32, FOLD>(g, s);
+    if (NP <= 320) return launch_gemm<T, 64, 320, LAZY, 32, FOLD>(g, s);
   }
   // wider outputs (EfficientDet-D4+ project convs: K = 1632 -> N = 448): 128-column tiles
   // (r03p sweep: 64-deep K chunks, 256-column tiles or both were 1.15-1.8x slower)
-  if (cdiv(g.M, 64) < 512) return launch_gemm<T, 32, 128, LAZY>(g, s);
-  return launch_gemm<T, 64, 128, LAZY>(g, s);
+  if constexpr (!only32)
+    if (cdiv(g.M, 64) >= 512) return launch_gemm<T, 64, 128, LAZY, 32, FOLD>(g, s);
+  return launch_gemm<T, 32, 128, LAZY, 32, FOLD>(g, s);
+}
+
+// dgrad with the BN-backward fold of the gradient's value (plain A, no statistics): the
+// wave-streaming form where it applies to one segment, else the K loop (any shape, pyramids)
+template <typename T>
+static int dispatch_dgrad_fold(const GemmArgs& g, hipStream_t s) {
+  if constexpr (sizeof(T) == 2) {
+    const bool vec = g.K % 8 == 0 && g.N % 8 == 0 && g.ldc % 8 == 0 && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
+                     g.fx.ld % 8 == 0 && !g.accumulate && g.pyr.nseg == 1;
+    if (vec && g.K <= 64 && g.N <= 96) {
+      switch (cdiv(g.N, 16)) {
+        case 1: return launch_gemm_s<T, false, 1, 2, true>(g, s);
+        case 2: return launch_gemm_s<T, false, 2, 2, true>(g, s);
+        case 3: return launch_gemm_s<T, false, 3, 2, true>(g, s);
+        case 4: return launch_gemm_s<T, false, 4, 2, true>(g, s);
+        case 5: return launch_gemm_s<T, false, 5, 2, true>(g, s);
+        default: return launch_gemm_s<T, false, 6, 2, true>(g, s);
+      }
+    }
+    if (vec && g.K <= 256 && g.N <= 48) {
+      const int nf = cdiv(g.N, 16);
+      switch (cdiv(g.K, 32)) {
+        case 3: return launch_gemm_s_nf<T, false, 3, true>(g, nf, s);
+        case 4: return launch_gemm_s_nf<T, false, 4, true>(g, nf, s);
+        case 5: return launch_gemm_s_nf<T, false, 5, true>(g, nf, s);
+        case 6: return launch_gemm_s_nf<T, false, 6, true>(g, nf, s);
+        case 7: return launch_gemm_s_nf<T, false, 7, true>(g, nf, s);
+        default: return launch_gemm_s_nf<T, false, 8, true>(g, nf, s);
+      }
+    }
+  }
+  return dispatch_gemm_kloop<T, false, true>(g, s);
 }
 
 template <typename T, bool LAZY>
@@ -2043,6 +2183,28 @@ int edet_conv1x1_dgrad(int dtype, const void* dy, int lddy, const edet_pyramid* 
   g.accumulate = accumulate; g.has_stats = 0;
   hipStream_t s = (hipStream_t)stream;
   EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_gemm<T, false>(g, s); });
+}
+
+int edet_conv1x1_dgrad_fold(int dtype, const void* dy, int lddy, const edet_pyramid* rows, int N,
+                            const void* wkn, int K, void* dx, int lddx, const edet_lazy* xv,
+                            const edet_bngrad64* fold, edet_stream_t stream) {
+  EDET_REQUIRE(dy && rows && wkn && dx && xv && xv->x && fold, "conv1x1_dgrad_fold: null argument");
+  EDET_REQUIRE(lddy % 8 == 0 && K % 8 == 0 && N > 0 && lddx % 8 == 0 && xv->ld % 8 == 0,
+               "conv1x1_dgrad_fold: need lddy, K, lddx, x->ld multiples of 8");
+  EDET_REQUIRE(xv->bn.enabled && xv->gate == nullptr, "conv1x1_dgrad_fold: the folded value needs BN and no gate");
+  EDET_REQUIRE(rows->nseg >= 1 && rows->nseg <= EDET_MAX_SEG, "conv1x1_dgrad_fold: bad pyramid");
+  for (int i = 0; i < rows->nseg; ++i)
+    EDET_REQUIRE(fold->dgamma[i] && fold->dbeta[i], "conv1x1_dgrad_fold: null fold destination (segment %d)", i);
+  GemmArgs g{};
+  g.a = dy; g.b = wkn; g.c = dx; g.bias = nullptr; g.pyr = *rows;
+  g.lda = lddy; g.ldb = cdiv(N, 8) * 8; g.ldc = lddx;
+  g.M = pyr_total_rows(*rows); g.K = N; g.N = K;  // GEMM K = conv out channels
+  g.accumulate = 0;
+  g.has_stats = 1;  // the statistics flush carries (sum du -> dbeta, sum du * xhat -> dgamma)
+  for (int i = 0; i < rows->nseg; ++i) { g.stats.sum[i] = fold->dbeta[i]; g.stats.sq[i] = fold->dgamma[i]; }
+  g.fx = *xv;
+  hipStream_t s = (hipStream_t)stream;
+  EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_dgrad_fold<T>(g, s); });
 }
 
 int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, int K,

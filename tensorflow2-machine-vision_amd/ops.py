@@ -151,7 +151,12 @@ def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optio
                    vp(P.grad(bname) if bname else None), stream())
         s = stream()
         dx, acc = eng.tape.dst(x)
-        L.call("edet_conv1x1_dgrad", eng.dt, vp(d), ld, x.pyr.c, N, vp(P.wtv(wname)), K, vp(dx), K, acc, s)
+        fold = _fold_dst(eng, x, acc) if FOLD_GEMM_BN else None
+        if fold is not None:
+            L.call("edet_conv1x1_dgrad_fold", eng.dt, vp(d), ld, x.pyr.c, N, vp(P.wtv(wname)), K, vp(dx), K, x.lazy(),
+                   fold, s)
+        else:
+            L.call("edet_conv1x1_dgrad", eng.dt, vp(d), ld, x.pyr.c, N, vp(P.wtv(wname)), K, vp(dx), K, acc, s)
 
     eng.record(bwd)
     return out
@@ -162,9 +167,27 @@ def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optio
 # input's BatchNorm when this op is the input's only consumer
 FUSED_DW_BWD = os.environ.get("EDET_FUSED_DW", "1") != "0"
 FOLD_DW_BN = os.environ.get("EDET_FOLD_DW_BN", "1") != "0"
+# the 1x1 dgrad takes the BN-backward sums of its output's value in its epilogue
+# (edet_conv1x1_dgrad_fold) when it owns that value's whole gradient
+FOLD_GEMM_BN = os.environ.get("EDET_FOLD_GEMM_BN", "1") != "0"
 # every switch that takes a BN-backward reduce into the kernel producing the gradient (the test
 # of the folds flips them all: tests/test_model_gpu.py::test_bn_backward_folds_equal_unfused_path)
-FOLD_SWITCHES = ("FUSED_DW_BWD", "FOLD_DW_BN")
+FOLD_SWITCHES = ("FUSED_DW_BWD", "FOLD_DW_BN", "FOLD_GEMM_BN")
+
+
+def _fold_dst(eng: Engine, x: Act, acc: int):
+    """BN-backward fold destination for x's gradient when the op writing it owns all of it (x has
+    one consumer, nothing accumulated yet) and x's value is BN(+act) without an SE gate: zeroed
+    fp64 [2][nseg][C] sums recorded on x's gradient (value_grad_to_raw then skips its reduce pass)
+    and their edet_bngrad64 descriptor; else None."""
+    if not (acc == 0 and x.uses == 1 and x.bns is not None and x.gate is None and x.se is None):
+        return None
+    sums = eng.zeros64(2, len(x.bns), x.C)
+    fold = L.BnGrad64()
+    for i in range(len(x.bns)):
+        fold.dgamma[i], fold.dbeta[i] = sums[0, i].data_ptr(), sums[1, i].data_ptr()
+    eng.tape.g[x].bn_sums = sums
+    return fold
 
 def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
            bns: Optional[List[BNParam]] = None, act: int = L.ACT_NONE, name: str = "",
@@ -194,14 +217,7 @@ def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
             # one pass over (d, x): dx, the filter gradient and, when this op owns x's whole
             # gradient, x's BN-backward sums (the reduce pass of value_grad_to_raw is skipped)
             dx, acc = eng.tape.dst(x)
-            fold = None
-            if (FOLD_DW_BN and acc == 0 and x.uses == 1 and x.bns is not None and x.gate is None
-                    and x.se is None):
-                sums = eng.zeros64(2, len(x.bns), C)
-                fold = L.BnGrad64()
-                for i in range(len(x.bns)):
-                    fold.dgamma[i], fold.dbeta[i] = sums[0, i].data_ptr(), sums[1, i].data_ptr()
-                eng.tape.g[x].bn_sums = sums
+            fold = _fold_dst(eng, x, acc) if FOLD_DW_BN else None
             L.call("edet_dwconv_bwd", eng.dt, x.lazy(), x.pyr.c, C, k, stride, vp(d), pout.c, vp(P.wcv(wname)),
                    vp(dx), acc, vp(P.grad(wname)), fold, stream())
             return

@@ -91,6 +91,63 @@ def test_conv1x1_dgrad(dt, M, N, K, ldy):
 
 
 @pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("M,N,K,act,nseg", [
+    # wave-streaming routes: N <= 96 / K <= 64, N <= 48 / K <= 256 (the D0 expand dgrads: 96 -> 16,
+    # 144 -> 24, 240 -> 40), then the K loop (480 -> 80 with 64-row tiles over M >= 32768,
+    # 1152 -> 192, a 5-level pyramid, an act-free and a swish value)
+    (2000, 96, 16, 0, 1), (1500, 144, 24, 0, 1), (1100, 240, 40, 1, 1), (900, 64, 64, 1, 1),
+    (32768, 480, 80, 0, 1), (1000, 1152, 192, 0, 1), (700, 672, 112, 1, 1), (0, 64, 64, 1, 5),
+    (0, 160, 96, 0, 2)])
+def test_conv1x1_dgrad_fold(dt, M, N, K, act, nseg):
+    """edet_conv1x1_dgrad_fold: dx as edet_conv1x1_dgrad, and the BN-backward sums of the value
+    dx is the gradient of equal to edet_lazy_bwd_reduce over (x, dx) -- the pass the fold
+    replaces (same fp64 destinations; the fold sums the stored dx, so only the order of the
+    fp32 partial sums differs) and to fp64."""
+    rng = np.random.default_rng(M + 3 * N + K + act)
+    if nseg == 5:
+        pyr = Pyr(2, [(16, 16), (8, 8), (4, 4), (2, 2), (1, 1)])
+    elif nseg == 2:
+        pyr = Pyr(3, [(13, 11), (7, 5)])
+    else:
+        pyr = Pyr(1, [(M, 1)])
+    dy = g(rnd(rng, pyr.rows, N), dt)
+    w = g(rnd(rng, N, K, scale=1 / math.sqrt(N)), dt)
+    ldn = (N + 7) // 8 * 8
+    wkn = torch.zeros(K, ldn)
+    wkn[:, :N] = w.float().cpu().t()
+    wkn = g(wkn, dt)
+    x = pyr_data(rng, pyr, K, dt, scale=2.0)
+    for sg in range(nseg - 1):  # padding rows between levels are never read
+        x[pyr.row_off[sg] + pyr.seg_rows(sg):pyr.row_off[sg + 1]] = float("nan")
+    bn = make_bn(x.nan_to_num(0.0), pyr, K, rng)
+    lz = LazyDesc(x, pyr, K, bn=bn, act=act)
+    dx = torch.empty(pyr.rows, K, dtype=TDT[dt], device=DEV)
+    acc_t, acc = bngrad64(nseg, K)
+    L.call("edet_conv1x1_dgrad_fold", DT[dt], vp(dy), N, pyr.c, N, vp(wkn), K, vp(dx), K, lz.c, acc, stream())
+    dx2 = torch.empty_like(dx)
+    L.call("edet_conv1x1_dgrad", DT[dt], vp(dy), N, pyr.c, N, vp(wkn), K, vp(dx2), K, 0, stream())
+    ref_t, ref = bngrad64(nseg, K)
+    L.call("edet_lazy_bwd_reduce", DT[dt], lz.c, pyr.c, K, vp(dx2), None, None, ref, stream())
+    for sg in range(nseg):
+        sl = pyr.seg_slice(sg)
+        assert torch.equal(dx[sl], dx2[sl])
+        n = pyr.seg_rows(sg)
+        close(acc_t[:, sg], ref_t[:, sg], "f32", scale=n ** 0.5, rtol=1e-4)
+        # fp64 from the stored dx
+        xs = x[sl].double().cpu()
+        su, sq, ga, be = (t.double().cpu() for t in bn[sg])
+        mean = su / n
+        rstd = 1 / torch.sqrt(torch.clamp(sq / n - mean * mean, min=0) + 1e-3)
+        u = (xs - mean) * rstd * ga + be
+        du = dx2[sl].double().cpu()
+        if act:
+            sg_ = torch.sigmoid(u)
+            du = du * sg_ * (1 + u * (1 - sg_))
+        close(acc_t[1, sg], du.sum(0), dt, scale=n ** 0.5)
+        close(acc_t[0, sg], (du * (xs - mean) * rstd).sum(0), dt, scale=n ** 0.5)
+
+
+@pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("K,N,lazy,nseg", [(24, 40, 0, 1), (96, 144, 1, 1), (64, 729, 0, 2), (40, 64, 2, 2),
                                            (16, 96, 0, 1), (32, 16, 0, 1), (144, 24, 0, 1), (1152, 320, 0, 1),
                                            (112, 672, 0, 1), (64, 36, 0, 2), (240, 40, 0, 1), (40, 240, 0, 2),
