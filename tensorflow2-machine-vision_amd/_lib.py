@@ -89,6 +89,7 @@ SIGNATURES = {
     "edet_conv1x1_wgrad": [c_int, PLazy, PPyr, c_int, P, c_int, c_int, P, P, P],
     "edet_dwconv_fwd": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, P, PPyr, PStat, P],
     "edet_dwconv_dgrad": [c_int, P, PPyr, c_int, c_int, c_int, P, P, PPyr, c_int, P],
+    "edet_dwconv_dgrad_fold": [c_int, P, PPyr, c_int, c_int, c_int, P, P, PPyr, PLazy, PBnG, P],
     "edet_dwconv_wgrad": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, PPyr, P, P],
     "edet_dwconv_bwd": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, PPyr, P, P, c_int, P, PBnG, P],
     "edet_dwconv_fwd_squeeze": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, P, PPyr, PLazy, P, P],

@@ -875,18 +875,25 @@ template <int CPT, typename T> __device__ __forceinline__ void stv(T* p, const f
   }
 }
 
-template <typename T, int K, int S, int CPT, int PH, int PW>
-__global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo) {
+// FOLD (accumulate == 0): dx is the gradient of the lazy value g.lz = act(bn(x)); the thread also
+// takes that BatchNorm's backward sums of its channels (du = dx * act'(bn(x)) from the stored dx,
+// dbeta += du, dgamma += du * xhat), reduced over the block's pixel rows in a fixed order at the end
+// of every segment and flushed as one fp64 atomic per channel -- the edet_lazy_bwd_reduce pass over
+// (x, dx) folded into the launch that writes dx (mb_conv_block.py:143-147 backward at stride 2)
+template <typename T, int K, int S, int CPT, int PH, int PW, bool FOLD = false>
+__global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo, edet_bngrad64 fold) {
   static_assert(PH % S == 0 && PW % S == 0, "patch must cover whole strides");
   constexpr int DLO = -((K - 1) / S), DHR = (PH - 1) / S, DHC = (PW - 1) / S;
+  extern __shared__ float fred[];  // FOLD: [2][R][TPR * CPT]
   const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
-  if (rr >= geo.R) return;
+  if (rr >= geo.R) return;  // (never: the block is TPR x R threads)
   // channel splits innermost (geo.ncs consecutive logical blocks = one XCD, the same pixels)
   const int bx = xcd_remap(blockIdx.x, gridDim.x), cs = bx % geo.ncs, pb = bx / geo.ncs;
   const int pgrid = gridDim.x / geo.ncs;
   const int c = (cs * geo.TPR + tv) * CPT, C = g.C;
   const T* DY = (const T*)g.dy;
   T* DX = (T*)g.dx;
+  const T* X = (const T*)g.lz.x;
   float w[K * K][CPT];
 #pragma unroll
   for (int i = 0; i < K * K; ++i) ldv<CPT>((const T*)g.w + (size_t)i * C + c, w[i]);
@@ -895,10 +902,35 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo) {
     const int pt = same_pad(H, K, S), pl = same_pad(W, K, S);
     const int PR = cdiv(H + pt, PH), PC = cdiv(W + pl, PW), per_img = PR * PC;
     const int npatch = g.pin.batch * per_img;
+    float ft[CPT][4], fs[CPT], fq[CPT];  // FOLD: (scale, shift, mean, rstd), sums
+    if constexpr (FOLD) {
+      const float inv = 1.f / (float)seg_rows(g.pin, seg);
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) {
+        const float2 af = bn_affine(g.lz.bn, seg, c + j, inv), mr = bn_mean_rstd(g.lz.bn, seg, c + j, inv);
+        ft[j][0] = af.x; ft[j][1] = af.y; ft[j][2] = mr.x; ft[j][3] = mr.y;
+        fs[j] = 0.f;
+        fq[j] = 0.f;
+      }
+    }
     for (int q = pb * geo.R + rr; q < npatch; q += pgrid * geo.R) {
       const int n = q / per_img, rem = q - n * per_img;
       const int pr = rem / PC, pc = rem - pr * PC;
       const int A = pr * (PH / S), Bc = pc * (PW / S);
+      // FOLD: the patch's x vectors requested before the dy loads (select-predicated, in flight
+      // together with them)
+      float xv[FOLD ? PH : 1][FOLD ? PW : 1][CPT];
+      if constexpr (FOLD) {
+        const T* xb = X + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * g.lz.ld + c;
+#pragma unroll
+        for (int e = 0; e < PH; ++e)
+#pragma unroll
+          for (int f = 0; f < PW; ++f) {
+            const int iy = pr * PH + e - pt, ix = pc * PW + f - pl;
+            const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
+            ldv<CPT>(xb + (ok ? (uint32_t)((iy * W + ix) * g.lz.ld) : 0u), xv[e][f]);
+          }
+      }
       const T* dyb = DY + ((size_t)g.pout.row_off[seg] + (size_t)n * OH * OW) * C + c;
       float acc[PH][PW][CPT];
 #pragma unroll
@@ -952,14 +984,39 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo) {
             for (int j = 0; j < CPT; ++j) acc[e][f][j] += o[j];
           }
           stv<CPT>(p, acc[e][f]);
+          if constexpr (FOLD) {
+#pragma unroll
+            for (int j = 0; j < CPT; ++j) {
+              const float y = to_f<T>(from_f<T>(acc[e][f][j])), x = xv[e][f][j];
+              const float du = g.lz.act ? y * dswishf_(x * ft[j][0] + ft[j][1]) : y;
+              fs[j] += du;
+              fq[j] += du * ((x - ft[j][2]) * ft[j][3]);
+            }
+          }
         }
       }
+    }
+    if constexpr (FOLD) {  // fixed-order block reduction, one fp64 atomic per channel and sum
+      const int CB = geo.TPR * CPT, cl = tv * CPT;
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) {
+        fred[rr * CB + cl + j] = fs[j];
+        fred[(geo.R + rr) * CB + cl + j] = fq[j];
+      }
+      __syncthreads();
+      for (int ch = tid; ch < CB; ch += blockDim.x) {
+        float a = 0.f, b = 0.f;
+        for (int i = 0; i < geo.R; ++i) { a += fred[i * CB + ch]; b += fred[(geo.R + i) * CB + ch]; }
+        stat_add(fold.dbeta[seg] + cs * CB + ch, (double)a);
+        stat_add(fold.dgamma[seg] + cs * CB + ch, (double)b);
+      }
+      __syncthreads();
     }
   }
 }
 
-template <typename T, int K, int S>
-static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s) {
+template <typename T, int K, int S, bool FOLD = false>
+static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s, const edet_bngrad64* fold = nullptr) {
   // k5: 4 channels per thread (25 fp32 weights each in registers); 2 channels measured
   // faster only at C = 1152
   constexpr int CPT = K == 3 ? 8 : 4;
@@ -986,7 +1043,10 @@ static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s) {
   if ((K == 5 && rows_in <= 32768) || (K == 3 && rows_in <= 131072)) cap = 1024;
   if (dev_knob(14) > 0) cap = dev_knob(14);
   const int grid = (int)std::max<long>(1, std::min<long>(cap, (patches + geo.R - 1) / geo.R));
-  if (patches) EDET_LAUNCH((k_dw4_dgrad<T, K, S, CPT, 2, 2>), dim3(grid * ncs), dim3(geo.TPR * geo.R), 0, s, g, geo);
+  const edet_bngrad64 fd = fold ? *fold : edet_bngrad64{};
+  const size_t lds = FOLD ? 2 * (size_t)geo.R * geo.TPR * CPT * sizeof(float) : 0;
+  if (patches)
+    EDET_LAUNCH((k_dw4_dgrad<T, K, S, CPT, 2, 2, FOLD>), dim3(grid * ncs), dim3(geo.TPR * geo.R), lds, s, g, geo, fd);
   return check_launch("edet dwconv dgrad");
 }
 
@@ -2218,6 +2278,30 @@ int edet_dwconv_dgrad(int dtype, const void* dy, const edet_pyramid* pout, int C
   DwArgs g{};
   g.dy = dy; g.w = w; g.dx = dx; g.pin = *pin; g.pout = *pout; g.C = C; g.accumulate = accumulate;
   EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_dw<T>(1, k, stride, g, (hipStream_t)stream); });
+}
+
+int edet_dwconv_dgrad_fold(int dtype, const void* dy, const edet_pyramid* pout, int C, int k,
+                           int stride, const void* w, void* dx, const edet_pyramid* pin,
+                           const edet_lazy* xv, const edet_bngrad64* fold, edet_stream_t stream) {
+  EDET_REQUIRE(dy && w && dx && xv && xv->x && fold, "dwconv_dgrad_fold: null argument");
+  EDET_REQUIRE(C % 8 == 0 && xv->ld % 8 == 0, "dwconv_dgrad_fold: need C%%8==0, x->ld%%8==0");
+  EDET_REQUIRE(xv->bn.enabled && xv->gate == nullptr, "dwconv_dgrad_fold: the folded value needs BN and no gate");
+  int rc = check_pyrs(pin, pout, k, stride);
+  if (rc) return rc;
+  for (int i = 0; i < pin->nseg; ++i)
+    EDET_REQUIRE(fold->dgamma[i] && fold->dbeta[i], "dwconv_dgrad_fold: null fold destination (segment %d)", i);
+  DwArgs g{};
+  g.dy = dy; g.w = w; g.dx = dx; g.pin = *pin; g.pout = *pout; g.C = C; g.accumulate = 0;
+  g.lz = *xv; g.x = xv->x;
+  const hipStream_t st = (hipStream_t)stream;
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    if (k == 3 && stride == 1) return launch_dw4_dgrad<T, 3, 1, true>(g, st, fold);
+    if (k == 3 && stride == 2) return launch_dw4_dgrad<T, 3, 2, true>(g, st, fold);
+    if (k == 5 && stride == 1) return launch_dw4_dgrad<T, 5, 1, true>(g, st, fold);
+    if (k == 5 && stride == 2) return launch_dw4_dgrad<T, 5, 2, true>(g, st, fold);
+    set_error("dwconv_dgrad_fold: unsupported kernel %d stride %d", k, stride);
+    return EDET_EUNSUPPORTED;
+  });
 }
 
 int edet_dwconv_wgrad(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,

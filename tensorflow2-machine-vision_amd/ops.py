@@ -226,7 +226,12 @@ def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
                    stream())
         s = stream()
         dx, acc = eng.tape.dst(x)
-        L.call("edet_dwconv_dgrad", eng.dt, vp(d), pout.c, C, k, stride, vp(P.wcv(wname)), vp(dx), x.pyr.c, acc, s)
+        fold = _fold_dst(eng, x, acc) if FOLD_DW_BN else None
+        if fold is not None:
+            L.call("edet_dwconv_dgrad_fold", eng.dt, vp(d), pout.c, C, k, stride, vp(P.wcv(wname)), vp(dx), x.pyr.c,
+                   x.lazy(), fold, s)
+        else:
+            L.call("edet_dwconv_dgrad", eng.dt, vp(d), pout.c, C, k, stride, vp(P.wcv(wname)), vp(dx), x.pyr.c, acc, s)
 
     eng.record(bwd)
     return out

@@ -313,6 +313,36 @@ def test_dwconv_bwd_fused(dt, k, H, W, C, act, nseg, fold, acc):
         torch.testing.assert_close(sums_t[:, sg].cpu(), acc2_t[:, sg].cpu(), **tol)
 
 
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("k,s,H,W,C,act,nseg", [(3, 2, 17, 13, 96, 1, 1), (5, 2, 20, 9, 144, 1, 1),
+                                               (3, 2, 33, 32, 240, 1, 1), (5, 2, 9, 8, 672, 0, 1),
+                                               (5, 2, 12, 12, 1152, 1, 1), (3, 1, 0, 0, 64, 1, 2)])
+def test_dwconv_dgrad_fold(dt, k, s, H, W, C, act, nseg):
+    """edet_dwconv_dgrad_fold (the stride-2 MBConv depthwise backward): dx equal to
+    edet_dwconv_dgrad's, and the fold sums of the input's BN equal to edet_lazy_bwd_reduce over
+    (x, dx) -- the pass it replaces (fp32 partial-sum order only)."""
+    rng = np.random.default_rng(k * 100 + s * 10 + C + act)
+    B = 3
+    pin = Pyr(B, [(11, 7), (6, 4)]) if nseg == 2 else Pyr(B, [(H, W)])
+    pout = pin.strided(s)
+    x = pyr_data(rng, pin, C, dt, scale=2.0)
+    bn = make_bn(x, pin, C, rng)
+    lz = LazyDesc(x, pin, C, bn=bn, act=act)
+    dy = pyr_data(rng, pout, C, dt)
+    w = g(rnd(rng, k * k, C, scale=0.3), dt)
+    dx = torch.empty(pin.rows, C, dtype=TDT[dt], device=DEV)
+    acc_t, acc = bngrad64(nseg, C)
+    L.call("edet_dwconv_dgrad_fold", DT[dt], vp(dy), pout.c, C, k, s, vp(w), vp(dx), pin.c, lz.c, acc, stream())
+    dx2 = torch.empty_like(dx)
+    L.call("edet_dwconv_dgrad", DT[dt], vp(dy), pout.c, C, k, s, vp(w), vp(dx2), pin.c, 0, stream())
+    ref_t, ref = bngrad64(nseg, C)
+    L.call("edet_lazy_bwd_reduce", DT[dt], lz.c, pin.c, C, vp(dx2), None, None, ref, stream())
+    for sg in range(nseg):
+        sl = pin.seg_slice(sg)
+        assert torch.equal(dx[sl], dx2[sl])
+        close(acc_t[:, sg], ref_t[:, sg], "f32", scale=pin.seg_rows(sg) ** 0.5, rtol=1e-4)
+
+
 @pytest.mark.parametrize("k,s,B,H,C", [(5, 1, 16, 64, 240), (3, 1, 8, 100, 64), (5, 2, 16, 72, 144)])
 def test_dwconv_long_blocks(k, s, B, H, C):
     """Forward and weight gradient at batch sizes where a row-streaming block walks many
