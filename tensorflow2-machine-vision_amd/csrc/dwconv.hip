@@ -884,7 +884,9 @@ template <typename T, int K, int S, int CPT, int PH, int PW, bool FOLD = false>
 __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo, edet_bngrad64 fold) {
   static_assert(PH % S == 0 && PW % S == 0, "patch must cover whole strides");
   constexpr int DLO = -((K - 1) / S), DHR = (PH - 1) / S, DHC = (PW - 1) / S;
-  extern __shared__ float fred[];  // FOLD: [2][R][TPR * CPT]
+  extern __shared__ float fred[];  // FOLD: [TPR * CPT] float4 tables, then [2][R][TPR * CPT] sums
+  float4* ftab = reinterpret_cast<float4*>(fred);
+  float* fsum = fred + 4 * geo.TPR * CPT;
   const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
   if (rr >= geo.R) return;  // (never: the block is TPR x R threads)
   // channel splits innermost (geo.ncs consecutive logical blocks = one XCD, the same pixels)
@@ -902,16 +904,19 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo, edet_bn
     const int pt = same_pad(H, K, S), pl = same_pad(W, K, S);
     const int PR = cdiv(H + pt, PH), PC = cdiv(W + pl, PW), per_img = PR * PC;
     const int npatch = g.pin.batch * per_img;
-    float ft[CPT][4], fs[CPT], fq[CPT];  // FOLD: (scale, shift, mean, rstd), sums
+    // FOLD: per channel (scale, shift, mean, rstd) in LDS (registers would cost the occupancy
+    // the patch loop needs), partial sums in registers
+    float fs[CPT], fq[CPT];
     if constexpr (FOLD) {
       const float inv = 1.f / (float)seg_rows(g.pin, seg);
-#pragma unroll
-      for (int j = 0; j < CPT; ++j) {
-        const float2 af = bn_affine(g.lz.bn, seg, c + j, inv), mr = bn_mean_rstd(g.lz.bn, seg, c + j, inv);
-        ft[j][0] = af.x; ft[j][1] = af.y; ft[j][2] = mr.x; ft[j][3] = mr.y;
-        fs[j] = 0.f;
-        fq[j] = 0.f;
+      for (int e = tid; e < geo.TPR * CPT; e += blockDim.x) {
+        const int ch = cs * geo.TPR * CPT + e;
+        const float2 af = bn_affine(g.lz.bn, seg, ch, inv), mr = bn_mean_rstd(g.lz.bn, seg, ch, inv);
+        ftab[e] = make_float4(af.x, af.y, mr.x, mr.y);
       }
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) { fs[j] = 0.f; fq[j] = 0.f; }
+      __syncthreads();
     }
     for (int q = pb * geo.R + rr; q < npatch; q += pgrid * geo.R) {
       const int n = q / per_img, rem = q - n * per_img;
@@ -987,10 +992,11 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo, edet_bn
           if constexpr (FOLD) {
 #pragma unroll
             for (int j = 0; j < CPT; ++j) {
+              const float4 t = ftab[tv * CPT + j];
               const float y = to_f<T>(from_f<T>(acc[e][f][j])), x = xv[e][f][j];
-              const float du = g.lz.act ? y * dswishf_(x * ft[j][0] + ft[j][1]) : y;
+              const float du = g.lz.act ? y * dswishf_(x * t.x + t.y) : y;
               fs[j] += du;
-              fq[j] += du * ((x - ft[j][2]) * ft[j][3]);
+              fq[j] += du * ((x - t.z) * t.w);
             }
           }
         }
@@ -1000,13 +1006,13 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo, edet_bn
       const int CB = geo.TPR * CPT, cl = tv * CPT;
 #pragma unroll
       for (int j = 0; j < CPT; ++j) {
-        fred[rr * CB + cl + j] = fs[j];
-        fred[(geo.R + rr) * CB + cl + j] = fq[j];
+        fsum[rr * CB + cl + j] = fs[j];
+        fsum[(geo.R + rr) * CB + cl + j] = fq[j];
       }
       __syncthreads();
       for (int ch = tid; ch < CB; ch += blockDim.x) {
         float a = 0.f, b = 0.f;
-        for (int i = 0; i < geo.R; ++i) { a += fred[i * CB + ch]; b += fred[(geo.R + i) * CB + ch]; }
+        for (int i = 0; i < geo.R; ++i) { a += fsum[i * CB + ch]; b += fsum[(geo.R + i) * CB + ch]; }
         stat_add(fold.dbeta[seg] + cs * CB + ch, (double)a);
         stat_add(fold.dgamma[seg] + cs * CB + ch, (double)b);
       }
@@ -1018,8 +1024,8 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo, edet_bn
 template <typename T, int K, int S, bool FOLD = false>
 static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s, const edet_bngrad64* fold = nullptr) {
   // k5: 4 channels per thread (25 fp32 weights each in registers); 2 channels measured
-  // faster only at C = 1152
-  constexpr int CPT = K == 3 ? 8 : 4;
+  // faster only at C = 1152.  The fold's x vectors and sums need registers: half the channels
+  constexpr int CPT = FOLD ? (K == 3 ? 4 : 2) : (K == 3 ? 8 : 4);
   DwGeom geo;
   // channel vectors per pixel row split over blockIdx.y until a row fits a block
   int ncs = 1;
@@ -1044,7 +1050,7 @@ static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s, const edet_bngrad64*
   if (dev_knob(14) > 0) cap = dev_knob(14);
   const int grid = (int)std::max<long>(1, std::min<long>(cap, (patches + geo.R - 1) / geo.R));
   const edet_bngrad64 fd = fold ? *fold : edet_bngrad64{};
-  const size_t lds = FOLD ? 2 * (size_t)geo.R * geo.TPR * CPT * sizeof(float) : 0;
+  const size_t lds = FOLD ? (4 + 2 * (size_t)geo.R) * geo.TPR * CPT * sizeof(float) : 0;
   if (patches)
     EDET_LAUNCH((k_dw4_dgrad<T, K, S, CPT, 2, 2, FOLD>), dim3(grid * ncs), dim3(geo.TPR * geo.R), lds, s, g, geo, fd);
   return check_launch("edet dwconv dgrad");
