@@ -918,23 +918,50 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo, edet_bn
       for (int j = 0; j < CPT; ++j) { fs[j] = 0.f; fq[j] = 0.f; }
       __syncthreads();
     }
-    for (int q = pb * geo.R + rr; q < npatch; q += pgrid * geo.R) {
-      const int n = q / per_img, rem = q - n * per_img;
-      const int pr = rem / PC, pc = rem - pr * PC;
-      const int A = pr * (PH / S), Bc = pc * (PW / S);
-      // FOLD: the patch's x vectors requested before the dy loads (select-predicated, in flight
-      // together with them)
-      float xv[FOLD ? PH : 1][FOLD ? PW : 1][CPT];
+    // FOLD: a patch's x vectors are requested one patch ahead (raw, select-predicated): their
+    // latency hides behind the current patch's dy loads and taps
+    using XR = typename std::conditional<sizeof(T) == 2, uint32_t, float>::type;
+    constexpr int XW = sizeof(T) == 2 ? CPT / 2 : CPT;  // raw words per CPT channels
+    XR xnext[FOLD ? PH : 1][FOLD ? PW : 1][XW];
+    auto fetch_x = [&](int qq) {
       if constexpr (FOLD) {
+        const bool live = qq < npatch;
+        const int n = live ? qq / per_img : 0, rem = live ? qq - n * per_img : 0;
+        const int pr = rem / PC, pc = rem - pr * PC;
         const T* xb = X + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * g.lz.ld + c;
 #pragma unroll
         for (int e = 0; e < PH; ++e)
 #pragma unroll
           for (int f = 0; f < PW; ++f) {
             const int iy = pr * PH + e - pt, ix = pc * PW + f - pl;
-            const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
-            ldv<CPT>(xb + (ok ? (uint32_t)((iy * W + ix) * g.lz.ld) : 0u), xv[e][f]);
+            const bool ok = live && iy >= 0 && iy < H && ix >= 0 && ix < W;
+            const XR* p = reinterpret_cast<const XR*>(xb + (ok ? (uint32_t)((iy * W + ix) * g.lz.ld) : 0u));
+#pragma unroll
+            for (int w = 0; w < XW; ++w) xnext[e][f][w] = p[w];
           }
+      }
+    };
+    fetch_x(pb * geo.R + rr);
+    for (int q = pb * geo.R + rr; q < npatch; q += pgrid * geo.R) {
+      const int n = q / per_img, rem = q - n * per_img;
+      const int pr = rem / PC, pc = rem - pr * PC;
+      const int A = pr * (PH / S), Bc = pc * (PW / S);
+      float xv[FOLD ? PH : 1][FOLD ? PW : 1][CPT];
+      if constexpr (FOLD) {
+#pragma unroll
+        for (int e = 0; e < PH; ++e)
+#pragma unroll
+          for (int f = 0; f < PW; ++f)
+#pragma unroll
+            for (int w = 0; w < XW; ++w) {
+              if constexpr (sizeof(T) == 2) {
+                xv[e][f][2 * w] = __uint_as_float(xnext[e][f][w] << 16);
+                xv[e][f][2 * w + 1] = __uint_as_float(xnext[e][f][w] & 0xffff0000u);
+              } else {
+                xv[e][f][w] = xnext[e][f][w];
+              }
+            }
+        fetch_x(q + pgrid * geo.R);
       }
       const T* dyb = DY + ((size_t)g.pout.row_off[seg] + (size_t)n * OH * OW) * C + c;
       float acc[PH][PW][CPT];
@@ -1024,8 +1051,8 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo, edet_bn
 template <typename T, int K, int S, bool FOLD = false>
 static int launch_dw4_dgrad(const DwArgs& g, hipStream_t s, const edet_bngrad64* fold = nullptr) {
   // k5: 4 channels per thread (25 fp32 weights each in registers); 2 channels measured
-  // faster only at C = 1152.  The fold's x vectors and sums need registers: half the channels
-  constexpr int CPT = FOLD ? (K == 3 ? 4 : 2) : (K == 3 ? 8 : 4);
+  // faster only at C = 1152.  The fold's x vectors and sums need registers: 4 channels at k3 too
+  constexpr int CPT = FOLD ? 4 : (K == 3 ? 8 : 4);
   DwGeom geo;
   // channel vectors per pixel row split over blockIdx.y until a row fits a block
   int ncs = 1;

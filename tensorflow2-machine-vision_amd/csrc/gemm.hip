@@ -179,6 +179,23 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 
   const T* A = (const T*)g.a;
   const T* B = (const T*)g.b;
+  // FOLD: the folded value's x tile is requested here, its latency hidden by the whole K loop,
+  // and parked in LDS next to the staged C tile after it
+  constexpr int VPR = BN / 8;  // 8-element vectors per tile row
+  constexpr int NXV = FOLD ? (BM * VPR + 255) / 256 : 1;
+  V xr[NXV][VW];
+  if constexpr (FOLD) {
+    const T* X = (const T*)g.fx.x;
+#pragma unroll
+    for (int u = 0; u < NXV; ++u) {
+      const int e = tid + u * 256, rl = e / VPR, cv = (e - rl * VPR) * 8;
+      const int row = row0 + rl, col = col0 + cv;
+      const bool ok = e < BM * VPR && row < g.M && col < g.N;  // N % 8 == 0: whole vectors
+      const V* src = reinterpret_cast<const V*>(X + (ok ? (size_t)row * g.fx.ld + col : 0));
+#pragma unroll
+      for (int w = 0; w < VW; ++w) xr[u][w] = ok ? src[w] : V{};
+    }
+  }
   struct Chunk {
     V ra[AV][VW], rb[BV][VW];
   };
@@ -323,23 +340,6 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   // the chunk buffers), then written as 16-byte row vectors (the MFMA layout's per-lane 2-byte
   // stores left 32-byte pieces of lines: 8192 x 192 -> 1152 ran at 0.65 TB/s)
   T* C = (T*)g.c;
-  constexpr int VPR = BN / 8;  // 8-element vectors per tile row
-  // FOLD: the x tile's vectors are requested before the C tile is staged (their latency overlaps
-  // the staging), then parked in LDS next to it
-  constexpr int NXV = FOLD ? (BM * VPR + 255) / 256 : 1;
-  V xr[NXV][VW];
-  if constexpr (FOLD) {
-    const T* X = (const T*)g.fx.x;
-#pragma unroll
-    for (int u = 0; u < NXV; ++u) {
-      const int e = tid + u * 256, rl = e / VPR, cv = (e - rl * VPR) * 8;
-      const int row = row0 + rl, col = col0 + cv;
-      const bool ok = e < BM * VPR && row < g.M && col < g.N;  // N % 8 == 0: whole vectors
-      const V* src = reinterpret_cast<const V*>(X + (ok ? (size_t)row * g.fx.ld + col : 0));
-#pragma unroll
-      for (int w = 0; w < VW; ++w) xr[u][w] = ok ? src[w] : V{};
-    }
-  }
   float ssum[FN], ssq[FN];
 #pragma unroll
   for (int j = 0; j < FN; ++j) { ssum[j] = 0.f; ssq[j] = 0.f; }
