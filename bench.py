@@ -79,6 +79,12 @@ def algorithmic_bytes(name, args, es):
     if name == "edet_conv1x1_dgrad":
         p, N, K, acc = args[3], args[4], args[6], args[9]
         return rows(p) * (N + K * (1 + acc)) * es + K * N * es
+    if name == "edet_conv1x1_dgrad_fold":  # dy, x of the folded value, dx
+        p, N, K = args[3], args[4], args[6]
+        return rows(p) * (N + 2 * K) * es + K * N * es
+    if name == "edet_dwconv_dgrad_fold":  # dy, x, dx
+        pout, C, pin = args[2], args[3], args[8]
+        return (rows(pout) + 2 * rows(pin)) * C * es
     if name == "edet_conv1x1_wgrad":
         p, K, N = args[2], args[3], args[6]
         return rows(p) * (K + N) * es
@@ -158,6 +164,10 @@ def shape_tag(name, args):
             return f"in={rows(args[2])} C={args[3]} k={args[4]} s={args[5]}" + (" fold" if args[12] else "")
         if name == "edet_dwconv_dgrad":
             return f"out={rows(args[2])} C={args[3]} k={args[4]} s={args[5]}"
+        if name == "edet_conv1x1_dgrad_fold":
+            return f"M={rows(args[3])} N={args[4]} K={args[6]} fold"
+        if name == "edet_dwconv_dgrad_fold":
+            return f"out={rows(args[2])} C={args[3]} k={args[4]} s={args[5]} fold"
         if name in ("edet_lazy_bwd_reduce", "edet_lazy_bwd_apply", "edet_lazy_materialize"):
             return f"M={rows(args[2])} C={args[3]} {lazy(args[1])}"
     except Exception:  # noqa: BLE001

@@ -198,8 +198,10 @@ int edet_dwconv_dgrad(int dtype, const void* dy, const edet_pyramid* pout, int C
 /* edet_dwconv_dgrad (accumulate = 0) with the BN-backward fold of the value dx is the gradient of
  * (ABI 7): xv = that value's lazy descriptor (raw x on pin's rows, BN enabled, act, no gate);
  * fold->dbeta[s][c] += sum du, fold->dgamma[s][c] += sum du * xhat with du = dx * act'(bn(x)) from
- * the stored dx (fp64, caller-zeroed) -- edet_lazy_bwd_reduce(xv, dv = dx) without its pass.  Used
- * for the stride-2 MBConv depthwise convs (mb_conv_block.py:143-147), whose backward is not fused. */
+ * the stored dx (fp64, caller-zeroed) -- edet_lazy_bwd_reduce(xv, dv = dx) without its pass where
+ * that is faster (measured per shape; elsewhere the library runs the dgrad and the reduce pass).
+ * Used for the stride-2 MBConv depthwise convs (mb_conv_block.py:143-147), whose backward is not
+ * fused. */
 int edet_dwconv_dgrad_fold(int dtype, const void* dy, const edet_pyramid* pout, int C, int k,
                            int stride, const void* w, void* dx, const edet_pyramid* pin,
                            const edet_lazy* xv, const edet_bngrad64* fold, edet_stream_t stream);

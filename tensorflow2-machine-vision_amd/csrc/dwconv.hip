@@ -2323,6 +2323,17 @@ int edet_dwconv_dgrad_fold(int dtype, const void* dy, const edet_pyramid* pout, 
   if (rc) return rc;
   for (int i = 0; i < pin->nseg; ++i)
     EDET_REQUIRE(fold->dgamma[i] && fold->dbeta[i], "dwconv_dgrad_fold: null fold destination (segment %d)", i);
+  // Route (kbench r04d, same box): the folded kernel wins the 256^2 k3 layer (2M x 96: 248 vs
+  // 135 + 140 us for dgrad + reduce); at k5 and on smaller planes the patch kernel's extra x
+  // stream costs more than the reduce pass it saves (524288 x 144 k5: 163 vs 57 + 52 us), so those
+  // run the dgrad and then the reduce pass over (x, dx) -- same results, same destinations
+  long rows_in = 0;
+  for (int i = 0; i < pin->nseg; ++i) rows_in += (long)pin->batch * pin->H[i] * pin->W[i];
+  if (!(k == 3 && rows_in >= (1L << 20))) {
+    rc = edet_dwconv_dgrad(dtype, dy, pout, C, k, stride, w, dx, pin, 0, stream);
+    if (rc) return rc;
+    return edet_lazy_bwd_reduce(dtype, xv, pin, C, dx, nullptr, nullptr, fold, stream);
+  }
   DwArgs g{};
   g.dy = dy; g.w = w; g.dx = dx; g.pin = *pin; g.pout = *pout; g.C = C; g.accumulate = 0;
   g.lz = *xv; g.x = xv->x;
