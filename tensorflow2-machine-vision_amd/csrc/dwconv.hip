@@ -1783,10 +1783,11 @@ __global__ __launch_bounds__(256) void k_dwb(DwArgs g, DwsPlan pl, edet_bngrad64
     for (int i = 0; i < CPG; ++i) {
       const int col = x0 + gc * CPG + i;
       if (col < W && cvalid) {
-        DX[(size_t)(r * W + col) * C + c] = from_f<T>(g.accumulate ? to_f<T>(dold[i]) + dxv[i] : dxv[i]);
-        if constexpr (FOLD) {
-          const float xv = to_f<T>(xr[i]);
-          const float du = act ? dxv[i] * dswishf_(xv * myaf.x + myaf.y) : dxv[i];
+        const T st = from_f<T>(g.accumulate ? to_f<T>(dold[i]) + dxv[i] : dxv[i]);
+        DX[(size_t)(r * W + col) * C + c] = st;
+        if constexpr (FOLD) {  // from the stored dx (the apply pass reads that value)
+          const float xv = to_f<T>(xr[i]), yv = to_f<T>(st);
+          const float du = act ? yv * dswishf_(xv * myaf.x + myaf.y) : yv;
           fs += du;
           fq += du * ((xv - mymr.x) * mymr.y);
         }
@@ -2028,10 +2029,11 @@ __global__ __launch_bounds__(256) void k_dwb2(DwArgs g, DwsPlan pl, edet_bngrad6
       for (int i = 0; i < CPG; ++i) {
         const int col = x0 + gc * CPG + i, r = r0 + j + p;
         if (col < W && cvalid && j + p < nrows) {
-          DX[(size_t)(r * W + col) * C + c] = from_f<T>(g.accumulate ? to_f<T>(dold[p][i]) + dxv[p][i] : dxv[p][i]);
-          if constexpr (FOLD) {
-            const float xv = to_f<T>(xr[p][i]);
-            const float du = act ? dxv[p][i] * dswishf_(xv * myaf.x + myaf.y) : dxv[p][i];
+          const T st = from_f<T>(g.accumulate ? to_f<T>(dold[p][i]) + dxv[p][i] : dxv[p][i]);
+          DX[(size_t)(r * W + col) * C + c] = st;
+          if constexpr (FOLD) {  // from the stored dx (the apply pass reads that value)
+            const float xv = to_f<T>(xr[p][i]), yv = to_f<T>(st);
+            const float du = act ? yv * dswishf_(xv * myaf.x + myaf.y) : yv;
             fs += du;
             fq += du * ((xv - mymr.x) * mymr.y);
           }
@@ -2057,6 +2059,285 @@ __global__ __launch_bounds__(256) void k_dwb2(DwArgs g, DwsPlan pl, edet_bngrad6
     if (i < K * K) atomicAdd(g.dw + (size_t)i * C + c0 + cc, sum);
     else if constexpr (FOLD) stat_add((i == K * K ? fold.dbeta[seg] : fold.dgamma[seg]) + c0 + cc, (double)sum);
   }
+}
+
+// ------------------------------------------------------------------ tiled fused backward (stride 1)
+// The same three results as k_dwb (dx, the filter gradient, the input BN's backward sums) with
+// no row-serial ring: a block owns one image x 16 channels and walks `tpb` 16 x 16 pixel tiles.
+// Per tile every dy and x vector of the (16 + K - 1)^2 halo window is requested at once (all in
+// flight together), dy is parked in LDS as stored and v(x) = act(bn(x)) * gate once in fp32,
+// then thread (channel c, patch row pr, wave = patch column) computes a 4 x 4 pixel patch of its
+// channel straight from LDS: dx from the dy window (the channel's K*K taps in registers), the
+// filter gradient from the v window against the patch's own dy (accumulated in registers over
+// all the block's tiles), both from the same (K + 3) x (K + 3) window rows.  dx goes back through
+// LDS and leaves as 16-byte vectors.  Two barriers per tile instead of one per output row: the
+// 32 x 32 and 16 x 16 planes of the late MBConv stages (where k_dwb's rings hold a handful of
+// rows per block and wait on memory between them) become a few fully overlapped load rounds.
+// LDS rows are padded so a wave's four patch rows (4 image rows apart) fall in disjoint banks.
+constexpr int DWT_T = 16;   // tile edge
+constexpr int DWT_CB = 16;  // channels per block
+
+struct DwtPlan {
+  int ntx[EDET_MAX_SEG];     // tiles across an image
+  int ntiles[EDET_MAX_SEG];  // tiles per image
+  int chunks[EDET_MAX_SEG];  // tile chunks (of tpb tiles) per image
+  int nblk[EDET_MAX_SEG];    // blocks of the segment: batch * chunks * ncg
+  int tpb, ncg;
+};
+
+template <typename T, int K, bool FOLD>
+__global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64 fold) {
+  constexpr int P = (K - 1) / 2, IT = DWT_T + K - 1, NPX = IT * IT;
+  constexpr int EPV = 16 / (int)sizeof(T);  // elements per 16-byte vector
+  constexpr int VPP = DWT_CB / EPV;         // vectors per pixel (16 channels)
+  constexpr int NV = NPX * VPP, NL = (NV + 255) / 256;
+  constexpr int KK = K * K;
+  // padded row strides (elements): 4 rows apart land 16 (dy bf16: 8) dwords apart in the banks
+  constexpr int DRS = IT * DWT_CB + (sizeof(T) == 2 ? 8 : 4), VRS = IT * DWT_CB + 4;
+  __shared__ __attribute__((aligned(16))) T dys[IT * DRS];       // dy window as stored; dx stage
+  __shared__ __attribute__((aligned(16))) float vs[IT * VRS];    // v(x) window; reductions
+  __shared__ __attribute__((aligned(16))) T xs[FOLD ? DWT_T * DWT_T * DWT_CB : 8];  // raw x, interior
+  __shared__ float2 af[DWT_CB];
+  __shared__ float gt[DWT_CB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  int id = xcd_remap(blockIdx.x, gridDim.x), seg = 0;
+  while (seg < g.pin.nseg - 1 && id >= pl.nblk[seg]) id -= pl.nblk[seg++];
+  const int cg = id % pl.ncg;
+  id /= pl.ncg;
+  const int chunk = id % pl.chunks[seg], n = id / pl.chunks[seg];
+  const int c0 = cg * DWT_CB, C = g.C;
+  const int H = g.pin.H[seg], W = g.pin.W[seg];
+  const T* X = (const T*)g.x + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * g.lz.ld + c0;
+  const T* DY = (const T*)g.dy + ((size_t)g.pout.row_off[seg] + (size_t)n * H * W) * C + c0;
+  T* DX = (T*)g.dx + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * C + c0;
+  const float inv = 1.f / (float)seg_rows(g.pin, seg);
+  if (tid < DWT_CB) {
+    af[tid] = bn_affine(g.lz.bn, seg, c0 + tid, inv);
+    gt[tid] = g.lz.gate ? g.lz.gate[(size_t)n * C + c0 + tid] : 1.f;
+  }
+  // this thread: channel c, the 4 x 4 patch at rows a0 .., columns b0 .. of every tile
+  const int c = lane & 15, a0 = (lane >> 4) * 4, b0 = wave * 4;
+  float w[KK];
+  load_taps(w, (const T*)g.w, C, c0 + c, true);
+  float4 ft = make_float4(0.f, 0.f, 0.f, 1.f);  // fold: this channel's (scale, shift, mean, rstd)
+  if constexpr (FOLD) {
+    const float2 a = bn_affine(g.lz.bn, seg, c0 + c, inv), m = bn_mean_rstd(g.lz.bn, seg, c0 + c, inv);
+    ft = make_float4(a.x, a.y, m.x, m.y);
+  }
+  float dwa[KK];
+#pragma unroll
+  for (int i = 0; i < KK; ++i) dwa[i] = 0.f;
+  float fs = 0.f, fq = 0.f;
+  const int act = g.lz.act;
+  const int t_begin = chunk * pl.tpb, t_end = min(pl.ntiles[seg], t_begin + pl.tpb);
+  for (int t = t_begin; t < t_end; ++t) {
+    const int y0 = (t / pl.ntx[seg]) * DWT_T, x0 = (t % pl.ntx[seg]) * DWT_T;
+    // ---- the halo window of dy and x: every vector requested before any is used
+    uint4 rd[NL], rx[NL];
+    uint32_t okm = 0;
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      const int e = tid + u * 256, px = e / VPP, q = e - px * VPP;
+      const int i = px / IT, j = px - i * IT, gy = y0 - P + i, gx = x0 - P + j;
+      const bool ok = e < NV && gy >= 0 && gy < H && gx >= 0 && gx < W;
+      const uint32_t pix = ok ? (uint32_t)(gy * W + gx) : 0u;
+      const uint4 a = *reinterpret_cast<const uint4*>(DY + (size_t)pix * C + (ok ? q * EPV : 0));
+      const uint4 b = *reinterpret_cast<const uint4*>(X + (size_t)pix * g.lz.ld + (ok ? q * EPV : 0));
+      rd[u] = ok ? a : make_uint4(0, 0, 0, 0);
+      rx[u] = b;
+      okm |= (uint32_t)ok << u;
+    }
+    __syncthreads();  // the previous tile's LDS reads are done (and the tables are in place)
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      const int e = tid + u * 256, px = e / VPP, q = e - px * VPP;
+      if (e >= NV) break;
+      const int i = px / IT, j = px - i * IT;
+      *reinterpret_cast<uint4*>(dys + i * DRS + j * DWT_CB + q * EPV) = rd[u];
+      const T* xe = reinterpret_cast<const T*>(&rx[u]);
+      const float m = ((okm >> u) & 1) ? 1.f : 0.f;  // zero padding of the transformed input
+      float vals[EPV];
+#pragma unroll
+      for (int jj = 0; jj < EPV; ++jj) {
+        const int cc = q * EPV + jj;
+        vals[jj] = lazy_apply(to_f<T>(xe[jj]), af[cc], act) * (gt[cc] * m);
+      }
+#pragma unroll
+      for (int jj = 0; jj < EPV; jj += 4)
+        *reinterpret_cast<float4*>(vs + i * VRS + j * DWT_CB + q * EPV + jj) =
+            make_float4(vals[jj], vals[jj + 1], vals[jj + 2], vals[jj + 3]);
+      if constexpr (FOLD) {
+        if (i >= P && i < P + DWT_T && j >= P && j < P + DWT_T)
+          *reinterpret_cast<uint4*>(xs + ((i - P) * DWT_T + (j - P)) * DWT_CB + q * EPV) = rx[u];
+      }
+    }
+    __syncthreads();
+    // ---- the patch: dx from the dy window, the filter gradient from the v window.  The window
+    // bases are made opaque per tile: otherwise every one of the ~(K+3)^2 LDS addresses is
+    // hoisted out of the tile loop into a register of its own (~60 VGPRs); from one base each
+    // read is an immediate offset
+    int dofs = a0 * DRS + b0 * DWT_CB + c, vofs = a0 * VRS + b0 * DWT_CB + c;
+    asm volatile("" : "+v"(dofs), "+v"(vofs));
+    const T* db = dys + dofs;
+    const float* vb = vs + vofs;
+    float dyi[4][4], dxa[4][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        dyi[e][f] = to_f<T>(db[(e + P) * DRS + (f + P) * DWT_CB]);
+        dxa[e][f] = 0.f;
+      }
+#pragma unroll
+    for (int r = 0; r < K + 3; ++r) {
+      float dyw[K + 3], vw[K + 3];
+#pragma unroll
+      for (int sc = 0; sc < K + 3; ++sc) {
+        dyw[sc] = to_f<T>(db[r * DRS + sc * DWT_CB]);
+        vw[sc] = vb[r * VRS + sc * DWT_CB];
+      }
+      // pin this row's window values here: left alone, the compiler gathers every row's v reads
+      // up front and runs the whole filter gradient as one packed block (the full v window live
+      // in registers: ~210-250 VGPRs at k5)
+#pragma unroll
+      for (int sc = 0; sc < K + 3; ++sc) asm volatile("" : "+v"(dyw[sc]), "+v"(vw[sc]));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kh = e + 2 * P - r;  // dx row a0+e takes dy window row r through tap row kh
+        if (kh >= 0 && kh < K) {
+#pragma unroll
+          for (int f = 0; f < 4; ++f)
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) dxa[e][f] += dyw[f + 2 * P - kw] * w[kh * K + kw];
+        }
+        const int kv = r - e;  // dW row kv takes v window row r against the dy of pixel row a0+e
+        if (kv >= 0 && kv < K) {
+#pragma unroll
+          for (int kw = 0; kw < K; ++kw) {
+            float a = 0.f;
+#pragma unroll
+            for (int f = 0; f < 4; ++f) a += dyi[e][f] * vw[f + kw];
+            dwa[kv * K + kw] += a;
+          }
+        }
+      }
+      // ... and this row's accumulations done here (the SLP vectorizer otherwise packs updates
+      // of neighbouring taps from different rows and emits them after the last row)
+#pragma unroll
+      for (int i = 0; i < KK; ++i) asm volatile("" : "+v"(dwa[i]));
+      __builtin_amdgcn_sched_barrier(0);  // one window row's values live at a time
+    }
+    __syncthreads();  // every dy / v read is done: dys takes the dx tile [16][16][16]
+    int sofs = (a0 * DWT_T + b0) * DWT_CB + c;  // (opaque per tile, as the window bases)
+    asm volatile("" : "+v"(sofs));
+    T* sb = dys + sofs;
+    const T* xb = xs + (FOLD ? sofs : 0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int po = (e * DWT_T + f) * DWT_CB;
+        const T sv = from_f<T>(dxa[e][f]);
+        sb[po] = sv;
+        if constexpr (FOLD) {  // BN-backward sums of x's BatchNorm from the stored dx
+          if (y0 + a0 + e < H && x0 + b0 + f < W) {
+            const float yv = to_f<T>(sv), xv = to_f<T>(xb[po]);
+            const float du = act ? yv * dswishf_(xv * ft.x + ft.y) : yv;
+            fs += du;
+            fq += du * ((xv - ft.z) * ft.w);
+          }
+          asm volatile("" : "+v"(fs), "+v"(fq));  // pixel by pixel (no batched transcendentals)
+        }
+      }
+    __syncthreads();
+    // ---- dx tile out as 16-byte vectors (accumulate: read-add-write)
+#pragma unroll
+    for (int u = 0; u < VPP; ++u) {
+      const int e = tid + u * 256, px = e / VPP, q = e - px * VPP;
+      const int gy = y0 + px / DWT_T, gx = x0 + px % DWT_T;
+      if (gy < H && gx < W) {
+        T* dst = DX + (size_t)(gy * W + gx) * C + q * EPV;
+        const uint4 v = *reinterpret_cast<const uint4*>(dys + px * DWT_CB + q * EPV);
+        if (g.accumulate) {
+          const T* ve = reinterpret_cast<const T*>(&v);
+          const uint4 o4 = *reinterpret_cast<const uint4*>(dst);
+          const T* oe = reinterpret_cast<const T*>(&o4);
+          T o[EPV];
+#pragma unroll
+          for (int jj = 0; jj < EPV; ++jj) o[jj] = from_f<T>(to_f<T>(ve[jj]) + to_f<T>(oe[jj]));
+          *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(o);
+        } else {
+          *reinterpret_cast<uint4*>(dst) = v;
+        }
+      }
+    }
+  }
+  // ---- block reductions: over the wave's 4 patch rows (lane bits 4-5), then the 4 waves in LDS
+  // in a fixed order; one fp32 atomic per (tap, channel), one fp64 atomic per fold sum and channel
+#pragma unroll
+  for (int i = 0; i < KK; ++i) {
+    float v = dwa[i];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    dwa[i] = v;
+  }
+  if constexpr (FOLD) {
+    fs += __shfl_xor(fs, 16, 64);
+    fs += __shfl_xor(fs, 32, 64);
+    fq += __shfl_xor(fq, 16, 64);
+    fq += __shfl_xor(fq, 32, 64);
+  }
+  __syncthreads();  // vs is free: [4 waves][KK + 2][16]
+  float* red = vs;
+  constexpr int NR = KK + (FOLD ? 2 : 0);
+  if (lane < 16) {
+#pragma unroll
+    for (int i = 0; i < KK; ++i) red[(wave * NR + i) * DWT_CB + c] = dwa[i];
+    if constexpr (FOLD) {
+      red[(wave * NR + KK) * DWT_CB + c] = fs;
+      red[(wave * NR + KK + 1) * DWT_CB + c] = fq;
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < NR * DWT_CB; e += 256) {
+    const int i = e / DWT_CB, cc = e - i * DWT_CB;
+    const float v = (red[(0 * NR + i) * DWT_CB + cc] + red[(1 * NR + i) * DWT_CB + cc]) +
+                    (red[(2 * NR + i) * DWT_CB + cc] + red[(3 * NR + i) * DWT_CB + cc]);
+    if (i < KK) atomicAdd(g.dw + (size_t)i * C + c0 + cc, v);
+    else if constexpr (FOLD) stat_add((i == KK ? fold.dbeta[seg] : fold.dgamma[seg]) + c0 + cc, (double)v);
+  }
+}
+
+template <typename T, int K, bool FOLD>
+static int launch_dwt(DwArgs g, const edet_bngrad64& fold, hipStream_t s) {
+  DwtPlan pl{};
+  pl.ncg = g.C / DWT_CB;
+  long tiles = 0;
+  for (int i = 0; i < g.pin.nseg; ++i) {
+    pl.ntx[i] = cdiv(g.pin.W[i], DWT_T);
+    pl.ntiles[i] = pl.ntx[i] * cdiv(g.pin.H[i], DWT_T);
+    tiles += (long)g.pin.batch * pl.ntiles[i] * pl.ncg;
+  }
+  // tiles per block: the most (<= 8) that still leaves >= 768 blocks -- fewer filter-gradient
+  // flushes and prologues per tile (tools/dwt_ab.py sweep r04e: 256^2 x 32 207 -> 178 us at 8,
+  // 32^2 x 480 k5 82 -> 77 at 4; the C = 64 32^2 level wants all 512 blocks).  Development slots
+  // 30 / 31: block floor / tiles per block
+  int tpb = 1;
+  const long floor_blocks = dev_knob(30) > 0 ? dev_knob(30) : 768;
+  while (tpb < 8 && tiles / (2 * tpb) >= floor_blocks) tpb *= 2;
+  if (dev_knob(31) > 0) tpb = dev_knob(31);
+  pl.tpb = tpb;
+  long total = 0;
+  for (int i = 0; i < g.pin.nseg; ++i) {
+    pl.chunks[i] = cdiv(pl.ntiles[i], tpb);
+    pl.nblk[i] = g.pin.batch * pl.chunks[i] * pl.ncg;
+    total += pl.nblk[i];
+  }
+  if (total == 0) return EDET_OK;
+  EDET_REQUIRE(total < (1L << 31), "dwconv_bwd: grid too large");
+  EDET_LAUNCH((k_dwt<T, K, FOLD>), dim3((unsigned)total), dim3(256), 0, s, g, pl, fold);
+  return check_launch("edet dwconv bwd (tiles)");
 }
 
 template <typename T, int K, int CPG, bool FOLD>
@@ -2110,6 +2391,8 @@ static int launch_dwb(DwArgs g, const edet_bngrad64& fold, hipStream_t s) {
 
 template <typename T, int K, bool FOLD>
 static int dispatch_dwb_cpg(const DwArgs& g, const edet_bngrad64& fold, hipStream_t s) {
+  // development slot 29 = 1: the tiled form (k_dwt) wherever it applies
+  if (dev_knob(29) == 1 && g.C % DWT_CB == 0 && g.lz.ld % 8 == 0) return launch_dwt<T, K, FOLD>(g, fold, s);
   int wmax = 0;
   for (int i = 0; i < g.pin.nseg; ++i) wmax = std::max(wmax, g.pin.W[i]);
   const int force = dev_knob(20);  // development: columns per thread (1, 2, 4)
