@@ -2197,11 +2197,6 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
         dyw[sc] = to_f<T>(db[r * DRS + sc * DWT_CB]);
         vw[sc] = vb[r * VRS + sc * DWT_CB];
       }
-      // pin this row's window values here: left alone, the compiler gathers every row's v reads
-      // up front and runs the whole filter gradient as one packed block (the full v window live
-      // in registers: ~210-250 VGPRs at k5)
-#pragma unroll
-      for (int sc = 0; sc < K + 3; ++sc) asm volatile("" : "+v"(dyw[sc]), "+v"(vw[sc]));
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int kh = e + 2 * P - r;  // dx row a0+e takes dy window row r through tap row kh
@@ -2222,11 +2217,11 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
           }
         }
       }
-      // ... and this row's accumulations done here (the SLP vectorizer otherwise packs updates
-      // of neighbouring taps from different rows and emits them after the last row)
-#pragma unroll
-      for (int i = 0; i < KK; ++i) asm volatile("" : "+v"(dwa[i]));
-      __builtin_amdgcn_sched_barrier(0);  // one window row's values live at a time
+      // (no per-row pinning of the window or the taps: the SLP vectorizer then gathers the whole
+      // filter gradient into v_pk_fma_f32 after the last row -- the full v window in registers,
+      // ~210-250 VGPRs at k5, but half the FMA instructions; pinned rows with scalar FMAs held
+      // 140 VGPRs and ran 5-10 % slower at k5, even at k3: tools/dwt_ab.py r04e-r04g)
+      __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();  // every dy / v read is done: dys takes the dx tile [16][16][16]
     int sofs = (a0 * DWT_T + b0) * DWT_CB + c;  // (opaque per tile, as the window bases)
