@@ -2386,8 +2386,13 @@ static int launch_dwb(DwArgs g, const edet_bngrad64& fold, hipStream_t s) {
 
 template <typename T, int K, bool FOLD>
 static int dispatch_dwb_cpg(const DwArgs& g, const edet_bngrad64& fold, hipStream_t s) {
-  // development slot 29 = 1: the tiled form (k_dwt) wherever it applies
-  if (dev_knob(29) == 1 && g.C % DWT_CB == 0 && g.lz.ld % 8 == 0) return launch_dwt<T, K, FOLD>(g, fold, s);
+  // the tiled form (k_dwt) for bf16 storage wherever it applies: 1068 -> 944 us over the D0 b32
+  // shapes, no shape slower (tools/dwt_ab.py, r04h; 32^2 x 480 k5 even); fp32 (parity runs)
+  // keeps the row-streaming kernels (tiles at 1-2 blocks per CU: 1185 vs 1205 us).
+  // Development slot 29: 1 forces the tiled form, 2 the row-streaming kernels
+  const int form = dev_knob(29);
+  if (form != 2 && g.C % DWT_CB == 0 && g.lz.ld % 8 == 0 && (form == 1 || sizeof(T) == 2))
+    return launch_dwt<T, K, FOLD>(g, fold, s);
   int wmax = 0;
   for (int i = 0; i < g.pin.nseg; ++i) wmax = std::max(wmax, g.pin.W[i]);
   const int force = dev_knob(20);  // development: columns per thread (1, 2, 4)

@@ -1,6 +1,6 @@
 """A/B of the fused stride-1 depthwise backward forms over the D0 b32 shapes (development;
-EDET_DEV library): the production route (edet_dev_set slot 29 = 0) against the tiled form
-k_dwt (slot 29 = 1; slots 30 / 31 = block target / tiles per block).  Per shape: us per launch of
+EDET_DEV library): the row-streaming kernels (edet_dev_set slot 29 = 2) against the tiled form
+k_dwt (slot 29 = 1; slots 30 / 31 = block floor / tiles per block).  Per shape: us per launch of
 each, and the tiled form's dx / filter gradient / fold sums against the production route's
 (fp32 summation order only: relative differences ~1e-6 in fp32, a few bf16 ulp in bf16).
 
@@ -57,7 +57,7 @@ def main():
         w = (torch.randn(k * k, C, device="cuda") * 0.3).to(tdt)
         dy = torch.randn(pin.rows, C, device="cuda").to(tdt)
         outs, us = [], []
-        for form in (0, 1):
+        for form in (2, 1):
             dev(29, form)
             for a, b in extra:
                 dev(a, b)
