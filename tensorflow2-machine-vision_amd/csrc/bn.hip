@@ -469,33 +469,35 @@ __global__ __launch_bounds__(256) void k_se_bn_combine(int B, int C, const float
 // chip: one wave per (n, r) dot product over C, then one thread per (n, c) over R.  Every
 // output (including the weight gradients) has exactly one writer: no atomics, reproducible.
 
-// z1[n][r] = sum_c w1[r][c] s[n][c] + b1[r]     (one wave per (n, r))
-__global__ __launch_bounds__(256) void k_se_reduce_c(int B, int C, int R, const double* s, const float* w1,
-                                                     const float* b1, float* z1) {
-  const int lane = threadIdx.x & 63;
-  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (item >= B * R) return;
-  const int n = item / R, r = item - n * R;
-  float a = 0.f;
+// SE excite, both FCs of one image in one block (edet_se_fwd, layers/se.py:37-39):
+//   z1[n][r] = sum_c w1[r][c] s[n][c] + b1[r]            (one wave per r, lane-strided + wave tree)
+//   gate[n][c] = sigmoid(sum_r w2[c][r] swish(z1[n][r]) + b2[c])   (one thread per c)
+// swish(z1) is parked in LDS between them: one launch per SE block (two kernels and a z1 round
+// trip before round 4: config 2's SE step took ~16 us)
+__global__ __launch_bounds__(256) void k_se_fwd1(int B, int C, int R, const double* s, const float* w1,
+                                                 const float* b1, const float* w2, const float* b2, float* z1,
+                                                 float* gate) {
+  extern __shared__ float zs[];  // [R] swish(z1)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n = blockIdx.x;
+  const double* sn = s + (size_t)n * C;
+  for (int r = wave; r < R; r += 4) {
+    float a = 0.f;
 #pragma unroll 4
-  for (int c = lane; c < C; c += 64) a += w1[(size_t)r * C + c] * (float)s[(size_t)n * C + c];
-  a = wave_sum(a);
-  if (lane == 0) z1[item] = a + b1[r];
-}
-
-// gate[n][c] = sigmoid(sum_r w2[c][r] swish(z1[n][r]) + b2[c])   (one thread per (n, c))
-__global__ __launch_bounds__(256) void k_se_excite(int B, int C, int R, const float* z1, const float* w2,
-                                                   const float* b2, float* gate) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= B * C) return;
-  const int n = idx / C, c = idx - n * C;
-  float a = b2[c];
-#pragma unroll 8
-  for (int r = 0; r < R; ++r) {
-    const float z = z1[(size_t)n * R + r];
-    a += w2[(size_t)c * R + r] * (z * sigmoidf_(z));
+    for (int c = lane; c < C; c += 64) a += w1[(size_t)r * C + c] * (float)sn[c];
+    a = wave_sum(a);
+    if (lane == 0) {
+      const float z = a + b1[r];
+      z1[(size_t)n * R + r] = z;
+      zs[r] = z * sigmoidf_(z);
+    }
   }
-  gate[idx] = sigmoidf_(a);
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float a = b2[c];
+#pragma unroll 8
+    for (int r = 0; r < R; ++r) a += w2[(size_t)c * R + r] * zs[r];
+    gate[(size_t)n * C + c] = sigmoidf_(a);
+  }
 }
 
 // backward, pass 1: dz1[n][r] = swish'(z1) * sum_c dz2[n][c] w2[c][r],
@@ -910,8 +912,7 @@ int edet_se_fwd(int B, int C, int R, const double* s, const float* w1, const flo
   EDET_REQUIRE(s && w1 && b1 && w2 && b2 && z1 && gate && B > 0 && C > 0 && R > 0,
                "se_fwd: bad argument");
   hipStream_t st = (hipStream_t)stream;
-  EDET_LAUNCH(k_se_reduce_c, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, s, w1, b1, z1);
-  EDET_LAUNCH(k_se_excite, dim3(cdiv(B * C, 256)), dim3(256), 0, st, B, C, R, z1, w2, b2, gate);
+  EDET_LAUNCH(k_se_fwd1, dim3(B), dim3(256), (size_t)R * sizeof(float), st, B, C, R, s, w1, b1, w2, b2, z1, gate);
   return check_launch("edet se_fwd");
 }
 
