@@ -268,10 +268,11 @@ class EfficientDetNet:
         d = ops.dwconv(eng, P, x, f"{pre}/depthwise_conv2d/depthwise_kernel", sp.kernel_size, sp.stride,
                        bns=[b["bn1"]], act=L.ACT_SWISH, name=f"{pre}/dw", squeeze=svec)
         ops.squeeze_excite(eng, P, d, f"{pre}/se", sp.se_filters, svec=svec)
-        # training: the gated value is written once, since the project conv's forward GEMM and its
-        # weight gradient both read it; inference: the GEMM applies BN + swish + gate while staging
-        # its A tile (once per element: the tile spans all output columns) -- no extra pass
-        if self.materialize_se and eng.training:
+        # the gated value is written once: the project conv's forward GEMM (and in training its
+        # weight gradient) read it plain.  Also in inference, where BN + swish + gate could ride in
+        # the GEMM's A staging: that lengthened the GEMMs' latency-bound K loops more than the
+        # pass costs (config 2: 40.5k -> 31.2k images/s, r04k)
+        if self.materialize_se:
             d = ops.materialize(eng, d, name=f"{pre}/se_out")
         return ops.conv1x1(eng, P, d, b["project_w"], sp.output_filters, bns=[b["bn2"]], name=f"{pre}/project")
 
