@@ -167,12 +167,16 @@ def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optio
 # input's BatchNorm when this op is the input's only consumer
 FUSED_DW_BWD = os.environ.get("EDET_FUSED_DW", "1") != "0"
 FOLD_DW_BN = os.environ.get("EDET_FOLD_DW_BN", "1") != "0"
-# the 1x1 dgrad takes the BN-backward sums of its output's value in its epilogue
-# (edet_conv1x1_dgrad_fold) when it owns that value's whole gradient
-FOLD_GEMM_BN = os.environ.get("EDET_FOLD_GEMM_BN", "1") != "0"
+# the 1x1 dgrad can take the BN-backward sums of its output's value in its epilogue
+# (edet_conv1x1_dgrad_fold) when it owns that value's whole gradient.  Off by default: the whole
+# D0 step measured no gain (13.777 vs 13.758 ms, three alternating runs each, r04j) -- the reduce
+# pass it saves runs at ~5.8 TB/s, and the GEMMs it extends are latency-bound
+FOLD_GEMM_BN = os.environ.get("EDET_FOLD_GEMM_BN", "0") != "0"
+# the stride-2 depthwise dgrad with the same fold (edet_dwconv_dgrad_fold)
+FOLD_DWS2_BN = os.environ.get("EDET_FOLD_DWS2_BN", "1") != "0"
 # every switch that takes a BN-backward reduce into the kernel producing the gradient (the test
 # of the folds flips them all: tests/test_model_gpu.py::test_bn_backward_folds_equal_unfused_path)
-FOLD_SWITCHES = ("FUSED_DW_BWD", "FOLD_DW_BN", "FOLD_GEMM_BN")
+FOLD_SWITCHES = ("FUSED_DW_BWD", "FOLD_DW_BN", "FOLD_GEMM_BN", "FOLD_DWS2_BN")
 
 
 def _fold_dst(eng: Engine, x: Act, acc: int):
@@ -226,7 +230,7 @@ def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
                    stream())
         s = stream()
         dx, acc = eng.tape.dst(x)
-        fold = _fold_dst(eng, x, acc) if FOLD_DW_BN else None
+        fold = _fold_dst(eng, x, acc) if FOLD_DWS2_BN else None
         if fold is not None:
             L.call("edet_dwconv_dgrad_fold", eng.dt, vp(d), pout.c, C, k, stride, vp(P.wcv(wname)), vp(dx), x.pyr.c,
                    x.lazy(), fold, s)
