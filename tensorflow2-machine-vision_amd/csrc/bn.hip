@@ -469,49 +469,33 @@ __global__ __launch_bounds__(256) void k_se_bn_combine(int B, int C, const float
 // chip: one wave per (n, r) dot product over C, then one thread per (n, c) over R.  Every
 // output (including the weight gradients) has exactly one writer: no atomics, reproducible.
 
-// SE excite, both FCs of one image in one block (edet_se_fwd, layers/se.py:37-39):
-//   z1[n][r] = sum_c w1[r][c] s[n][c] + b1[r]
-//   gate[n][c] = sigmoid(sum_r w2[c][r] swish(z1[n][r]) + b2[c])
-// Each thread takes channels c = t, t + 256, ... and accumulates all R <= RT partial sums of
-// the first FC at once (coalesced rows of w1, every load independent), the block folds them with
-// wave trees and one LDS pass in a fixed order; swish(z1) is parked in LDS and the gates follow
-// one thread per channel.  One launch per SE block (two kernels before round 4, one wave per
-// (image, r) dot product: config 2's SE step ~16 us).
-template <int RT>
-__global__ __launch_bounds__(256) void k_se_fwd1(int B, int C, int R, const double* s, const float* w1,
-                                                 const float* b1, const float* w2, const float* b2, float* z1,
-                                                 float* gate) {
-  __shared__ float part[4][RT];
-  __shared__ float zs[RT];  // swish(z1)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n = blockIdx.x;
-  const double* sn = s + (size_t)n * C;
-  float a[RT];
-#pragma unroll
-  for (int r = 0; r < RT; ++r) a[r] = 0.f;
-  for (int c = threadIdx.x; c < C; c += 256) {
-    const float sv = (float)sn[c];
-#pragma unroll
-    for (int r = 0; r < RT; ++r) a[r] += w1[(size_t)(r < R ? r : 0) * C + c] * (r < R ? sv : 0.f);
-  }
-#pragma unroll
-  for (int r = 0; r < RT; ++r) {
-    const float v = wave_sum(a[r]);
-    if (lane == 0) part[wave][r] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < R) {
-    const int r = threadIdx.x;
-    const float z = ((part[0][r] + part[1][r]) + (part[2][r] + part[3][r])) + b1[r];
-    z1[(size_t)n * R + r] = z;
-    zs[r] = z * sigmoidf_(z);
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float g = b2[c];
+// z1[n][r] = sum_c w1[r][c] s[n][c] + b1[r]     (one wave per (n, r))
+__global__ __launch_bounds__(256) void k_se_reduce_c(int B, int C, int R, const double* s, const float* w1,
+                                                     const float* b1, float* z1) {
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= B * R) return;
+  const int n = item / R, r = item - n * R;
+  float a = 0.f;
+#pragma unroll 4
+  for (int c = lane; c < C; c += 64) a += w1[(size_t)r * C + c] * (float)s[(size_t)n * C + c];
+  a = wave_sum(a);
+  if (lane == 0) z1[item] = a + b1[r];
+}
+
+// gate[n][c] = sigmoid(sum_r w2[c][r] swish(z1[n][r]) + b2[c])   (one thread per (n, c))
+__global__ __launch_bounds__(256) void k_se_excite(int B, int C, int R, const float* z1, const float* w2,
+                                                   const float* b2, float* gate) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * C) return;
+  const int n = idx / C, c = idx - n * C;
+  float a = b2[c];
 #pragma unroll 8
-    for (int r = 0; r < R; ++r) g += w2[(size_t)c * R + r] * zs[r];
-    gate[(size_t)n * C + c] = sigmoidf_(g);
+  for (int r = 0; r < R; ++r) {
+    const float z = z1[(size_t)n * R + r];
+    a += w2[(size_t)c * R + r] * (z * sigmoidf_(z));
   }
+  gate[idx] = sigmoidf_(a);
 }
 
 // backward, pass 1: dz1[n][r] = swish'(z1) * sum_c dz2[n][c] w2[c][r],
@@ -926,13 +910,8 @@ int edet_se_fwd(int B, int C, int R, const double* s, const float* w1, const flo
   EDET_REQUIRE(s && w1 && b1 && w2 && b2 && z1 && gate && B > 0 && C > 0 && R > 0,
                "se_fwd: bad argument");
   hipStream_t st = (hipStream_t)stream;
-  EDET_REQUIRE(R <= 128, "se_fwd: R=%d above 128", R);
-  if (R <= 8) EDET_LAUNCH(k_se_fwd1<8>, dim3(B), dim3(256), 0, st, B, C, R, s, w1, b1, w2, b2, z1, gate);
-  else if (R <= 16) EDET_LAUNCH(k_se_fwd1<16>, dim3(B), dim3(256), 0, st, B, C, R, s, w1, b1, w2, b2, z1, gate);
-  else if (R <= 32) EDET_LAUNCH(k_se_fwd1<32>, dim3(B), dim3(256), 0, st, B, C, R, s, w1, b1, w2, b2, z1, gate);
-  else if (R <= 48) EDET_LAUNCH(k_se_fwd1<48>, dim3(B), dim3(256), 0, st, B, C, R, s, w1, b1, w2, b2, z1, gate);
-  else if (R <= 64) EDET_LAUNCH(k_se_fwd1<64>, dim3(B), dim3(256), 0, st, B, C, R, s, w1, b1, w2, b2, z1, gate);
-  else EDET_LAUNCH(k_se_fwd1<128>, dim3(B), dim3(256), 0, st, B, C, R, s, w1, b1, w2, b2, z1, gate);
+  EDET_LAUNCH(k_se_reduce_c, dim3(cdiv(B * R, 4)), dim3(256), 0, st, B, C, R, s, w1, b1, z1);
+  EDET_LAUNCH(k_se_excite, dim3(cdiv(B * C, 256)), dim3(256), 0, st, B, C, R, z1, w2, b2, gate);
   return check_launch("edet se_fwd");
 }
 
