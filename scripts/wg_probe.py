@@ -1,8 +1,9 @@
-"""Isolated check + timing of edet_conv1x1_wgrad (plain bf16 A) at the D0 step's shapes.
+"""Isolated check + timing of edet_conv1x1_wgrad (bf16 A) at the D0 step's shapes.
 
-    python scripts/wg_probe.py [mode ...]      modes via edet_dev_set(0, mode) where present
-Prints per shape: relative error vs a torch fp32 reference, us per launch, achieved GB/s
-(algorithmic bytes = M (K + N) * 2)."""
+    python scripts/wg_probe.py [--slot S] [--lazy] [mode ...]   modes via edet_dev_set(S, mode) (S = 0)
+Prints per shape: relative error vs a torch fp32 reference (--lazy: A = swish(bn(x)) applied on
+load, errors against the first mode's result), us per launch, achieved GB/s (algorithmic bytes =
+M (K + N) * 2)."""
 import ctypes
 import os
 import sys
@@ -14,6 +15,8 @@ import torch  # noqa: E402
 
 from tf2mv_amd import _lib as L  # noqa: E402
 from tf2mv_amd.runtime import Pyr, ensure_workspace, stream, vp  # noqa: E402
+
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 D0_LEVELS = [(64, 64), (32, 32), (16, 16), (8, 8), (4, 4)]
 SHAPES = [  # (rows layout, K, N, lddy)
@@ -40,7 +43,16 @@ def timeit(fn, reps=20):
 
 
 def main():
-    modes = [int(m) for m in sys.argv[1:]] or [0]
+    args = sys.argv[1:]
+    slot, lazy = 0, "--lazy" in args
+    if "--slot" in args:
+        slot = int(args[args.index("--slot") + 1])
+        del args[args.index("--slot"):args.index("--slot") + 2]
+    modes = [int(m) for m in args if m != "--lazy"] or [0]
+    if lazy:
+        import numpy as np
+        from gpu_util import LazyDesc, make_bn
+        rng = np.random.default_rng(0)
     lib = L.lib()
     dev = getattr(lib.dll, "edet_dev_set", None)
     ensure_workspace(torch.device("cuda"))
@@ -57,20 +69,27 @@ def main():
             valid[pyr.seg_slice(sgi)] = True
         ref_w = (dy[valid, :N].float().t() @ a[valid].float()).double()
         ref_b = dy[valid, :N].float().sum(0).double()
-        lz = L.Lazy()
-        lz.x, lz.gate, lz.ld, lz.act = a.data_ptr(), None, K, 0
+        if lazy:
+            ld = LazyDesc(a, pyr, K, bn=make_bn(a, pyr, K, rng), act=1)
+            lzp = ld.c
+        else:
+            lz = L.Lazy()
+            lz.x, lz.gate, lz.ld, lz.act = a.data_ptr(), None, K, 0
+            lzp = ctypes.byref(lz)
         algo = sum(pyr.seg_rows(i) for i in range(pyr.nseg)) * (K + N) * 2
         line = f"M={M:8d} K={K:5d} N={N:5d}"
         for m in modes:
             if dev is not None:
-                dev(0, m)
+                dev(slot, m)
             dw = torch.zeros(N, K, device="cuda")
             db = torch.zeros(N, device="cuda")
-            L.call("edet_conv1x1_wgrad", L.BF16, ctypes.byref(lz), pyr.c, K, vp(dy), lddy, N, vp(dw), vp(db), stream())
+            L.call("edet_conv1x1_wgrad", L.BF16, lzp, pyr.c, K, vp(dy), lddy, N, vp(dw), vp(db), stream())
             torch.cuda.synchronize()
+            if lazy and m == modes[0]:
+                ref_w, ref_b = dw.double().clone(), db.double().clone()
             ew = float((dw.double() - ref_w).norm() / ref_w.norm())
             eb = float((db.double() - ref_b).norm() / ref_b.norm())
-            us = timeit(lambda: L.call("edet_conv1x1_wgrad", L.BF16, ctypes.byref(lz), pyr.c, K, vp(dy), lddy, N,
+            us = timeit(lambda: L.call("edet_conv1x1_wgrad", L.BF16, lzp, pyr.c, K, vp(dy), lddy, N,
                                        vp(dw), vp(db), stream()))
             tot[m] += us
             flag = "" if ew < 1e-4 and eb < 1e-4 else "  <<< WRONG"
@@ -78,7 +97,7 @@ def main():
         print(line, flush=True)
     print("total " + " ".join(f"m{m}={t:.1f}us" for m, t in tot.items()))
     if dev is not None:
-        dev(0, 0)
+        dev(slot, 0)
 
 
 if __name__ == "__main__":

@@ -184,6 +184,42 @@ __host__ __device__ __forceinline__ int seg_of_row(const edet_pyramid& p, int ro
     if (row >= p.row_off[i]) s = i;
   return s;
 }
+// Range-checked 16-byte loads (buffer_load_dwordx4 through a descriptor over [base, base +
+// bytes)): an offset at or past the range reads zeros.  A pipelined loop fetches its operand
+// tiles with these -- the bounds are in the offset, the load itself is unconditional and its
+// result needs no select -- so the compiler's wait before a commit counts just that stage's
+// loads (loads under branches, or selected after, left it waiting for every stage in flight).
+// The descriptor must come from wave-uniform values; callers pass kernel-argument pointers
+// advanced by block-uniform amounts.
+constexpr uint32_t BUF_OOB = 0x80000000u;
+// a load the compiler knows is global (a pointer it cannot place becomes a flat load, which the
+// wait-count pass orders against LDS and every load in flight)
+__device__ __forceinline__ float gld(const float* p) {
+  return *(const __attribute__((address_space(1))) float*)p;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, long bytes) {
+  const uint32_t n = bytes <= 0 ? 0u : (bytes >= (long)BUF_OOB ? BUF_OOB : (uint32_t)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, 0x00020000);
+}
+__device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// seg_of_row for a per-lane row, plus the end of that segment's valid rows: compile-time
+// segment indices only, so the pyramid stays in scalar registers (a per-lane index into the
+// kernel-argument struct becomes per-lane vector loads, each waited for at once -- with the
+// in-order vmcnt counter, behind every load already in flight)
+__device__ __forceinline__ int seg_of_row_end(const edet_pyramid& p, int row, int& end) {
+  int s = 0, e = p.row_off[0] + seg_rows(p, 0);
+#pragma unroll
+  for (int i = 1; i < EDET_MAX_SEG; ++i) {
+    const bool in = i < p.nseg && row >= p.row_off[i];
+    s = in ? i : s;
+    e = in ? p.row_off[i] + seg_rows(p, i) : e;
+  }
+  end = e;
+  return s;
+}
 __host__ __device__ __forceinline__ int pyr_valid_rows(const edet_pyramid& p) {
   int n = 0;
   for (int i = 0; i < p.nseg; ++i) n += seg_rows(p, i);

@@ -118,6 +118,11 @@ __device__ __forceinline__ bf16x8_t lds_frag_bf16(const uint16_t* p) {
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// images a BM-row tile of one segment can span (the staged SE gate rows of k_gemm)
+__host__ __device__ __forceinline__ int gemm_gate_imgs(int BM, int hw, int batch) {
+  return min(batch, (BM - 1) / hw + 2);
+}
+
 // K-streaming GEMM for K > 512 (the MBConv project convs, K = 480 ... 1152, N <= 320): one
 // block owns a BM x BN tile with the whole N, and walks K in 32-wide chunks.  Software
 // pipelined: chunk k+1 is fetched global -> registers while chunk k's MFMAs run, LDS is
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   T* Xs = Cs + BM * LDC_S;         // FOLD
   __shared__ float4 ftab[FOLD ? BN : 1];
   __shared__ float red[2][2][BN];  // [sum|sq][wm][col]: one writer each, summed in fixed order
-  extern __shared__ float2 xf[];   // [K] lazy affine per input channel, then [2][K] gate rows
+  extern __shared__ float2 xf[];   // [K] lazy affine per input channel, then [images][K] gate rows
   float* gts = reinterpret_cast<float*>(xf + (LAZY ? g.K : 0));
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -162,18 +167,20 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
       ftab[c] = col0 + c < g.N ? fold_table(g.fx.bn, seg, col0 + c, inv) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 
-  // SE gate rows of the (at most two, hw >= BM) images this tile spans, staged in LDS once:
-  // the per-element global gate loads sat on the chunk loop's critical path
-  const bool gate_lds = LAZY && g.lz.gate != nullptr && hw >= BM;
+  // SE gate rows of the images this tile spans (gemm_gate_imgs of them), staged in LDS once:
+  // per-element global gate loads sat on the chunk loop's critical path
+  const bool has_gate = LAZY && g.lz.gate != nullptr;
   const int n_lo = (row0 - seg_off) / hw;
   if constexpr (LAZY) {
     const float inv = 1.f / (float)seg_rows(g.pyr, seg);
     for (int k = tid; k < g.K; k += 256) xf[k] = bn_affine(g.lz.bn, seg, k, inv);
-    if (gate_lds)
-      for (int k = tid; k < 2 * g.K; k += 256) {
-        const int n = n_lo + (k >= g.K);
-        gts[k] = (n < g.pyr.batch) ? g.lz.gate[(size_t)n * g.K + (k >= g.K ? k - g.K : k)] : 0.f;
+    if (has_gate) {
+      const int ni = gemm_gate_imgs(BM, hw, g.pyr.batch);
+      for (int e = tid; e < ni * g.K; e += 256) {
+        const int i = e / g.K, k = e - i * g.K, n = n_lo + i;
+        gts[e] = (n < g.pyr.batch) ? g.lz.gate[(size_t)n * g.K + k] : 0.f;
       }
+    }
   }
   __syncthreads();
 
@@ -199,68 +206,81 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   struct Chunk {
     V ra[AV][VW], rb[BV][VW];
   };
-  // per-thread A rows are fixed across chunks: resolve their gate rows once
-  const float* gpu_[AV];
+  // per-thread A rows are fixed across chunks: resolve their staged gate rows once
+  int goff[AV];
 #pragma unroll
   for (int u = 0; u < AV; ++u) {
-    const int grow = row0 + (tid + u * 256) / KV;
-    gpu_[u] = nullptr;
-    if (LAZY && g.lz.gate && grow < g.M) {
-      const int img = (grow - seg_off) / hw;
-      gpu_[u] = gate_lds ? gts + (img - n_lo) * g.K : g.lz.gate + (size_t)img * g.K;
-    }
+    const int grow = min(row0 + (tid + u * 256) / KV, g.M - 1);
+    goff[u] = has_gate ? ((grow - seg_off) / hw - n_lo) * g.K : 0;
   }
-  // global -> registers (raw); invalid lanes hold zeros
+  // global -> registers (raw), branch-free: an element outside the operand reads zeros
+  // (buf_ld16).  Loads under branches left the compiler's wait-count merge pessimistic: every
+  // commit waited for the chunks in flight behind it (s_waitcnt vmcnt(0)).
+  // (range-checked loads over the block's A rows / B rows: rows past M or N read zeros, a
+  // chunk column past K takes an out-of-range offset)
+  const auto ra_ = buf_rsrc(A + (size_t)row0 * g.lda, (long)min(BM, g.M - row0) * g.lda * (long)sizeof(T));
+  const auto rb_ = buf_rsrc(B + (size_t)col0 * g.ldb, (long)min(BN, g.N - col0) * g.ldb * (long)sizeof(T));
   auto fetch = [&](Chunk& R, int k0) {
 #pragma unroll
     for (int u = 0; u < AV; ++u) {
       const int v = tid + u * 256;
-      const int r = v / KV, kv = (v % KV) * 8, grow = row0 + r, gk = k0 + kv;
+      const int r = v / KV, kv = (v % KV) * 8;
+      const uint32_t off = (v < BM * KV && k0 + kv < g.K) ? (uint32_t)((r * g.lda + k0 + kv) * (int)sizeof(T)) : BUF_OOB;
 #pragma unroll
-      for (int w = 0; w < VW; ++w) R.ra[u][w] = V{};
-      if (v < BM * KV && grow < g.M && gk < g.K) {
-        const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + gk);
-#pragma unroll
-        for (int w = 0; w < VW; ++w) R.ra[u][w] = src[w];
-      }
+      for (int w = 0; w < VW; ++w) R.ra[u][w] = __builtin_bit_cast(V, buf_ld16(ra_, off + 16 * w));
     }
 #pragma unroll
     for (int u = 0; u < BV; ++u) {
       const int v = tid + u * 256;
-      const int n = v / KV, kv = (v % KV) * 8, gn = col0 + n, gk = k0 + kv;
+      const int n = v / KV, kv = (v % KV) * 8;
+      const uint32_t off = (v < BN * KV && k0 + kv < g.K) ? (uint32_t)((n * g.ldb + k0 + kv) * (int)sizeof(T)) : BUF_OOB;
 #pragma unroll
-      for (int w = 0; w < VW; ++w) R.rb[u][w] = V{};
-      if (v < BN * KV && gn < g.N && gk < g.K) {
-        const V* src = reinterpret_cast<const V*>(B + (size_t)gn * g.ldb + gk);
+      for (int w = 0; w < VW; ++w) R.rb[u][w] = __builtin_bit_cast(V, buf_ld16(rb_, off + 16 * w));
+    }
+  };
+  // registers -> LDS buffer, lazy transform of A on the way: branch-free per element (the
+  // activation and the gate are block-uniform choices, taken once around the whole chunk)
+  auto lazy_a = [&](auto act_c, auto gate_c, const Chunk& R, int buf, int k0) {
+    constexpr bool ACT = decltype(act_c)::value, GATE = decltype(gate_c)::value;
 #pragma unroll
-        for (int w = 0; w < VW; ++w) R.rb[u][w] = src[w];
+    for (int u = 0; u < AV; ++u) {
+      const int v = tid + u * 256;
+      if (v < BM * KV) {
+        const int r = v / KV, kv = (v % KV) * 8, gk = k0 + kv;
+        const bool rok = row0 + r < g.M;
+        const T* e = reinterpret_cast<const T*>(&R.ra[u][0]);
+        float vals[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = min(gk + j, g.K - 1);
+          float x = to_f<T>(e[j]) * xf[k].x + xf[k].y;
+          if constexpr (ACT) x = swishf_(x);
+          if constexpr (GATE) x *= gts[goff[u] + k];
+          vals[j] = (rok && gk + j < g.K) ? x : 0.f;
+        }
+        st8(&As[buf][r * LDK + kv], vals);
       }
     }
   };
-  // registers -> LDS buffer, lazy transform of A on the way
   auto commit = [&](const Chunk& R, int buf, int k0) {
+    if constexpr (LAZY) {
+      using TT = std::true_type;
+      using FF = std::false_type;
+      if (g.lz.act) {
+        if (has_gate) lazy_a(TT{}, TT{}, R, buf, k0);
+        else lazy_a(TT{}, FF{}, R, buf, k0);
+      } else {
+        if (has_gate) lazy_a(FF{}, TT{}, R, buf, k0);
+        else lazy_a(FF{}, FF{}, R, buf, k0);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < AV; ++u) {
       const int v = tid + u * 256;
       if (v < BM * KV) {
         const int r = v / KV, kv = (v % KV) * 8;
         T* dst = &As[buf][r * LDK + kv];
-        if constexpr (LAZY) {
-          const int grow = row0 + r, gk = k0 + kv;
-          const T* e = reinterpret_cast<const T*>(&R.ra[u][0]);
-          float vals[8];
-          const float* gp = gpu_[u];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float x = 0.f;
-            if (grow < g.M && gk + j < g.K) {
-              x = lazy_apply(to_f<T>(e[j]), xf[gk + j], g.lz.act);
-              if (gp) x *= gp[gk + j];
-            }
-            vals[j] = x;
-          }
-          st8(dst, vals);
-        } else {
+        if constexpr (!LAZY) {
 #pragma unroll
           for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(dst)[w] = R.ra[u][w];
         }
@@ -289,8 +309,8 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   Chunk R0, R1;
   fetch(R0, 0);
   commit(R0, 0, 0);
-  if (1 < nk) fetch(R0, KC);
-  if (2 < nk) fetch(R1, 2 * KC);
+  fetch(R0, KC);  // (past K: every element is outside, committed as zeros or not at all)
+  fetch(R1, 2 * KC);
   __syncthreads();
   auto kstep = [&](Chunk& R, int kt) {
     const int buf = kt & 1;
@@ -327,8 +347,8 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         }
       }
     }
-    if (kt + 1 < nk) commit(R, buf ^ 1, (kt + 1) * KC);
-    if (kt + 3 < nk) fetch(R, (kt + 3) * KC);
+    commit(R, buf ^ 1, (kt + 1) * KC);
+    fetch(R, (kt + 3) * KC);
     __syncthreads();
   };
   for (int kt = 0; kt < nk; kt += 2) {
@@ -888,12 +908,18 @@ __device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* img, int ldm, int r0
   return __builtin_bit_cast(bf16x8_t, c);
 }
 
-constexpr int WT_BM = 64, WT_LDM = 64 + 8;
+constexpr int WT_BM = 64, WT_LDM = 64 + 8;  // WT_BM: the unit the row splits are sized in
 
-template <bool LAZY>
+// BM rows per stage (one barrier each), PF stages in flight in registers ahead of the one being
+// committed.  A block's stage chain is latency-bound on the mid-M shapes (~1.2 us per 64-row
+// stage at 2 in flight, whatever the tile count: profiles/r03ab_wgrad_plan_sweep.txt), so more
+// bytes in flight per block shorten it without adding splits (= fp32 atomic bytes).
+template <bool LAZY, int BM = 64, int PF = 2>
 __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
-  __shared__ __attribute__((aligned(16))) uint16_t Ds[2][WT_BM * WT_LDM];
-  __shared__ __attribute__((aligned(16))) uint16_t Xs[2][WT_BM * WT_LDM];
+  static_assert(BM % 64 == 0 && PF >= 1, "stage rows: multiple of 64");
+  constexpr int HR = BM / 32;  // rows per thread per stage (32 rows per pass of the 256 threads)
+  __shared__ __attribute__((aligned(16))) uint16_t Ds[2][BM * WT_LDM];
+  __shared__ __attribute__((aligned(16))) uint16_t Xs[2][BM * WT_LDM];
   __shared__ float2 xf[EDET_MAX_SEG][64];
   __shared__ float dbred[4][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -914,64 +940,58 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
       xf[sg][e & 63] = (k < g.K) ? bn_affine(g.lz.bn, sg, k, 1.f / (float)seg_rows(g.pyr, sg)) : make_float2(1.f, 0.f);
     }
   }
-  // each thread moves rows (tid>>3) and (tid>>3)+32, 8-column vector (tid&7)*8 of both tiles
+  // each thread moves rows (tid>>3) + 32h, 8-column vector (tid&7)*8 of both tiles
   const int lr = tid >> 3, lc = (tid & 7) * 8;
   struct Stage {
-    uint4 rd[2], rx[2];
-    int rseg[2];
+    uint4 rd[HR], rx[HR];
+    int rseg[HR];
   };
+  // Branch-free fetches: a dead row (past the range or in a segment's padding) loads a live row
+  // of the block and a column vector past the row loads the row's last vector, and commit zeroes
+  // both.  A vector straddling N (or K) is loaded whole: lda / lddy % 8 == 0 keeps it inside the
+  // row, and its columns >= N (>= K) only reach dW rows (columns) that are never stored.  With
+  // every load unconditional the compiler's wait before a commit counts only that stage's loads
+  // (loads under branches made it wait for every stage in flight: s_waitcnt vmcnt(0)).
+  const bool dcol = n0 + lc < g.N, xcol = kk0 + lc < g.K;
+  const int dc = min(n0 + lc, g.lddy - 8), xc = min(kk0 + lc, g.lda - 8);
   auto fetch = [&](Stage& S, int m0) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < HR; ++h) {
       const int row = m0 + lr + 32 * h;
-      const int sg = seg_of_row(g.pyr, row);
-      const bool live = row < m_end && row < g.pyr.row_off[sg] + seg_rows(g.pyr, sg);
+      int send;
+      const int sg = seg_of_row_end(g.pyr, row, send);
+      const bool live = row < m_end && row < send;
       S.rseg[h] = live ? sg : -1;
-      const int nn = g.N - (n0 + lc), nk = g.K - (kk0 + lc);
-      S.rd[h] = make_uint4(0, 0, 0, 0);
-      S.rx[h] = make_uint4(0, 0, 0, 0);
-      if (live && nn >= 8) S.rd[h] = *reinterpret_cast<const uint4*>(DY + (size_t)row * g.lddy + n0 + lc);
-      else if (live && nn > 0) {
-        float v[8];
-        ld8m(DY + (size_t)row * g.lddy + n0 + lc, nn, v);
-        uint16_t t[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) t[j] = from_f<uint16_t>(v[j]);
-        S.rd[h] = *reinterpret_cast<uint4*>(t);
-      }
-      if (live && nk >= 8) S.rx[h] = *reinterpret_cast<const uint4*>(A + (size_t)row * g.lda + kk0 + lc);
-      else if (live && nk > 0) {
-        float v[8];
-        ld8m(A + (size_t)row * g.lda + kk0 + lc, nk, v);
-        uint16_t t[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) t[j] = from_f<uint16_t>(v[j]);
-        S.rx[h] = *reinterpret_cast<uint4*>(t);
-      }
+      const size_t r = live ? row : m_begin;
+      S.rd[h] = *reinterpret_cast<const uint4*>(DY + r * g.lddy + dc);
+      S.rx[h] = *reinterpret_cast<const uint4*>(A + r * g.lda + xc);
     }
   };
+  auto zsel = [](bool keep, uint4 v) {
+    return make_uint4(keep ? v.x : 0u, keep ? v.y : 0u, keep ? v.z : 0u, keep ? v.w : 0u);
+  };
   // SE gate of this thread's 8 columns, cached per image (the image changes every hw rows)
-  int gimg[2] = {-1, -1};
-  float gcache[2][8];
+  int gimg = -1;
+  float gcache[8];
   auto commit = [&](const Stage& S, int buf, int m0) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < HR; ++h) {
       const int r = lr + 32 * h;
-      *reinterpret_cast<uint4*>(&Ds[buf][r * WT_LDM + lc]) = S.rd[h];
-      uint4 x = S.rx[h];
+      *reinterpret_cast<uint4*>(&Ds[buf][r * WT_LDM + lc]) = zsel(S.rseg[h] >= 0 && dcol, S.rd[h]);
+      uint4 x = zsel(S.rseg[h] >= 0 && xcol, S.rx[h]);
       if constexpr (LAZY) {
         if (S.rseg[h] >= 0) {
           const int row = m0 + r, sg = S.rseg[h];
           const uint16_t* t = reinterpret_cast<const uint16_t*>(&x);
           if (g.lz.gate) {
             const int img = (row - g.pyr.row_off[sg]) / (g.pyr.H[sg] * g.pyr.W[sg]);
-            if (img != gimg[h]) {
-              gimg[h] = img;
+            if (img != gimg) {
+              gimg = img;
               const int nk = g.K - (kk0 + lc);
-              if (nk >= 8) ld8(g.lz.gate + (size_t)img * g.K + kk0 + lc, gcache[h]);
+              if (nk >= 8) ld8(g.lz.gate + (size_t)img * g.K + kk0 + lc, gcache);
               else
 #pragma unroll
-                for (int j = 0; j < 8; ++j) gcache[h][j] = j < nk ? g.lz.gate[(size_t)img * g.K + kk0 + lc + j] : 0.f;
+                for (int j = 0; j < 8; ++j) gcache[j] = j < nk ? g.lz.gate[(size_t)img * g.K + kk0 + lc + j] : 0.f;
             }
           }
           uint16_t o[8];
@@ -980,7 +1000,7 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
             float u = 0.f;
             if (kk0 + lc + j < g.K) {
               u = lazy_apply(to_f<uint16_t>(t[j]), xf[sg][lc + j], g.lz.act);
-              if (g.lz.gate) u *= gcache[h][j];
+              if (g.lz.gate) u *= gcache[j];
             }
             o[j] = from_f<uint16_t>(u);
           }
@@ -998,20 +1018,21 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
     for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   float dbacc = 0.f;
   if constexpr (LAZY) __syncthreads();  // xf tables
-  // Two register stages in flight: stage m+1 was fetched two iterations before its commit
-  // (one stage ahead left each 64-row stage waiting a full memory round trip; the mid-size
-  // shapes run ~1 block per CU, so nothing else hid it: 8192 x 672 -> 192 at 0.7 TB/s)
-  Stage S0, S1;
-  if (m_begin < m_end) {
-    fetch(S0, m_begin);
-    commit(S0, 0, m_begin);
-  }
-  if (m_begin + WT_BM < m_end) fetch(S0, m_begin + WT_BM);
-  if (m_begin + 2 * WT_BM < m_end) fetch(S1, m_begin + 2 * WT_BM);
-  __syncthreads();
-  auto iter = [&](Stage& S, int m0, int buf) {
+  // stage t sits in LDS buffer t & 1; stage t + 1 is in register slot t % PF when stage t is
+  // multiplied, and its slot is refilled with stage t + 1 + PF right after its commit
+  // Every fetch / commit / stage runs unconditionally (stages past the block's rows are all
+  // dead rows: zeros in LDS, nothing added): a fetch under a branch leaves the compiler's
+  // wait-count merge pessimistic, and each commit then waited for the stages behind it too.
+  Stage S[PF];
+  fetch(S[0], m_begin);
+  commit(S[0], 0, m_begin);
 #pragma unroll
-    for (int ks = 0; ks < WT_BM; ks += 32) {
+  for (int p = 0; p < PF; ++p) fetch(S[p], m_begin + (p + 1) * BM);
+  __syncthreads();
+  int t = 0;
+  auto iter = [&](Stage& R, int m0, int buf) {
+#pragma unroll
+    for (int ks = 0; ks < BM; ks += 32) {
       bf16x8_t af[2], bfr[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) af[i] = tr_frag(Ds[buf], WT_LDM, ks, wn * 32 + i * 16);
@@ -1024,17 +1045,19 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (do_db) {
-      const uint16_t* col = &Ds[buf][(wave * 16) * WT_LDM + lane];
+      const uint16_t* col = &Ds[buf][(wave * (BM / 4)) * WT_LDM + lane];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) dbacc += to_f<uint16_t>(col[m * WT_LDM]);
+      for (int m = 0; m < BM / 4; ++m) dbacc += to_f<uint16_t>(col[m * WT_LDM]);
     }
-    if (m0 + WT_BM < m_end) commit(S, buf ^ 1, m0 + WT_BM);
-    if (m0 + 3 * WT_BM < m_end) fetch(S, m0 + 3 * WT_BM);
+    commit(R, buf ^ 1, m0 + BM);
+    fetch(R, m0 + (PF + 1) * BM);
     __syncthreads();
+    ++t;
   };
-  for (int m0 = m_begin; m0 < m_end; m0 += 2 * WT_BM) {
-    iter(S0, m0, 0);
-    if (m0 + WT_BM < m_end) iter(S1, m0 + WT_BM, 1);
+  for (int m0 = m_begin; m0 < m_end; m0 += PF * BM) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p)  // (an even PF keeps the LDS buffer a compile-time constant)
+      iter(S[p], m0 + p * BM, PF % 2 == 0 ? (p & 1) : (t & 1));
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -1964,7 +1987,8 @@ static int launch_gemm(GemmArgs g, hipStream_t s) {
   g.ntn = cdiv(g.N, BN);
   const int nwg = g.ntm * g.ntn;
   if (nwg == 0) return EDET_OK;
-  const size_t dyn = LAZY ? (size_t)g.K * (sizeof(float2) + 2 * sizeof(float)) : 0;
+  const int nimg = (LAZY && g.lz.gate) ? gemm_gate_imgs(BM, g.pyr.H[0] * g.pyr.W[0], g.pyr.batch) : 0;
+  const size_t dyn = LAZY ? (size_t)g.K * (sizeof(float2) + nimg * sizeof(float)) : 0;
   EDET_LAUNCH((k_gemm<T, BM, BN, KC, LAZY, FOLD>), dim3(nwg), dim3(256), dyn, s, g);
   return check_launch("edet gemm");
 }
@@ -2278,8 +2302,29 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
     // 240: 37 -> 27 us); many tiles keep the atomics (class predict 105 vs 124 us with partials)
     const bool use_part = dev_knob(2) == 1 || (dev_knob(2) == 0 && tiles <= 4 && split >= 128);
     g.part = use_part && split > 1 ? workspace_f32((size_t)split * ((size_t)N * K + N)) : nullptr;
-    if (plain) EDET_LAUNCH((k_wgrad_tr<false>), dim3(tiles * split), dim3(256), 0, s, g);
-    else EDET_LAUNCH((k_wgrad_tr<true>), dim3(tiles * split), dim3(256), 0, s, g);
+    // stage rows / stages in flight (development slot 21: 1 = 64/3, 2 = 64/4, 3 = 128/2, 4 = 128/3)
+    const int form = dev_knob(21);
+    // (whole PF-stage rounds per block: a block runs its stages in rounds of PF)
+    const int bm = (form >= 3 ? 128 : 64) * (form == 1 || form == 4 ? 3 : form == 2 ? 4 : 2);
+    if (g.rows_per % bm) {
+      g.rows_per = cdiv(g.rows_per, bm) * bm;
+      split = std::max(1, cdiv(g.M, g.rows_per));
+      if (g.part) g.part = workspace_f32((size_t)split * ((size_t)N * K + N));
+    }
+    const dim3 grid(tiles * split);
+#define EDET_WGT(BM_, PF_)                                                            \
+  do {                                                                                \
+    if (plain) EDET_LAUNCH((k_wgrad_tr<false, BM_, PF_>), grid, dim3(256), 0, s, g); \
+    else EDET_LAUNCH((k_wgrad_tr<true, BM_, PF_>), grid, dim3(256), 0, s, g);        \
+  } while (0)
+    switch (form) {
+      case 1: EDET_WGT(64, 3); break;
+      case 2: EDET_WGT(64, 4); break;
+      case 3: EDET_WGT(128, 2); break;
+      case 4: EDET_WGT(128, 3); break;
+      default: EDET_WGT(64, 2); break;
+    }
+#undef EDET_WGT
     int rc = check_launch("edet wgrad");
     if (rc || !g.part) return rc;
     return sum_partials(g.part, split, (long)N * K, dwt, s, N, dbias);  // dW and db, one launch

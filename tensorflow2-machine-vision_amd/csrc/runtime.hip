@@ -33,8 +33,8 @@ int check_launch(const char* what) {
 }
 
 #ifdef EDET_DEV
-static int g_dev[32] = {};
-int dev_knob(int slot) { return (slot >= 0 && slot < 32) ? g_dev[slot] : 0; }
+static int g_dev[64] = {};
+int dev_knob(int slot) { return (slot >= 0 && slot < 64) ? g_dev[slot] : 0; }
 #endif
 
 // Caller-registered scratch for split reductions (weight gradients): blocks write partial
@@ -124,7 +124,7 @@ int edet_launched_kernels(char* buf, size_t size) {
 
 int edet_dev_set(int slot, int value) {
 #ifdef EDET_DEV
-  if (slot < 0 || slot >= 32) return 0;
+  if (slot < 0 || slot >= 64) return 0;
   const int old = edet::g_dev[slot];
   edet::g_dev[slot] = value;
   return old;
