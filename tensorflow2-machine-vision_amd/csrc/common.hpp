@@ -201,6 +201,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, lon
   const uint32_t n = bytes <= 0 ? 0u : (bytes >= (long)BUF_OOB ? BUF_OOB : (uint32_t)bytes);
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, 0x00020000);
 }
+// off when ok, else an offset past any range -- as arithmetic: a select here was turned into
+// control flow around the load, and the register merge after it cost a full wait
+__device__ __forceinline__ uint32_t buf_off(bool ok, uint32_t off) { return off | ((uint32_t)!ok << 31); }
 __device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }

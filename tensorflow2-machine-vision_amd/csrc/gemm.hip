@@ -82,19 +82,24 @@ __device__ __forceinline__ void stage_rows(T* lds, int lds_ld, const T* src, int
   using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
   constexpr int VW = sizeof(T) == 2 ? 1 : 2, U = 8;
   const int kv8 = KP / 8, total = nrows * kv8;
+  // range-checked loads: rows at or past nvalid read zeros, vectors at or past K take an
+  // out-of-range offset (a select on each loaded value made the compiler wait for it at once)
+  const auto rs = buf_rsrc(src, (long)min(nrows, nvalid) * ld * (long)sizeof(T));
   for (int v0 = 0; v0 < total; v0 += 256 * U) {
     V t[U][VW];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int v = v0 + threadIdx.x + u * 256;
       const int n = v / kv8, kv = (v - n * kv8) * 8;
-      const bool ok = v < total && n < nvalid && kv < K;
-      const V* p = reinterpret_cast<const V*>(src + (ok ? (size_t)n * ld + kv : 0));
+      const uint32_t off = buf_off(v < total && kv < K, (uint32_t)((n * ld + kv) * (int)sizeof(T)));
 #pragma unroll
-      for (int w = 0; w < VW; ++w) t[u][w] = p[w];
+      for (int w = 0; w < VW; ++w) t[u][w] = __builtin_bit_cast(V, buf_ld16(rs, off + 16 * w));
+    }
 #pragma unroll
-      for (int w = 0; w < VW; ++w) t[u][w] = ok ? t[u][w] : V{};
-      if (ok && K - kv < 8) {  // tail vector: zero the elements at or past K
+    for (int u = 0; u < U; ++u) {
+      const int v = v0 + threadIdx.x + u * 256;
+      const int n = v / kv8, kv = (v - n * kv8) * 8;
+      if (v < total && kv < K && K - kv < 8) {  // tail vector: zero the elements at or past K
         T* e = reinterpret_cast<T*>(&t[u][0]);
 #pragma unroll
         for (int j = 0; j < 8; ++j)
@@ -225,7 +230,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     for (int u = 0; u < AV; ++u) {
       const int v = tid + u * 256;
       const int r = v / KV, kv = (v % KV) * 8;
-      const uint32_t off = (v < BM * KV && k0 + kv < g.K) ? (uint32_t)((r * g.lda + k0 + kv) * (int)sizeof(T)) : BUF_OOB;
+      const uint32_t off = buf_off(v < BM * KV && k0 + kv < g.K, (uint32_t)((r * g.lda + k0 + kv) * (int)sizeof(T)));
 #pragma unroll
       for (int w = 0; w < VW; ++w) R.ra[u][w] = __builtin_bit_cast(V, buf_ld16(ra_, off + 16 * w));
     }
@@ -233,7 +238,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     for (int u = 0; u < BV; ++u) {
       const int v = tid + u * 256;
       const int n = v / KV, kv = (v % KV) * 8;
-      const uint32_t off = (v < BN * KV && k0 + kv < g.K) ? (uint32_t)((n * g.ldb + k0 + kv) * (int)sizeof(T)) : BUF_OOB;
+      const uint32_t off = buf_off(v < BN * KV && k0 + kv < g.K, (uint32_t)((n * g.ldb + k0 + kv) * (int)sizeof(T)));
 #pragma unroll
       for (int w = 0; w < VW; ++w) R.rb[u][w] = __builtin_bit_cast(V, buf_ld16(rb_, off + 16 * w));
     }
@@ -468,8 +473,9 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   // two wm halves are added in a fixed order at the flush (LDS float atomics would make the
   // block partial depend on wave timing, and BN statistics must be reproducible)
   float* red = reinterpret_cast<float*>(Cs + BM * LDC);
-  float2* xf = reinterpret_cast<float2*>(red + 4 * LDC);  // [K] (LAZY)
-  float* gt = reinterpret_cast<float*>(xf + (LAZY ? g.K : 0));  // [2][K] SE gate rows (LAZY)
+  float* bias_s = red + 4 * LDC;                           // [LDC] this split's bias
+  float2* xf = reinterpret_cast<float2*>(bias_s + LDC);    // [K] (LAZY)
+  float* gt = reinterpret_cast<float*>(xf + (LAZY ? g.K : 0));  // [images][K] SE gate rows (LAZY)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -487,6 +493,7 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   const int cbase = ch_begin * RNB;                      // first column of this split
   const int ncols = min(N, ch_end * RNB) - cbase;         // valid columns of this split
   for (int c = tid; c < 4 * LDC; c += 256) red[c] = 0.f;
+  for (int c = tid; c < LDC; c += 256) bias_s[c] = (g.bias && c < ncols) ? g.bias[cbase + c] : 0.f;
   int cur_seg = -1;
 
   // A tile rows: vector v = v0 + tid + u*256 is row v / kv8, channels (v % kv8) * 8 .. +8
@@ -494,46 +501,62 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   const int kv8 = KP / 8;
   using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
   constexpr int VW = sizeof(T) == 2 ? 1 : 2, UNR = 4;
-  auto fetch_a = [&](V (&raw)[UNR][VW], int tmt, int v0) {  // select-predicated, all in flight
+  // range-checked loads (rows past M, columns past K read zeros): every load is issued
+  // unconditionally and needs no select, so the compiler does not wait for it where it is issued
+  auto fetch_a = [&](V (&raw)[UNR][VW], int tmt, int v0) {
+    const auto rs = buf_rsrc(A + (size_t)tmt * BM * g.lda, (long)min(BM, g.M - tmt * BM) * g.lda * (long)sizeof(T));
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int v = v0 + tid + u * 256;
       const int r = v / kv8, kv = (v - r * kv8) * 8;
-      const int grow = tmt * BM + r;
-      const bool ok = v < BM * kv8 && grow < g.M && kv < K;  // K % 8 == 0: whole vectors
-      const V* src = reinterpret_cast<const V*>(A + (ok ? (size_t)grow * g.lda + kv : 0));
+      const uint32_t off = buf_off(v < BM * kv8 && kv < K, (uint32_t)((r * g.lda + kv) * (int)sizeof(T)));
 #pragma unroll
-      for (int w = 0; w < VW; ++w) raw[u][w] = ok ? src[w] : V{};
+      for (int w = 0; w < VW; ++w) raw[u][w] = __builtin_bit_cast(V, buf_ld16(rs, off + 16 * w));
     }
   };
-  auto commit_a = [&](const V (&raw)[UNR][VW], int v0, int row0, int seg_off, int hw, bool gate_lds, int n_lo) {
+  const bool has_gate = LAZY && g.lz.gate != nullptr;
+  auto lazy_a = [&](auto act_c, auto gate_c, const V (&raw)[UNR][VW], int v0, int row0, int seg_off, int hw, int n_lo) {
+    constexpr bool ACT = decltype(act_c)::value, GATE = decltype(gate_c)::value;
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const int v = v0 + tid + u * 256;
       if (v >= BM * kv8) break;
       const int r = v / kv8, kv = (v - r * kv8) * 8;
       const int grow = row0 + r;
-      T* dst = &As[r * LDA + kv];
-      if constexpr (LAZY) {
-        const T* e = reinterpret_cast<const T*>(&raw[u][0]);
-        float vals[8];
-        const bool live = grow < g.M && kv < K;
-        const int img = (grow - seg_off) / hw;
-        const float* gp = nullptr;
-        if (live && g.lz.gate) gp = gate_lds ? gt + (img - n_lo) * K : g.lz.gate + (size_t)img * K;
+      const bool live = grow < g.M && kv < K;
+      const int gbase = GATE ? ((min(grow, g.M - 1) - seg_off) / hw - n_lo) * K : 0;
+      const T* e = reinterpret_cast<const T*>(&raw[u][0]);
+      float vals[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float x = 0.f;
-          if (live) {
-            x = lazy_apply(to_f<T>(e[j]), xf[kv + j], g.lz.act);
-            if (gp) x *= gp[kv + j];
-          }
-          vals[j] = x;
-        }
-        st8(dst, vals);
+      for (int j = 0; j < 8; ++j) {
+        const int k = min(kv + j, K - 1);
+        float x = to_f<T>(e[j]) * xf[k].x + xf[k].y;
+        if constexpr (ACT) x = swishf_(x);
+        if constexpr (GATE) x *= gt[gbase + k];
+        vals[j] = live ? x : 0.f;
+      }
+      st8(&As[r * LDA + kv], vals);
+    }
+  };
+  auto commit_a = [&](const V (&raw)[UNR][VW], int v0, int row0, int seg_off, int hw, int n_lo) {
+    if constexpr (LAZY) {
+      using TT = std::true_type;
+      using FF = std::false_type;
+      if (g.lz.act) {
+        if (has_gate) lazy_a(TT{}, TT{}, raw, v0, row0, seg_off, hw, n_lo);
+        else lazy_a(TT{}, FF{}, raw, v0, row0, seg_off, hw, n_lo);
       } else {
+        if (has_gate) lazy_a(FF{}, TT{}, raw, v0, row0, seg_off, hw, n_lo);
+        else lazy_a(FF{}, FF{}, raw, v0, row0, seg_off, hw, n_lo);
+      }
+    } else {
 #pragma unroll
-        for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(dst)[w] = raw[u][w];
+      for (int u = 0; u < UNR; ++u) {
+        const int v = v0 + tid + u * 256;
+        if (v >= BM * kv8) break;
+        const int r = v / kv8, kv = (v - r * kv8) * 8;
+#pragma unroll
+        for (int w = 0; w < VW; ++w) reinterpret_cast<V*>(&As[r * LDA + kv])[w] = raw[u][w];
       }
     }
   };
@@ -558,16 +581,15 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
       else zero8(dst);
     }
   };
-  auto fetch_b = [&](int ch) {  // registers, every load issued before any use (K % 8 == 0)
+  auto fetch_b = [&](int ch) {  // registers, range-checked (K % 8 == 0)
+    const auto rs = buf_rsrc(B + (size_t)ch * RNB * g.ldb, (long)min(RNB, N - ch * RNB) * g.ldb * (long)sizeof(T));
 #pragma unroll
     for (int u = 0; u < NBV; ++u) {
       const int v = tid + u * 256;
       const int n = v / kv8, kv = (v - n * kv8) * 8;
-      const int gn = ch * RNB + n;
-      const bool ok = v < RNB * kv8 && gn < N && kv < K;
-      const VB* src = reinterpret_cast<const VB*>(B + (ok ? (size_t)gn * g.ldb + kv : 0));
+      const uint32_t off = buf_off(v < RNB * kv8 && kv < K, (uint32_t)((n * g.ldb + kv) * (int)sizeof(T)));
 #pragma unroll
-      for (int w = 0; w < VWB; ++w) rb[u][w] = ok ? src[w] : VB{};
+      for (int w = 0; w < VWB; ++w) rb[u][w] = __builtin_bit_cast(VB, buf_ld16(rs, off + 16 * w));
     }
   };
   auto commit_b = [&](T* bs) {
@@ -603,13 +625,13 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
     cur_seg = seg;
     __syncthreads();
   }
-  // ---- SE gate rows of this tile's images in LDS (a tile spans <= 2 images when hw >= BM)
-  const bool gate_lds = LAZY && g.lz.gate != nullptr && hw >= BM;
+  // ---- SE gate rows of this tile's images in LDS (gemm_gate_imgs of them)
   const int n_lo = (row0 - seg_off) / hw;
-  if (gate_lds) {
-    for (int k = tid; k < 2 * K; k += 256) {
-      const int n = n_lo + (k >= K);
-      gt[k] = (n < g.pyr.batch) ? g.lz.gate[(size_t)n * K + (k >= K ? k - K : k)] : 0.f;
+  if (has_gate) {
+    const int ni = gemm_gate_imgs(BM, hw, g.pyr.batch);
+    for (int e = tid; e < ni * K; e += 256) {
+      const int i = e / K, k = e - i * K, n = n_lo + i;
+      gt[e] = (n < g.pyr.batch) ? g.lz.gate[(size_t)n * K + k] : 0.f;
     }
     __syncthreads();
   }
@@ -618,16 +640,17 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   // fetched here and committed at the next tile's start (its HBM latency overlaps this tile's
   // MFMAs, epilogue and write-out)
   if (apre) {
-    commit_a(araw, 0, row0, seg_off, hw, gate_lds, n_lo);
-    if (tm + G < ntm) fetch_a(araw, tm + G, 0);
+    commit_a(araw, 0, row0, seg_off, hw, n_lo);
   } else {
     for (int v0 = 0; v0 < BM * kv8; v0 += 256 * UNR) {
       V raw[UNR][VW];
       fetch_a(raw, tm, v0);
-      commit_a(raw, v0, row0, seg_off, hw, gate_lds, n_lo);
+      commit_a(raw, v0, row0, seg_off, hw, n_lo);
     }
   }
   if (!bres) load_b(ch_begin, Bs);
+  // (after the in-place B loads: their waits would drain it -- the wait counter is in order)
+  if (apre && tm + G < ntm) fetch_a(araw, tm + G, 0);
   __syncthreads();
   if (bpipe && ch_begin + 1 < ch_end) fetch_b(ch_begin + 1);
   for (int ch = ch_begin; ch < ch_end; ++ch) {
@@ -678,7 +701,7 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
     for (int j = 0; j < FN; ++j) {
       const int cl = wn * 32 + j * 16 + (lane & 15);
       const int col = col0 + cl;
-      const float bv = (g.bias && col < N) ? g.bias[col] : 0.f;
+      const float bv = col - cbase < LDC ? bias_s[col - cbase] : 0.f;
       float s = 0.f, q = 0.f;
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -1321,8 +1344,9 @@ struct PwPlan {
 
 constexpr int PW_NV = 8;  // max 16-byte A vectors per thread per chunk
 
-template <typename T, int FN, bool KSTREAM, bool LAZY>
+template <typename T, int FN, bool KSTREAM, bool LAZY, bool GATE = false>
 __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
+  static_assert(!GATE || LAZY, "gate: lazy A only");
   using V = typename std::conditional<sizeof(T) == 2, uint4, float4>::type;
   constexpr int VW = sizeof(T) == 2 ? 1 : 2;
   constexpr int CWLD = 16 * FN + 8;
@@ -1331,7 +1355,9 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
   T* As = Bs + (size_t)p.NG * p.LDB;                    // [2][R][LDA]
   T* Cw = As + 2 * (size_t)p.R * p.LDA;                 // [4 waves][32][CWLD]
   float* red = reinterpret_cast<float*>(Cw + 4 * 32 * CWLD);  // [sum|sq][wm][NGtot]
-  float2* xf = reinterpret_cast<float2*>(red + 4 * p.NGtot);  // [nseg][KP] (LAZY)
+  float* bias_s = red + 4 * p.NGtot;                          // [NGtot] (a bias load in the
+  // epilogue would be waited for behind the next chunk's prefetch)
+  float2* xf = reinterpret_cast<float2*>(bias_s + p.NGtot);   // [nseg][KP] (LAZY)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -1353,6 +1379,7 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
       else zero8(dst);
     }
     for (int c = tid; c < 4 * p.NGtot; c += 256) red[c] = 0.f;
+    for (int c = tid; c < p.NGtot; c += 256) bias_s[c] = (g.bias && col_base + c < N) ? g.bias[col_base + c] : 0.f;
     if constexpr (LAZY) {
       for (int s = 0; s < g.pyr.nseg; ++s) {
         const float inv = 1.f / (float)seg_rows(g.pyr, s);
@@ -1365,34 +1392,34 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
   const int nvec = p.R * KV;
   const int nq = ((p.nrg - 1 - rg0) / G + 1) * p.nkc;
   const T* A = (const T*)g.a;
-  const bool has_gate = LAZY && g.lz.gate != nullptr;
+  constexpr bool has_gate = GATE;  // (the gate vectors cost 64 registers: their own instance)
   V ra[PW_NV][VW];
-  float4 gr[LAZY ? PW_NV : 1][2];
+  float4 gr[GATE ? PW_NV : 1][2];
 
+  // Branch-free fetch: range-checked loads (rows past M, columns past K and the gate of a dead
+  // element read zeros; a launch without a gate reads through an empty range).  Loads under
+  // branches merged into registers that live across the chunk loop: the compiler waited for
+  // each one where it was issued.
+  const auto rs_gate = buf_rsrc(GATE ? g.lz.gate : nullptr, GATE ? (long)g.pyr.batch * K * 4 : 0);
   auto fetch = [&](int q) {
     const int rg = rg0 + (q / p.nkc) * G, kc = q % p.nkc;
     const int rbase = rg * p.R;
     int seg = 0, seg_off = 0, hw = 1;
     if (has_gate) { seg = seg_of_row(g.pyr, rbase); seg_off = g.pyr.row_off[seg]; hw = g.pyr.H[seg] * g.pyr.W[seg]; }
+    const auto rs_a = buf_rsrc(A + (size_t)rbase * g.lda, (long)min(p.R, M - rbase) * g.lda * (long)sizeof(T));
 #pragma unroll
     for (int u = 0; u < PW_NV; ++u) {
       const int v = tid + u * 256;
-#pragma unroll
-      for (int ww = 0; ww < VW; ++ww) ra[u][ww] = V{};
       const int r = v / KV, kv = (v - r * KV) * 8;
       const int grow = rbase + r, gk = kc * p.KC + kv;
-      const bool live = v < nvec && grow < M && gk < K;
-      if (live) {
-        const V* src = reinterpret_cast<const V*>(A + (size_t)grow * g.lda + gk);
+      const bool ok = v < nvec && gk < K;
+      const uint32_t off = buf_off(ok, (uint32_t)((r * g.lda + gk) * (int)sizeof(T)));
 #pragma unroll
-        for (int ww = 0; ww < VW; ++ww) ra[u][ww] = src[ww];
-      }
-      if constexpr (LAZY) {
-        if (has_gate && live) {
-          const float4* gp = reinterpret_cast<const float4*>(g.lz.gate + (size_t)((grow - seg_off) / hw) * K + gk);
-          gr[u][0] = gp[0];
-          gr[u][1] = gp[1];
-        }
+      for (int ww = 0; ww < VW; ++ww) ra[u][ww] = __builtin_bit_cast(V, buf_ld16(rs_a, off + 16 * ww));
+      if constexpr (GATE) {
+        const uint32_t goff = buf_off(ok && grow < M, (uint32_t)((((grow - seg_off) / hw) * K + gk) * 4));
+        gr[u][0] = __builtin_bit_cast(float4, buf_ld16(rs_gate, goff));
+        gr[u][1] = __builtin_bit_cast(float4, buf_ld16(rs_gate, goff + 16));
       }
     }
   };
@@ -1411,8 +1438,9 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
         const int grow = rbase + r, gk = kc * p.KC + kv;
         const bool live = grow < M && gk < K;
         const T* e = reinterpret_cast<const T*>(&ra[u][0]);
-        const float gv[8] = {gr[u][0].x, gr[u][0].y, gr[u][0].z, gr[u][0].w,
-                             gr[u][1].x, gr[u][1].y, gr[u][1].z, gr[u][1].w};
+        const float4 g0 = GATE ? gr[u][0] : make_float4(1.f, 1.f, 1.f, 1.f);
+        const float4 g1 = GATE ? gr[u][1] : make_float4(1.f, 1.f, 1.f, 1.f);
+        const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
         const float2* af = xf + seg * p.KP + (live ? gk : 0);
         float vals[8];
 #pragma unroll
@@ -1472,8 +1500,7 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int cl = wcl0 + j * 16 + (lane & 15);
-      const int col = col_base + cl;
-      const float bv = (g.bias && col < N) ? g.bias[col] : 0.f;
+      const float bv = bias_s[cl];
       float s = 0.f, q = 0.f;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -1578,7 +1605,7 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
 
 static size_t pw_lds(const PwPlan& p, int FN, int nseg, bool lazy, int es) {
   return (size_t)p.NG * p.LDB * es + 2 * (size_t)p.R * p.LDA * es + 4 * 32 * (16 * FN + 8) * (size_t)es +
-         4 * (size_t)p.NGtot * 4 + (lazy ? (size_t)nseg * p.KP * 8 : 0);
+         5 * (size_t)p.NGtot * 4 + (lazy ? (size_t)nseg * p.KP * 8 : 0);
 }
 
 // Plan the B-resident launch; false when the shape does not fit (caller falls back).
@@ -1643,7 +1670,8 @@ static int launch_pwb(const GemmArgs& g, const PwPlan& p, hipStream_t s) {
   const long want = (long)256 * per_cu;
   long rows = std::min<long>(p.nrg, std::max<long>(1, want / p.ngroups));
   const int grid = (int)(rows * p.ngroups);
-  EDET_LAUNCH((k_pwb<T, FN, KS, LAZY>), dim3(grid), dim3(256), lds, s, g, p);
+  if (LAZY && g.lz.gate) EDET_LAUNCH((k_pwb<T, FN, KS, LAZY, LAZY>), dim3(grid), dim3(256), lds, s, g, p);
+  else EDET_LAUNCH((k_pwb<T, FN, KS, LAZY>), dim3(grid), dim3(256), lds, s, g, p);
   return check_launch("edet pwb");
 }
 
@@ -1773,13 +1801,27 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   // FOLD: the folded value's raw x at this lane's output positions (row, 4 channels per
   // fragment), fetched with the group's A rows
   const T* X = (const T*)g.fx.x;
-  auto fetch = [&](int grp, uint4* v, uint2* xv) {
-    const int row = grp * 16 + (lane & 15);
+  // Range-checked loads over the block's rows (buf_ld16): a group past the block's range, a row
+  // past M and k past K read zeros, with no branch and no select -- and the SE gate values of
+  // the group come with its A rows (a gate load at the use waited for every load in flight).
+  const auto rs_a = buf_rsrc(A + (size_t)g_begin * 16 * g.lda,
+                             (long)(min(g_end * 16, M) - g_begin * 16) * g.lda * (long)sizeof(T));
+  const bool has_gate = LAZY && g.lz.gate != nullptr;
+  const auto rs_g = buf_rsrc(LAZY ? g.lz.gate : nullptr, has_gate ? (long)g.pyr.batch * K * 4 : 0);
+  constexpr int NG = LAZY ? KS : 1;
+  auto fetch = [&](int grp, uint4* v, float4 (*gv)[2], uint2* xv) {
+    const int rl = (grp - g_begin) * 16 + (lane & 15), row = grp * 16 + (lane & 15);
+    const bool gok = grp < g_end;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int k = 32 * ks + kq;
-      v[ks] = make_uint4(0, 0, 0, 0);
-      if (k < K && grp < g_end) v[ks] = *reinterpret_cast<const uint4*>(A + (size_t)(row < M ? row : 0) * g.lda + k);
+      const uint32_t off = buf_off(k < K && gok, (uint32_t)((rl * g.lda + k) * (int)sizeof(T)));
+      v[ks] = buf_ld16(rs_a, off);
+      if constexpr (LAZY) {
+        const uint32_t go = buf_off(k < K && gok && row < M, (uint32_t)(((row / hw) * K + k) * 4));
+        gv[ks][0] = __builtin_bit_cast(float4, buf_ld16(rs_g, go));
+        gv[ks][1] = __builtin_bit_cast(float4, buf_ld16(rs_g, go + 16));
+      }
     }
     if constexpr (FOLD) {
 #pragma unroll
@@ -1791,39 +1833,27 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
       }
     }
   };
-  uint4 pre[GS_PF][KS];
-  uint2 prex[GS_PF][FOLD ? NF : 1];
-#pragma unroll
-  for (int u = 0; u < GS_PF; ++u) fetch(g_begin + wave + u * 4, pre[u], prex[u]);
-  for (int grp = g_begin + wave; grp < g_end; grp += 4) {
+  // one 16-row group: transform + MFMA into the wave's staging rows, the refill of this slot
+  // (GS_PF groups ahead) issued before the group's stores (vmcnt counts loads and stores in
+  // order: a load issued after the stores would wait for them), then the stores.  Slots are
+  // compile-time (the loop below is unrolled by GS_PF): rotating in-flight registers through a
+  // rolled loop made the compiler wait for each load where its register was moved.
+  auto group = [&](int grp, uint4 (&pre)[KS], float4 (&pg)[NG][2], uint2 (&prex)[FOLD ? NF : 1]) {
     const int row = grp * 16 + (lane & 15);
     if (g.has_stats && grp * 16 >= seg_end) {  // wave-uniform; segments start on 128-row multiples
-      const int sg = seg_of_row(g.pyr, grp * 16);  // (padding rows past a segment map to it)
+      int send;
+      const int sg = seg_of_row_end(g.pyr, grp * 16, send);  // (padding rows past a segment map to it)
       if (sg != cur_seg) {
         if (cur_seg >= 0) wflush(cur_seg);
         cur_seg = sg;
-        seg_end = g.pyr.row_off[sg] + seg_rows(g.pyr, sg);
+        seg_end = send;
       }
     }
     const bool live = row < M && row < seg_end;
-    uint4 raw[KS];
-    uint2 xcur[FOLD ? NF : 1];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) raw[ks] = pre[0][ks];
-#pragma unroll
-    for (int f = 0; f < (FOLD ? NF : 1); ++f) xcur[f] = prex[0][f];
-#pragma unroll
-    for (int u = 0; u + 1 < GS_PF; ++u) {
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) pre[u][ks] = pre[u + 1][ks];
-#pragma unroll
-      for (int f = 0; f < (FOLD ? NF : 1); ++f) prex[u][f] = prex[u + 1][f];
-    }
-    fetch(grp + GS_PF * 4, pre[GS_PF - 1], prex[GS_PF - 1]);
     bf16x8_t bfrag[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      uint4 rv = raw[ks];
+      uint4 rv = pre[ks];
       if constexpr (LAZY) {
         const int k0 = 32 * ks + kq;
         float x[8];
@@ -1833,19 +1863,22 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
           x[2 * i] = __uint_as_float(w4[i] << 16);
           x[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
         }
-        float gt[8];
-        if (g.lz.gate && k0 < K) ld8(g.lz.gate + (size_t)((live ? row : 0) / hw) * K + k0, gt);
+        const float gt[8] = {pg[ks][0].x, pg[ks][0].y, pg[ks][0].z, pg[ks][0].w,
+                             pg[ks][1].x, pg[ks][1].y, pg[ks][1].z, pg[ks][1].w};
         uint16_t o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float u = lazy_apply(x[j], af[ks][j], g.lz.act);
-          if (g.lz.gate) u *= (k0 < K ? gt[j] : 0.f);
+          if (has_gate) u *= gt[j];
           o[j] = k0 + j < K ? f2bf(u) : (uint16_t)0;
         }
         rv = *reinterpret_cast<uint4*>(o);
       }
       bfrag[ks] = __builtin_bit_cast(bf16x8_t, rv);
     }
+    uint2 xcur[FOLD ? NF : 1];
+#pragma unroll
+    for (int f = 0; f < (FOLD ? NF : 1); ++f) xcur[f] = prex[f];
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
       floatx4 d = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -1870,19 +1903,35 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
       *reinterpret_cast<uint2*>(cw + (lane & 15) * LDW + n0) =
           make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
     }
+    fetch(grp + GS_PF * 4, pre, pg, prex);
     // the 16 x N tile leaves as 16-byte vectors, a whole row range per store instruction
+    // (a fixed number of store slots per lane, so the wait counts stay exact)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int vpr = N / 8, row0 = grp * 16;
-    for (int e = lane; e < 16 * vpr; e += 64) {
+#pragma unroll
+    for (int i = 0; i < (32 * NF + 63) / 64; ++i) {
+      const int e = lane + 64 * i;
       const int rl = e / vpr, c8 = (e - rl * vpr) * 8;
-      if (row0 + rl < M)
+      if (e < 16 * vpr && row0 + rl < M)
         *reinterpret_cast<uint4*>(Y + (size_t)(row0 + rl) * g.ldc + c8) = *reinterpret_cast<const uint4*>(cw + rl * LDW + c8);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  uint4 pre[GS_PF][KS];
+  float4 pg[GS_PF][NG][2];
+  uint2 prex[GS_PF][FOLD ? NF : 1];
+#pragma unroll
+  for (int u = 0; u < GS_PF; ++u) fetch(g_begin + wave + u * 4, pre[u], pg[u], prex[u]);
+  for (int grp0 = g_begin + wave; grp0 < g_end; grp0 += 4 * GS_PF) {
+#pragma unroll
+    for (int u = 0; u < GS_PF; ++u) {
+      if (grp0 + 4 * u >= g_end) break;
+      group(grp0 + 4 * u, pre[u], pg[u], prex[u]);
+    }
   }
   if (!g.has_stats) return;  // block-uniform
   if (cur_seg >= 0) wflush(cur_seg);
@@ -1993,11 +2042,12 @@ static int launch_gemm(GemmArgs g, hipStream_t s) {
   return check_launch("edet gemm");
 }
 
+// gemm_r's LDS image; nimg = SE gate rows staged per tile (gemm_gate_imgs, 0 without a gate)
 template <typename T, int BM, bool LAZY>
-static size_t gemm_r_lds(int K, int KP, int LDC) {
+static size_t gemm_r_lds(int K, int KP, int LDC, int nimg = 2) {
   return (size_t)(BM + (KP <= 128 ? 2 : 1) * RNB) * (KP + 8) * sizeof(T) + (size_t)BM * LDC * sizeof(T) +
-         4 * (size_t)LDC * sizeof(float) +
-         (LAZY ? (size_t)K * (sizeof(float2) + 2 * sizeof(float)) : 0);
+         5 * (size_t)LDC * sizeof(float) +
+         (LAZY ? (size_t)K * (sizeof(float2) + nimg * sizeof(float)) : 0);
 }
 
 template <typename T, int BM, bool LAZY>
@@ -2010,10 +2060,11 @@ static int launch_gemm_r(GemmArgs g, hipStream_t s) {
   if (nsplit > nch) nsplit = nch;
   int cps = cdiv(nch, nsplit);
   // narrow the per-block column range until the staged C tile fits
-  while (cps > 1 && gemm_r_lds<T, BM, LAZY>(g.K, KP, cps * RNB) > 150 * 1024) cps = cdiv(cps, 2);
+  const int nimg = (LAZY && g.lz.gate) ? gemm_gate_imgs(BM, g.pyr.H[0] * g.pyr.W[0], g.pyr.batch) : 0;
+  while (cps > 1 && gemm_r_lds<T, BM, LAZY>(g.K, KP, cps * RNB, nimg) > 150 * 1024) cps = cdiv(cps, 2);
   nsplit = cdiv(nch, cps);
   const int LDC = nsplit == 1 ? cdiv(g.N, 8) * 8 : cps * RNB;
-  const size_t lds = gemm_r_lds<T, BM, LAZY>(g.K, KP, LDC);
+  const size_t lds = gemm_r_lds<T, BM, LAZY>(g.K, KP, LDC, nimg);
   EDET_REQUIRE(lds <= 160 * 1024, "edet gemm_r: tile does not fit LDS (K=%d N=%d)", g.K, g.N);
   if (ntm == 0) return EDET_OK;
   // resident blocks per CU from the LDS image; the row-tile workers per split fill that once
@@ -2087,6 +2138,9 @@ static int dispatch_dgrad_fold(const GemmArgs& g, hipStream_t s) {
 
 template <typename T, bool LAZY>
 static int dispatch_gemm(GemmArgs g, hipStream_t s) {
+  auto gemm_r_imgs = [&](int bm) {  // SE gate rows gemm_r stages per tile
+    return (LAZY && g.lz.gate) ? gemm_gate_imgs(bm, g.pyr.H[0] * g.pyr.W[0], g.pyr.batch) : 0;
+  };
   const int KP0 = cdiv(g.K, 32) * 32;
 #ifdef EDET_DEV
   // development slot 26: force a kernel family where it applies (1 = wave-streaming, 2 =
@@ -2117,9 +2171,9 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
       }
     }
     if (route == 3 && g.K <= 512) {
-      if (gemm_r_lds<T, 128, LAZY>(g.K, KP, LDCf) <= 96 * 1024) return launch_gemm_r<T, 128, LAZY>(g, s);
-      if (gemm_r_lds<T, 64, LAZY>(g.K, KP, LDCf) <= 96 * 1024) return launch_gemm_r<T, 64, LAZY>(g, s);
-      if (gemm_r_lds<T, 32, LAZY>(g.K, KP, LDCf) <= 96 * 1024) return launch_gemm_r<T, 32, LAZY>(g, s);
+      if (gemm_r_lds<T, 128, LAZY>(g.K, KP, LDCf, gemm_r_imgs(128)) <= 96 * 1024) return launch_gemm_r<T, 128, LAZY>(g, s);
+      if (gemm_r_lds<T, 64, LAZY>(g.K, KP, LDCf, gemm_r_imgs(64)) <= 96 * 1024) return launch_gemm_r<T, 64, LAZY>(g, s);
+      if (gemm_r_lds<T, 32, LAZY>(g.K, KP, LDCf, gemm_r_imgs(32)) <= 96 * 1024) return launch_gemm_r<T, 32, LAZY>(g, s);
     }
     if (route == 4) return dispatch_gemm_kloop<T, LAZY>(g, s);
   }
@@ -2153,10 +2207,10 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
     // the largest row tile that still gives >= 256 (row tile, column chunk) blocks: at M = 8192
     // the 128-row tiles left 64 blocks for 256 CUs (8192 x 320 -> 64: 21 us)
     const bool fills = (long)cdiv(g.M, 128) * cdiv(g.N, RNB) >= 256;  // (21 -> 19 us at 8192 x 320 -> 64)
-    if (!fills && gemm_r_lds<T, 32, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 32, LAZY>(g, s);
-    if (gemm_r_lds<T, 128, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 128, LAZY>(g, s);
-    if (gemm_r_lds<T, 64, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 64, LAZY>(g, s);
-    if (gemm_r_lds<T, 32, LAZY>(g.K, KP, LDCf) <= BUDGET) return launch_gemm_r<T, 32, LAZY>(g, s);
+    if (!fills && gemm_r_lds<T, 32, LAZY>(g.K, KP, LDCf, gemm_r_imgs(32)) <= BUDGET) return launch_gemm_r<T, 32, LAZY>(g, s);
+    if (gemm_r_lds<T, 128, LAZY>(g.K, KP, LDCf, gemm_r_imgs(128)) <= BUDGET) return launch_gemm_r<T, 128, LAZY>(g, s);
+    if (gemm_r_lds<T, 64, LAZY>(g.K, KP, LDCf, gemm_r_imgs(64)) <= BUDGET) return launch_gemm_r<T, 64, LAZY>(g, s);
+    if (gemm_r_lds<T, 32, LAZY>(g.K, KP, LDCf, gemm_r_imgs(32)) <= BUDGET) return launch_gemm_r<T, 32, LAZY>(g, s);
     // wider C tiles than fit: the column-split A-resident form walked its chunks one
     // dependent B load at a time with one block per CU (dgrad 8192 x 320 -> 1152: 88 us);
     // the pipelined K loop over 128-column tiles takes 31 us
