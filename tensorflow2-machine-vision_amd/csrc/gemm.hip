@@ -1741,14 +1741,10 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
       if (n < N && k < K) v = *reinterpret_cast<const uint4*>(Wt + (size_t)n * g.ldb + k);
       wf[ks][f] = __builtin_bit_cast(bf16x8_t, v);
     }
-  float bias[NF][4];
-#pragma unroll
-  for (int f = 0; f < NF; ++f)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = 16 * f + 4 * (lane >> 4) + r;
-      bias[f][r] = (g.bias && n < N) ? g.bias[n] : 0.f;
-    }
+  // bias in LDS (4 * NF registers per lane held it: at NF = 9 the difference between one and
+  // two waves per SIMD)
+  __shared__ __attribute__((aligned(16))) float bias_s[NF * 16];
+  for (int n = threadIdx.x; n < NF * 16; n += 256) bias_s[n] = (g.bias && n < N) ? g.bias[n] : 0.f;
   float2 af[KS][8];
   if constexpr (LAZY) {
     const float inv = 1.f / (float)M;
@@ -1789,7 +1785,7 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
         sq[f][r] = 0.f;
       }
   };
-  if (g.has_stats) __syncthreads();  // red zeroed before any wave flushes
+  __syncthreads();  // red zeroed before any wave flushes; bias table in place
   // each block owns a contiguous range of 16-row groups (its waves interleave inside it), so
   // a block meets one pyramid level, rarely two: per-wave flushes and the block's fp64
   // atomics cover only the levels it touched (a grid-strided wave met a new level about once
@@ -1885,10 +1881,12 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks][f], bfrag[ks], d, 0, 0, 0);
       const int n0 = 16 * f + 4 * (lane >> 4);
+      const float4 bv = *reinterpret_cast<const float4*>(&bias_s[n0]);
+      const float bias4[4] = {bv.x, bv.y, bv.z, bv.w};
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        v[r] = d[r] + bias[f][r];
+        v[r] = d[r] + bias4[r];
         if constexpr (FOLD) {
           const float xf_ = __uint_as_float(r & 1 ? ((r < 2 ? xcur[f].x : xcur[f].y) & 0xffff0000u)
                                                   : ((r < 2 ? xcur[f].x : xcur[f].y) << 16));

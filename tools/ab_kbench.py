@@ -40,10 +40,10 @@ def main():
     rows = sorted((new[0].get(k, 0.0) - old[0].get(k, 0.0), k, old[0].get(k, 0.0), new[0].get(k, 0.0))
                   for k in set(old[0]) | set(new[0]))
     print("most improved launches:")
-    for r in rows[:10]:
+    for r in rows[:15]:
         print(f"  {r[0]:+7.1f} {r[2]:7.1f} {r[3]:7.1f} {r[1]}")
     print("most regressed launches:")
-    for r in rows[-10:]:
+    for r in rows[-15:]:
         print(f"  {r[0]:+7.1f} {r[2]:7.1f} {r[3]:7.1f} {r[1]}")
 
 
