@@ -197,6 +197,11 @@ constexpr uint32_t BUF_OOB = 0x80000000u;
 __device__ __forceinline__ float gld(const float* p) {
   return *(const __attribute__((address_space(1))) float*)p;
 }
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 gld16(const void* p) {
+  const u32x4_t v = *(const __attribute__((address_space(1))) u32x4_t*)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, long bytes) {
   const uint32_t n = bytes <= 0 ? 0u : (bytes >= (long)BUF_OOB ? BUF_OOB : (uint32_t)bytes);
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, 0x00020000);
