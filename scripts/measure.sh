@@ -12,7 +12,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r03}
 O=gpurun_out/$TAG
-rm -rf $O && mkdir -p $O
+rm -rf $O/pmc_fetch $O/pmc_write $O/pmc_mfma $O/ktrace && mkdir -p $O
 BENCH="--steps ${STEPS:-20} --warmup ${WARMUP:-5}"
 EAGER="python bench.py --steps 3 --warmup 1 --graph 0 --cpu-baseline 0 --kernel-timing 0"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run --output-format csv \

@@ -35,7 +35,7 @@ for step in $STEPS; do
       timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.log
       rc=$?; tail -3 $O/bench.log; cut -c1-300 $O/bench.json; [ $rc -eq 0 ] || exit $rc ;;
     measure)
-      TAG=$TAG bash scripts/measure.sh > $O/measure.log 2>&1
+      env -u STEPS TAG=$TAG bash scripts/measure.sh > $O/measure.log 2>&1
       rc=$?; tail -8 $O/measure.log; [ $rc -eq 0 ] || exit $rc ;;
     configs)
       timeout -k 10 400 python bench.py --workload backbone --batch 64 --steps 20 --warmup 5 --cpu-baseline 0 \
