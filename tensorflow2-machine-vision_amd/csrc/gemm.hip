@@ -1703,6 +1703,21 @@ static int dispatch_pwb(const GemmArgs& g, hipStream_t s, bool& done) {
   return launch_pwb<T, 1, true, LAZY>(g, p, s);
 }
 
+// the B-resident plan without the per-shape preference above (round-4 routing rules)
+template <typename T, bool LAZY>
+static int dispatch_pwb_forced(const GemmArgs& g, hipStream_t s, bool& done) {
+  PwPlan p;
+  int FN;
+  bool ks;
+  done = false;
+  if (g.ldc % 8 != 0 || g.lda % 8 != 0 || g.K % 8 != 0) return EDET_OK;
+  if (g.M == 0 || !pw_plan(g, LAZY, sizeof(T), p, FN, ks)) return EDET_OK;
+  done = true;
+  if (!ks) return launch_pwb<T, 2, false, LAZY>(g, p, s);
+  if (FN == 2) return launch_pwb<T, 2, true, LAZY>(g, p, s);
+  return launch_pwb<T, 1, true, LAZY>(g, p, s);
+}
+
 // ------------------------------------------------------------------ wave-streaming small-K GEMM
 // For K <= 32 (the stage 0-1 convs: 2M x 16 -> 96, 524K x 24 -> 144, 2M x 32 -> 16) the
 // GEMM is a pure stream: the outputs are 3-6x the inputs.  Every wave works alone, with no
@@ -2176,6 +2191,28 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
     if (route == 4) return dispatch_gemm_kloop<T, LAZY>(g, s);
   }
 #endif
+  // Round-4 route sweep (development slot 26 over every D0 and D4 conv1x1 launch after the
+  // loaders were made countable, profiles/r04ad_route_sweep/): the K loop now wins the plain,
+  // statistics-free K = 224 products into N >= 192 (the D4 head / BiFPN dgrads and the class
+  // predict: 174592 x 224 -> 224 dgrad 87 -> 67 us, -> 729 fwd 254 -> 200 us) and a lazy A
+  // with K > 64 into 192 < N <= 320 (D4 32768 x 160 -> 224: 95 -> 59 us); the A-resident form
+  // wins K = 224 into N >= 192 with statistics at M <= 8192 (8192 x 224 -> 224: 33 -> 24 us);
+  // the B-resident form wins the D0 class predict (174592 x 64 -> 729: 114 -> 93 us)
+  if constexpr (sizeof(T) == 2) {
+    const int KPr = cdiv(g.K, 32) * 32;
+    const bool w224 = g.N >= 192 && KPr > 192 && KPr <= 224;
+    if (!LAZY && !g.has_stats && w224) return dispatch_gemm_kloop<T, LAZY>(g, s);
+    if (LAZY && g.K > 64 && g.N > 192 && g.N <= 320) return dispatch_gemm_kloop<T, LAZY>(g, s);
+    if (!LAZY && g.has_stats && w224 && g.M <= 8192 && g.K <= 512) {
+      const int LDCf = cdiv(g.N, 8) * 8;
+      if (gemm_r_lds<T, 32, LAZY>(g.K, KPr, LDCf, 0) <= 96 * 1024) return launch_gemm_r<T, 32, LAZY>(g, s);
+    }
+    if (!LAZY && !g.has_stats && g.K <= 64 && g.N > 640 && g.M >= 131072) {
+      bool done = false;
+      const int rc = dispatch_pwb_forced<T, LAZY>(g, s, done);
+      if (done || rc) return rc;
+    }
+  }
   {
     bool done = false;
     const int rc = dispatch_gemm_s<T, LAZY>(g, s, done);

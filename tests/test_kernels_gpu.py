@@ -42,7 +42,13 @@ def pyr_data(rng, pyr, C, dt, scale=1.0):
                                             # route rules of round 3: lazy K <= 64 into N <= 64 (wave
                                             # streaming), lazy K > 64 into N > 320 (K loop), plain without
                                             # statistics (K loop; the stats-free call is below)
-                                            (1000, 40, 64, 1, 1), (700, 80, 480, 3, 1)])
+                                            (1000, 40, 64, 1, 1), (700, 80, 480, 3, 1),
+                                            # route rules of round 4: lazy K > 64 into 192 < N <= 320
+                                            # (K loop), plain K = 224 into N >= 192 with statistics at
+                                            # M <= 8192 (A-resident; without them the K loop), the
+                                            # class predict's K = 64 into N = 729 over M >= 131072
+                                            # without statistics (B-resident)
+                                            (800, 160, 224, 3, 1), (800, 160, 224, 1, 1), (131072, 64, 729, 0, 1)])
 def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
     """conv1x1 forward with BN statistics (and without them for plain inputs: the stats-free
     route) against fp64."""
