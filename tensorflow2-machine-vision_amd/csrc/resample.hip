@@ -593,6 +593,121 @@ __global__ __launch_bounds__(256) void k_fuse_fwd(FuseArgs g) {
   }
 }
 
+// bf16 forward with the input modes compile-time (M0..M2: EDET_MODE_*, M2 = -1: two inputs): every
+// input's raw vectors of an output pixel are loaded before any is transformed, so a thread has
+// all its inputs' round trips in flight at once (the runtime mode loop loaded, waited for and
+// transformed one input at a time: three serial round trips per vector at a bottom-up node).
+// Same values, same order of the weighted sum, same pool taps as k_fuse_fwd.
+template <int M>
+struct FuseRaw {
+  uint4 r[M == EDET_MODE_MAXPOOL ? 9 : 1];
+  uint32_t ok;
+};
+template <int M>
+__device__ __forceinline__ void fuse_raw_load(FuseRaw<M>& s, const edet_fuse_input& fi, int n, int h, int w, int OH,
+                                              int OW, int c) {
+  const int Hi = fi.H, Wi = fi.W;
+  const uint16_t* X = (const uint16_t*)fi.v.x + (size_t)n * Hi * Wi * fi.v.ld + c;
+  if constexpr (M == EDET_MODE_SAME) {
+    s.r[0] = gld16(X + (size_t)(h * Wi + w) * fi.v.ld);
+  } else if constexpr (M == EDET_MODE_UPSAMPLE) {
+    const int iy = nearest_src(h, Hi, OH), ix = nearest_src(w, Wi, OW);
+    s.r[0] = gld16(X + (size_t)(iy * Wi + ix) * fi.v.ld);
+  } else if constexpr (M == EDET_MODE_MAXPOOL) {
+    const int y0 = h * 2 - same_pad(Hi, 3, 2), x0 = w * 2 - same_pad(Wi, 3, 2);
+    s.ok = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int iy = y0 + k / 3, ix = x0 + k % 3;
+      const bool in = iy >= 0 && iy < Hi && ix >= 0 && ix < Wi;
+      s.r[k] = gld16(X + (in ? (size_t)(iy * Wi + ix) * fi.v.ld : 0));
+      s.ok |= (uint32_t)in << k;
+    }
+  }
+}
+__device__ __forceinline__ void unpack_bf8(const uint4& q, float* o) {
+  const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(w4[i] << 16);
+    o[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
+  }
+}
+template <int M>
+__device__ __forceinline__ void fuse_raw_value(const FuseRaw<M>& s, const edet_fuse_input& fi, const float2* af,
+                                               size_t pix, int C, int c, float* v) {
+  if constexpr (M == EDET_MODE_MAXPOOL) {
+    float best[8];
+    int arg[8], tk[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -FLT_MAX; arg[j] = -1; tk[j] = 0; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      if (!((s.ok >> k) & 1)) continue;
+      float x[8];
+      unpack_bf8(s.r[k], x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float t = lazy_apply(x[j], af[j], fi.v.act);
+        if (arg[j] < 0 || t > best[j]) { best[j] = t; arg[j] = k; tk[j] = k; }
+      }
+    }
+    if (fi.pool_arg) store_taps(fi.pool_arg + pix * C + c, tk);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = best[j];
+  } else {
+    float x[8];
+    unpack_bf8(s.r[0], x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = lazy_apply(x[j], af[j], fi.v.act);
+  }
+}
+template <int M0, int M1, int M2>
+__global__ __launch_bounds__(256) void k_fuse_fwd_m(FuseArgs g) {
+  using T = uint16_t;
+  extern __shared__ float2 aft[];  // [n_in][C]
+  constexpr int NIN = 2 + (M2 >= 0);
+  for (int i = 0; i < NIN; ++i)
+    load_affine(g.in[i].v, g.C, 1.f / (float)(g.B * g.in[i].H * g.in[i].W), aft + i * g.C);
+  __syncthreads();
+  const int nv = g.C / 8;
+  const long total = (long)g.B * g.H * g.W * nv;
+  const float den = fuse_denom(g.w, NIN);
+  float wn[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) wn[i] = i < NIN ? g.w[i] / den : 0.f;  // one division per input
+  for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const int cv = (int)(idx % nv);
+    const long pix = idx / nv;
+    const int n = (int)(pix / ((long)g.H * g.W));
+    const int rem = (int)(pix - (long)n * g.H * g.W);
+    const int h = rem / g.W, w = rem - h * g.W;
+    FuseRaw<M0> r0;
+    FuseRaw<M1> r1;
+    FuseRaw<M2 >= 0 ? M2 : EDET_MODE_SAME> r2;
+    fuse_raw_load<M0>(r0, g.in[0], n, h, w, g.H, g.W, cv * 8);
+    fuse_raw_load<M1>(r1, g.in[1], n, h, w, g.H, g.W, cv * 8);
+    if constexpr (M2 >= 0) fuse_raw_load<M2>(r2, g.in[2], n, h, w, g.H, g.W, cv * 8);
+    float o[8], v[8];
+    float2 af[8];
+    affine8_lds(aft, cv * 8, af);
+    fuse_raw_value<M0>(r0, g.in[0], af, (size_t)pix, g.C, cv * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = v[j] * wn[0];
+    affine8_lds(aft + g.C, cv * 8, af);
+    fuse_raw_value<M1>(r1, g.in[1], af, (size_t)pix, g.C, cv * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = o[j] + v[j] * wn[1];
+    if constexpr (M2 >= 0) {
+      affine8_lds(aft + 2 * g.C, cv * 8, af);
+      fuse_raw_value<M2>(r2, g.in[2], af, (size_t)pix, g.C, cv * 8, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = o[j] + v[j] * wn[2];
+    }
+    st8((T*)g.out + (size_t)pix * g.C + cv * 8, o);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_fuse_bwd(FuseArgs g) {
   __shared__ float red[3][4];
@@ -825,6 +940,22 @@ int edet_bifpn_fuse_fwd(int dtype, int n_in, const edet_fuse_input* ins, const f
   // Development slot 28 overrides the cap.
   const int cap = dev_knob(28) > 0 ? dev_knob(28) : 2048;
   if (nb > cap) nb = cap;
+  // the BiFPN's input-mode combinations as compile-time forms (bf16; development slot 34 = 2:
+  // the runtime-mode kernel)
+  if (dtype == EDET_BF16 && nb && dev_knob(34) != 2) {
+    const size_t lds = n_in * C * sizeof(float2);
+    const int m0 = ins[0].mode, m1 = ins[1].mode, m2 = n_in == 3 ? ins[2].mode : -1;
+    constexpr int S_ = EDET_MODE_SAME, U_ = EDET_MODE_UPSAMPLE, P_ = EDET_MODE_MAXPOOL;
+    hipStream_t st = (hipStream_t)stream;
+    bool hit = true;
+    if (m0 == S_ && m1 == U_ && m2 == -1) EDET_LAUNCH((k_fuse_fwd_m<S_, U_, -1>), dim3(nb), dim3(256), lds, st, g);
+    else if (m0 == S_ && m1 == S_ && m2 == P_) EDET_LAUNCH((k_fuse_fwd_m<S_, S_, P_>), dim3(nb), dim3(256), lds, st, g);
+    else if (m0 == S_ && m1 == P_ && m2 == -1) EDET_LAUNCH((k_fuse_fwd_m<S_, P_, -1>), dim3(nb), dim3(256), lds, st, g);
+    else if (m0 == S_ && m1 == S_ && m2 == U_) EDET_LAUNCH((k_fuse_fwd_m<S_, S_, U_>), dim3(nb), dim3(256), lds, st, g);
+    else if (m0 == S_ && m1 == S_ && m2 == -1) EDET_LAUNCH((k_fuse_fwd_m<S_, S_, -1>), dim3(nb), dim3(256), lds, st, g);
+    else hit = false;
+    if (hit) return check_launch("edet bifpn_fuse_fwd");
+  }
   EDET_DTYPE_DISPATCH(dtype, T, {
     if (nb) EDET_LAUNCH(k_fuse_fwd<T>, dim3(nb), dim3(256), n_in * C * sizeof(float2), (hipStream_t)stream, g);
     return check_launch("edet bifpn_fuse_fwd");
