@@ -708,6 +708,122 @@ __global__ __launch_bounds__(256) void k_fuse_fwd_m(FuseArgs g) {
   }
 }
 
+// the dx blocks of the fusion backward (input i's pixels: b counts from the first dx block)
+template <typename T>
+__device__ __forceinline__ void fuse_bwd_dx(const FuseArgs& g, const float2* aft, int b) {
+  const int tid = threadIdx.x;
+  const int nv = g.C / 8;
+  const float den = fuse_denom(g.w, g.n_in);
+  int i = 0;
+  for (; i < g.n_in - 1; ++i) {
+    if (b < g.nb_in[i]) break;
+    b -= g.nb_in[i];
+  }
+  const edet_fuse_input& fi = g.in[i];
+  const int Hi = fi.H, Wi = fi.W;
+  const long idx = (long)b * 256 + tid;
+  if (idx >= (long)g.B * Hi * Wi * nv) return;
+  const int cv = (int)(idx % nv);
+  const long pix = idx / nv;
+  const int n = (int)(pix / ((long)Hi * Wi));
+  const int rem = (int)(pix - (long)n * Hi * Wi);
+  const int iy = rem / Wi, ix = rem - iy * Wi;
+  const float wn = g.w[i] / den;
+  const T* dF = (const T*)g.dout;
+  const size_t o0 = (size_t)n * g.H * g.W;
+  float d[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] = 0.f;
+  if (fi.mode == EDET_MODE_SAME) {
+    float v[8];
+    ld8(dF + (o0 + (size_t)iy * g.W + ix) * g.C + cv * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = v[j] * wn;
+  } else if (fi.mode == EDET_MODE_UPSAMPLE && g.H == 2 * Hi && g.W == 2 * Wi) {
+    // exact x2 (the BiFPN's): input (iy, ix) is the nearest source of output rows 2iy, 2iy+1 and
+    // columns 2ix, 2ix+1 -- four loads at once (the window walk below waited for each in turn)
+    uint4 q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      q[k] = gld16(dF + (o0 + (size_t)(2 * iy + (k >> 1)) * g.W + 2 * ix + (k & 1)) * g.C + cv * 8);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float v[8];
+      if constexpr (sizeof(T) == 2) {
+        const uint32_t w4[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] = __uint_as_float(w4[e] << 16);
+          v[2 * e + 1] = __uint_as_float(w4[e] & 0xffff0000u);
+        }
+      } else {
+        ld8(dF + (o0 + (size_t)(2 * iy + (k >> 1)) * g.W + 2 * ix + (k & 1)) * g.C + cv * 8, v);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] += v[j] * wn;
+    }
+  } else if (fi.mode == EDET_MODE_UPSAMPLE) {
+    // output rows h with nearest_src(h) == iy lie in [iy*OH/Hi - 1, (iy+1)*OH/Hi + 1]
+    const int h_lo = max(0, (int)((long)iy * g.H / Hi) - 1), h_hi = min(g.H - 1, (int)((long)(iy + 1) * g.H / Hi) + 1);
+    const int w_lo = max(0, (int)((long)ix * g.W / Wi) - 1), w_hi = min(g.W - 1, (int)((long)(ix + 1) * g.W / Wi) + 1);
+    for (int h = h_lo; h <= h_hi; ++h) {
+      if (nearest_src(h, Hi, g.H) != iy) continue;
+      for (int w = w_lo; w <= w_hi; ++w) {
+        if (nearest_src(w, Wi, g.W) != ix) continue;
+        float v[8];
+        ld8(dF + (o0 + (size_t)h * g.W + w) * g.C + cv * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] += v[j] * wn;
+      }
+    }
+  } else if (fi.pool_arg) {
+    // max-pooled input with the forward's taps: the (at most 2 x 2) outputs whose window holds
+    // this pixel, their taps and dF loaded at once (pool_bwd_gather's loops waited for each)
+    const int pt = same_pad(Hi, 3, 2), pl = same_pad(Wi, 3, 2);
+    const int oy_lo = max(0, fdiv(iy + pt - 1, 2)), oy_hi = min(g.H - 1, fdiv(iy + pt, 2));
+    const int ox_lo = max(0, fdiv(ix + pl - 1, 2)), ox_hi = min(g.W - 1, fdiv(ix + pl, 2));
+    uint2 tq[4];
+    uint4 dq[4];
+    bool okk[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int oy = oy_lo + (k >> 1), ox = ox_lo + (k & 1);
+      okk[k] = oy <= oy_hi && ox <= ox_hi;
+      const size_t o = o0 + (okk[k] ? (size_t)oy * g.W + ox : 0);
+      tq[k] = *reinterpret_cast<const uint2*>(fi.pool_arg + o * g.C + cv * 8);
+      dq[k] = gld16(dF + o * g.C + cv * 8);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (!okk[k]) continue;
+      const int oy = oy_lo + (k >> 1), ox = ox_lo + (k & 1);
+      const int kme = (iy - (oy * 2 - pt)) * 3 + (ix - (ox * 2 - pl));
+      float gv[8];
+      if constexpr (sizeof(T) == 2) {
+        const uint32_t w4[4] = {dq[k].x, dq[k].y, dq[k].z, dq[k].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          gv[2 * e] = __uint_as_float(w4[e] << 16);
+          gv[2 * e + 1] = __uint_as_float(w4[e] & 0xffff0000u);
+        }
+      } else {
+        ld8(dF + (o0 + (size_t)oy * g.W + ox) * g.C + cv * 8, gv);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int tap = (int)(((j < 4 ? tq[k].x : tq[k].y) >> (8 * (j & 3))) & 0xffu);
+        if (tap == kme) d[j] += gv[j] * wn;
+      }
+    }
+  } else {
+    float2 af[8];
+    affine8_lds(aft + i * g.C, cv * 8, af);
+    pool_bwd_gather<T>(fi.v, af, dF, (size_t)n * Hi * Wi, o0, Hi, Wi, g.H, g.W, g.C, iy, ix, cv * 8, wn, d,
+                       fi.pool_arg);
+  }
+  acc8m((T*)fi.dx + (size_t)pix * g.C + cv * 8, 8, d, fi.accumulate);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_fuse_bwd(FuseArgs g) {
   __shared__ float red[3][4];
@@ -755,53 +871,79 @@ __global__ __launch_bounds__(256) void k_fuse_bwd(FuseArgs g) {
     if (tid < g.n_in) atomicAdd(g.dw + tid, red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3]);
     return;
   }
-  b -= g.nb_w;
-  int i = 0;
-  for (; i < g.n_in - 1; ++i) {
-    if (b < g.nb_in[i]) break;
-    b -= g.nb_in[i];
+  fuse_bwd_dx<T>(g, aft, b - g.nb_w);
+}
+
+// bf16 backward with compile-time input modes: the weight-gradient blocks load F, dF and every
+// input's raw vectors of a pixel before any use (the runtime loop waited for each input in turn:
+// with a bounded grid of long-lived blocks those serial round trips were the launch's tail, D4
+// 130-138 us per call); a max-pooled input recomputes its 3x3 window (nine loads at once)
+// instead of chaining a tap load and the tap-indexed rows.  The dx blocks are k_fuse_bwd's.
+template <int M0, int M1, int M2>
+__global__ __launch_bounds__(256) void k_fuse_bwd_m(FuseArgs g) {
+  using T = uint16_t;
+  __shared__ float red[3][4];
+  extern __shared__ float2 aft[];  // [n_in][C]
+  constexpr int NIN = 2 + (M2 >= 0);
+  for (int i = 0; i < NIN; ++i)
+    load_affine(g.in[i].v, g.C, 1.f / (float)(g.B * g.in[i].H * g.in[i].W), aft + i * g.C);
+  __syncthreads();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nv = g.C / 8;
+  const float den = fuse_denom(g.w, NIN);
+  const int b = blockIdx.x;
+  if (b >= g.nb_w) {
+    fuse_bwd_dx<T>(g, aft, b - g.nb_w);
+    return;
   }
-  const edet_fuse_input& fi = g.in[i];
-  const int Hi = fi.H, Wi = fi.W;
-  const long idx = (long)b * 256 + tid;
-  if (idx >= (long)g.B * Hi * Wi * nv) return;
-  const int cv = (int)(idx % nv);
-  const long pix = idx / nv;
-  const int n = (int)(pix / ((long)Hi * Wi));
-  const int rem = (int)(pix - (long)n * Hi * Wi);
-  const int iy = rem / Wi, ix = rem - iy * Wi;
-  const float wn = g.w[i] / den;
-  const T* dF = (const T*)g.dout;
-  const size_t o0 = (size_t)n * g.H * g.W;
-  float d[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) d[j] = 0.f;
-  if (fi.mode == EDET_MODE_SAME) {
-    float v[8];
-    ld8(dF + (o0 + (size_t)iy * g.W + ix) * g.C + cv * 8, v);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = v[j] * wn;
-  } else if (fi.mode == EDET_MODE_UPSAMPLE) {
-    // output rows h with nearest_src(h) == iy lie in [iy*OH/Hi - 1, (iy+1)*OH/Hi + 1]
-    const int h_lo = max(0, (int)((long)iy * g.H / Hi) - 1), h_hi = min(g.H - 1, (int)((long)(iy + 1) * g.H / Hi) + 1);
-    const int w_lo = max(0, (int)((long)ix * g.W / Wi) - 1), w_hi = min(g.W - 1, (int)((long)(ix + 1) * g.W / Wi) + 1);
-    for (int h = h_lo; h <= h_hi; ++h) {
-      if (nearest_src(h, Hi, g.H) != iy) continue;
-      for (int w = w_lo; w <= w_hi; ++w) {
-        if (nearest_src(w, Wi, g.W) != ix) continue;
-        float v[8];
-        ld8(dF + (o0 + (size_t)h * g.W + w) * g.C + cv * 8, v);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] += v[j] * wn;
-      }
-    }
-  } else {
+  float part[3] = {0.f, 0.f, 0.f};
+  const float rden = 1.f / den;
+  const long total = (long)g.B * g.H * g.W * nv;
+  for (long idx = (long)b * 256 + tid; idx < total; idx += (long)g.nb_w * 256) {
+    const int cv = (int)(idx % nv);
+    const long pix = idx / nv;
+    const int n = (int)(pix / ((long)g.H * g.W));
+    const int rem = (int)(pix - (long)n * g.H * g.W);
+    const int h = rem / g.W, w = rem - h * g.W;
+    const uint4 fr = gld16((const T*)g.fused + (size_t)pix * g.C + cv * 8);
+    const uint4 dr = gld16((const T*)g.dout + (size_t)pix * g.C + cv * 8);
+    FuseRaw<M0> r0;
+    FuseRaw<M1> r1;
+    FuseRaw<M2 >= 0 ? M2 : EDET_MODE_SAME> r2;
+    fuse_raw_load<M0>(r0, g.in[0], n, h, w, g.H, g.W, cv * 8);
+    fuse_raw_load<M1>(r1, g.in[1], n, h, w, g.H, g.W, cv * 8);
+    if constexpr (M2 >= 0) fuse_raw_load<M2>(r2, g.in[2], n, h, w, g.H, g.W, cv * 8);
+    float F[8], dF[8], v[8];
+    unpack_bf8(fr, F);
+    unpack_bf8(dr, dF);
     float2 af[8];
-    affine8_lds(aft + i * g.C, cv * 8, af);
-    pool_bwd_gather<T>(fi.v, af, dF, (size_t)n * Hi * Wi, o0, Hi, Wi, g.H, g.W, g.C, iy, ix, cv * 8, wn, d,
-                       fi.pool_arg);
+    auto acc = [&](int i) {
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t += dF[j] * (v[j] - F[j]);
+      part[i] += t * rden;
+    };
+    // (the pool taps are not stored from here: pool_arg belongs to the forward)
+    edet_fuse_input f0 = g.in[0], f1 = g.in[1], f2 = g.in[NIN - 1];
+    f0.pool_arg = nullptr; f1.pool_arg = nullptr; f2.pool_arg = nullptr;
+    affine8_lds(aft, cv * 8, af);
+    fuse_raw_value<M0>(r0, f0, af, (size_t)pix, g.C, cv * 8, v);
+    acc(0);
+    affine8_lds(aft + g.C, cv * 8, af);
+    fuse_raw_value<M1>(r1, f1, af, (size_t)pix, g.C, cv * 8, v);
+    acc(1);
+    if constexpr (M2 >= 0) {
+      affine8_lds(aft + 2 * g.C, cv * 8, af);
+      fuse_raw_value<M2>(r2, f2, af, (size_t)pix, g.C, cv * 8, v);
+      acc(2);
+    }
   }
-  acc8m((T*)fi.dx + (size_t)pix * g.C + cv * 8, 8, d, fi.accumulate);
+  for (int i = 0; i < NIN; ++i) {
+    const float s = wave_sum(part[i]);
+    if (lane == 0) red[i][wave] = s;
+  }
+  __syncthreads();
+  if (tid < NIN) atomicAdd(g.dw + tid, red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3]);
 }
 
 }  // namespace edet
@@ -976,6 +1118,20 @@ int edet_bifpn_fuse_bwd(int dtype, int n_in, const edet_fuse_input* ins, const f
   for (int i = 0; i < n_in; ++i) {
     g.nb_in[i] = (int)(((long)B * ins[i].H * ins[i].W * (C / 8) + 255) / 256);
     nb += g.nb_in[i];
+  }
+  if (dtype == EDET_BF16 && nb && dev_knob(34) != 2) {
+    const size_t lds = n_in * C * sizeof(float2);
+    const int m0 = ins[0].mode, m1 = ins[1].mode, m2 = n_in == 3 ? ins[2].mode : -1;
+    constexpr int S_ = EDET_MODE_SAME, U_ = EDET_MODE_UPSAMPLE, P_ = EDET_MODE_MAXPOOL;
+    hipStream_t st = (hipStream_t)stream;
+    bool hit = true;
+    if (m0 == S_ && m1 == U_ && m2 == -1) EDET_LAUNCH((k_fuse_bwd_m<S_, U_, -1>), dim3(nb), dim3(256), lds, st, g);
+    else if (m0 == S_ && m1 == S_ && m2 == P_) EDET_LAUNCH((k_fuse_bwd_m<S_, S_, P_>), dim3(nb), dim3(256), lds, st, g);
+    else if (m0 == S_ && m1 == P_ && m2 == -1) EDET_LAUNCH((k_fuse_bwd_m<S_, P_, -1>), dim3(nb), dim3(256), lds, st, g);
+    else if (m0 == S_ && m1 == S_ && m2 == U_) EDET_LAUNCH((k_fuse_bwd_m<S_, S_, U_>), dim3(nb), dim3(256), lds, st, g);
+    else if (m0 == S_ && m1 == S_ && m2 == -1) EDET_LAUNCH((k_fuse_bwd_m<S_, S_, -1>), dim3(nb), dim3(256), lds, st, g);
+    else hit = false;
+    if (hit) return check_launch("edet bifpn_fuse_bwd");
   }
   EDET_DTYPE_DISPATCH(dtype, T, {
     if (nb) EDET_LAUNCH(k_fuse_bwd<T>, dim3(nb), dim3(256), n_in * C * sizeof(float2), (hipStream_t)stream, g);
