@@ -2217,7 +2217,9 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
           }
         }
       }
-      // (no per-row pinning of the window or the taps: the SLP vectorizer then gathers the whole
+      // (dx as v_pk_fma_f32 column pairs: the odd-aligned dy pairs need copies, 247 -> 300
+      // registers at k5 fold (occupancy 2 -> 1), 155 -> 176 at k3 fold (3 -> 2); not kept.
+      // No per-row pinning of the window or the taps: the SLP vectorizer then gathers the whole
       // filter gradient into v_pk_fma_f32 after the last row -- the full v window in registers,
       // ~210-250 VGPRs at k5, but half the FMA instructions; pinned rows with scalar FMAs held
       // 140 VGPRs and ran 5-10 % slower at k5, even at k3: tools/dwt_ab.py r04e-r04g)
@@ -2236,12 +2238,12 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
         const T sv = from_f<T>(dxa[e][f]);
         sb[po] = sv;
         if constexpr (FOLD) {  // BN-backward sums of x's BatchNorm from the stored dx
-          if (y0 + a0 + e < H && x0 + b0 + f < W) {
-            const float yv = to_f<T>(sv), xv = to_f<T>(xb[po]);
-            const float du = act ? yv * dswishf_(xv * ft.x + ft.y) : yv;
-            fs += du;
-            fq += du * ((xv - ft.z) * ft.w);
-          }
+          // branch-free: pixels past the plane edge (stale LDS) are selected out, not skipped
+          const bool in = y0 + a0 + e < H && x0 + b0 + f < W;
+          const float yv = to_f<T>(sv), xv = to_f<T>(xb[po]);
+          const float du = act ? yv * dswishf_(xv * ft.x + ft.y) : yv;
+          fs += in ? du : 0.f;
+          fq += in ? du * ((xv - ft.z) * ft.w) : 0.f;
           asm volatile("" : "+v"(fs), "+v"(fq));  // pixel by pixel (no batched transcendentals)
         }
       }
