@@ -550,6 +550,27 @@ def test_maxpool(dt, H, W):
         close(dx.double().cpu().sum(0), v.grad.sum(0), dt, scale=8)
 
 
+@pytest.mark.parametrize("H,W", [(16, 16), (9, 7), (8, 8), (4, 4), (3, 5)])
+def test_maxpool_bwd_bf16_exact(H, W):
+    """bf16 max-pool backward (the 5 x 5 neighbourhood gather) routes every dy to its window's
+    argmax exactly: per-channel distinct integer inputs (no ties) and integer dy, so the expected
+    dx is exact in bf16 (resample_feature_map.py's max_pooling2d, SAME padding)."""
+    rng = np.random.default_rng(7 * H + W)
+    B, C = 2, 64
+    pyr = Pyr(B, [(H, W)])
+    xn = np.stack([np.stack([rng.permutation(H * W) for _ in range(C)], axis=1) for _ in range(B)])
+    x = torch.tensor(xn.reshape(B * H * W, C), dtype=torch.bfloat16, device=DEV)
+    lz = LazyDesc(x, pyr, C)
+    OH, OW = (H + 1) // 2, (W + 1) // 2
+    dy = torch.tensor(rng.integers(-4, 5, (B * OH * OW, C)), dtype=torch.bfloat16, device=DEV)
+    dx = torch.empty(B * H * W, C, dtype=torch.bfloat16, device=DEV)
+    L.call("edet_maxpool_bwd", DT["bf16"], lz.c, B, H, W, C, vp(dy), vp(dx), 0, stream())
+    v = torch.tensor(xn.reshape(B * H * W, C), dtype=torch.float64).requires_grad_(True)
+    (maxpool_ref(v, B, H, W, C) * dy.double().cpu()).sum().backward()
+    torch.cuda.synchronize()
+    assert torch.equal(dx.double().cpu(), v.grad)
+
+
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("B,H,W", [(2, 8, 8), (4, 136, 136)])  # the second exceeds the forward's 2048-block grid
 def test_bifpn_fuse(dt, B, H, W):
