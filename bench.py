@@ -642,6 +642,7 @@ def main():
     value = world * B * args.steps / el
     # global-batch loss: the replicas' data terms sum to it (Multi-GPU); each
     # replica's scalars[0] also holds the (identical) L2 term once
+    scal_timed = model.scalars.cpu()  # the last timed step's scalars (rank 0's instrumentation reruns them)
     lt = model.scalars[0:1].clone()
     if ar is not None:
         ar(lt)
@@ -699,6 +700,14 @@ def main():
             "kernels": kernels,
         }
         print(json.dumps(out), flush=True)
+    dump = os.environ.get("EDET_BENCH_DUMP")
+    if dump:
+        # test hook (tests/test_bench_dp_gpu.py): every rank's optimizer-visible state after the
+        # run, so replicas can be compared bit for bit (rank 0 after its instrumentation restore)
+        P = model.P
+        torch.save({"w": P.w.cpu(), "v": P.v.cpu(), "ema": P.ema.cpu(), "step": model.step_counter.cpu(),
+                    "scalars": scal_timed, "l2_term": l2, "loss": loss, "value": value, "world": world},
+                   os.path.join(dump, f"rank{rank}.pt"))
     dp.shutdown(ctx)
 
 

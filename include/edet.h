@@ -104,6 +104,24 @@ typedef struct edet_bngrad64 {
   double* dbeta[EDET_MAX_SEG];
 } edet_bngrad64;
 
+/* The gradient of a lazy value's RAW tensor left unmaterialised (ABI 8): its consumer computes
+ *   d(raw y) = sc*du + kb*y + kc,  du = (dv * gate[n][c] + dsq[n][c]) * act'(bn(y))
+ * (kb, kc from acc: edet_lazy_bwd_apply's formula, element for element) while it loads it, so
+ * the apply pass over (dv, y) and the write + re-read of d(raw y) disappear.
+ *   dv   : d(value) [rows][C] in the storage dtype (the value's own row layout)
+ *   y    : the value's descriptor (raw y, training BN statistics, act, SE gate or null)
+ *   dsq  : [batch][C] SE squeeze-path gradient (edet_se_bwd*), nullable
+ *   acc  : the final fp64 (dgamma, dbeta) sums of y's BatchNorm (y.bn.enabled)
+ *   grads: fp32 gamma / beta parameter gradients, += (float)acc once by the consumer (a[s] null:
+ *          not written) */
+typedef struct edet_dgrad_lazy {
+  const void* dv;
+  edet_lazy y;
+  const float* dsq;
+  edet_bngrad64 acc;
+  edet_segout grads;
+} edet_dgrad_lazy;
+
 /* per-segment fp64 BN statistics outputs of a producer: sum and sum of squares */
 typedef struct edet_statout {
   double* sum[EDET_MAX_SEG];
@@ -242,6 +260,15 @@ int edet_dwconv_bwd(int dtype, const edet_lazy* x, const edet_pyramid* pin, int 
                     int stride, const void* dy, const edet_pyramid* pout, const void* w,
                     void* dx, int accumulate, float* dw, const edet_bngrad64* fold,
                     edet_stream_t stream);
+/* edet_dwconv_bwd with dy given lazily (ABI 8): dy = d(raw y) of the edet_dgrad_lazy `dyl`
+ * (the SE-gated swish(BN) depthwise output's gradient of an MBConv block, mb_conv_block.py:
+ * 147-150 with se.py:35-39), built while the dy window is loaded, rounded to the storage dtype
+ * as edet_lazy_bwd_apply would store it.  Also writes dyl->grads (y's gamma / beta gradients).
+ * Stride 1, C % 16 == 0, dyl->y.ld == C; same results as edet_lazy_bwd_apply + edet_dwconv_bwd. */
+int edet_dwconv_bwd_lazy(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
+                         const edet_dgrad_lazy* dyl, const edet_pyramid* pout, const void* w,
+                         void* dx, int accumulate, float* dw, const edet_bngrad64* fold,
+                         edet_stream_t stream);
 
 /* ---- squeeze-excitation ---- */
 /* s += mean_hw v(x) into a zeroed fp64 [B][C] (fp64 cross-block sums: the squeeze feeds the
@@ -364,8 +391,12 @@ int edet_transpose_cast(int dtype, const float* src, void* dst, const int64_t* t
 /* inference-mode BN: express moving mean/var as the sums the lazy loaders expect */
 int edet_bn_inference_stats(int64_t n, const float* mmean, const float* mvar, const float* count,
                             double* sum, double* sq, edet_stream_t stream);
+/* Keras moving statistics from the step's batch sums.  `skip` (nullable, device): the
+ * optimizer's scalars[6]; when it is non-zero (edet_opt_apply skipped a non-finite step) the
+ * moving statistics are left unchanged (ABI 8). */
 int edet_bn_update_moving(int64_t n, const double* sum, const double* sq, const float* count,
-                          float momentum, float* mmean, float* mvar, edet_stream_t stream);
+                          float momentum, const float* skip, float* mmean, float* mvar,
+                          edet_stream_t stream);
 int edet_dropmask(float* out, int n, float survival, uint64_t seed, const int32_t* step,
                   edet_stream_t stream);
 

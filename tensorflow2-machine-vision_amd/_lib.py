@@ -15,7 +15,7 @@ import torch  # noqa: F401
 from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
 
 MAX_SEG = 5
-ABI_VERSION = 7  # must equal edet_abi_version() of the loaded library (struct layouts)
+ABI_VERSION = 8  # must equal edet_abi_version() of the loaded library (struct layouts)
 OPT_NORM_BLOCKS = 256  # EDET_OPT_NORM_BLOCKS: edet_opt_norm partial-sum slots per quantity
 F32, BF16 = 0, 1
 ACT_NONE, ACT_SWISH = 0, 1
@@ -56,6 +56,11 @@ class BnGrad64(ctypes.Structure):
     _fields_ = [("dgamma", c_void_p * MAX_SEG), ("dbeta", c_void_p * MAX_SEG)]
 
 
+class DgradLazy(ctypes.Structure):
+    """edet_dgrad_lazy: d(raw y) of a lazy value, built by its consumer on load (ABI 8)."""
+    _fields_ = [("dv", c_void_p), ("y", Lazy), ("dsq", c_void_p), ("acc", BnGrad64), ("grads", SegOut)]
+
+
 class FuseInput(ctypes.Structure):
     _fields_ = [("v", Lazy), ("dx", c_void_p), ("H", c_int32), ("W", c_int32),
                 ("mode", c_int32), ("accumulate", c_int32), ("pool_arg", c_void_p)]
@@ -71,6 +76,7 @@ class Sched(ctypes.Structure):
 P = c_void_p
 PPyr, PLazy, PSeg, PStat, PBnG, PFuse, PSched = (POINTER(Pyramid), POINTER(Lazy), POINTER(SegOut), POINTER(StatOut),
                                                  POINTER(BnGrad64), POINTER(FuseInput), POINTER(Sched))
+PDgl = POINTER(DgradLazy)
 
 # name -> argtypes (all return int unless listed in _RESTYPE)
 SIGNATURES = {
@@ -92,6 +98,7 @@ SIGNATURES = {
     "edet_dwconv_dgrad_fold": [c_int, P, PPyr, c_int, c_int, c_int, P, P, PPyr, PLazy, PBnG, P],
     "edet_dwconv_wgrad": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, PPyr, P, P],
     "edet_dwconv_bwd": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, PPyr, P, P, c_int, P, PBnG, P],
+    "edet_dwconv_bwd_lazy": [c_int, PLazy, PPyr, c_int, c_int, PDgl, PPyr, P, P, c_int, P, PBnG, P],
     "edet_dwconv_fwd_squeeze": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, P, PPyr, PLazy, P, P],
     "edet_stem_fwd": [c_int, P, c_int, c_int, c_int, P, c_int, P, P, P, P],
     "edet_stem_wgrad": [c_int, P, c_int, c_int, c_int, P, c_int, P, P],
@@ -123,7 +130,7 @@ SIGNATURES = {
     "edet_cast_f32": [c_int, P, P, c_int64, P],
     "edet_transpose_cast": [c_int, P, P, P, c_int, c_int, P],
     "edet_bn_inference_stats": [c_int64, P, P, P, P, P, P],
-    "edet_bn_update_moving": [c_int64, P, P, P, c_float, P, P, P],
+    "edet_bn_update_moving": [c_int64, P, P, P, c_float, P, P, P, P],
     "edet_dropmask": [P, c_int, c_float, c_uint64, P, P],
 }
 _RESTYPE = {"edet_last_error": c_char_p}

@@ -720,10 +720,14 @@ __global__ __launch_bounds__(256) void k_materialize(LArgs g) {
 
 // Keras BatchNormalization moving statistics: m -= (m - batch) * (1 - momentum), with the
 // Bessel-corrected batch variance that FusedBatchNormV3 returns in training mode.
+// `skip` (nullable): edet_opt_apply's scalars[6]; a step the optimizer skipped as non-finite
+// (sched.skip_nonfinite) leaves the moving statistics unchanged too (its batch statistics
+// are as suspect as its gradient)
 __global__ void k_bn_update(int64_t n, const double* sum, const double* sq, const float* count,
-                            float momentum, float* mmean, float* mvar) {
+                            float momentum, const float* skip, float* mmean, float* mvar) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (skip && *skip != 0.f) return;
   const double cnt = count[i];
   const double mean = sum[i] / cnt;
   const double var = fmax(sq[i] / cnt - mean * mean, 0.0);
@@ -998,11 +1002,12 @@ int edet_bn_inference_stats(int64_t n, const float* mmean, const float* mvar, co
 }
 
 int edet_bn_update_moving(int64_t n, const double* sum, const double* sq, const float* count,
-                          float momentum, float* mmean, float* mvar, edet_stream_t stream) {
+                          float momentum, const float* skip, float* mmean, float* mvar,
+                          edet_stream_t stream) {
   EDET_REQUIRE(sum && sq && count && mmean && mvar, "bn_update_moving: null argument");
   if (n <= 0) return EDET_OK;
   EDET_LAUNCH(k_bn_update, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     n, sum, sq, count, momentum, mmean, mvar);
+                     n, sum, sq, count, momentum, skip, mmean, mvar);
   return check_launch("edet bn_update_moving");
 }
 

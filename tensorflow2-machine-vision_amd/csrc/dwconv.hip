@@ -32,6 +32,7 @@ struct DwArgs {
   float* part;  // wgrad: per-chunk partials [chunks][K*K][C] (null: atomics)
   edet_lazy yv;  // fwd + squeeze: the output's own lazy transform (inference BN, act)
   double* sq;    // fwd + squeeze: [batch][C] += mean_hw v(y)  (null: no squeeze)
+  edet_dgrad_lazy dyl;  // bwd with a lazy dy (k_dwt GIN): dy = d(raw y) built on load
 };
 
 // The N filter taps of channel ch (stride C between taps) into fp32 registers.  Every load is
@@ -1265,20 +1266,18 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
   // wgrad: the P dy rows of step j; vector e = tid + u*256: row e / (4 TW), pixel, channels
   constexpr int DYV = (P * TW * 4 + 255) / 256;
   uint4 dyr[DYV][WORDS];
+  // range-checked buffer loads: a vector past the rows, the strip or the channels reads zeros
+  // (a select zeroing the loaded value made the compiler wait for every load in flight)
+  const auto rsdy = buf_rsrc(WG ? (const T*)g.dy + obase * C : nullptr, WG ? (long)OH * OW * C * (long)sizeof(T) : 0);
   auto fetch_dy = [&](int j) {
 #pragma unroll
     for (int u = 0; u < DYV; ++u) {
       const int e = tid + u * 256, p = e / (TW * 4), rem = e - p * (TW * 4);
       const int px = rem >> 2, cv = (rem & 3) * 8, oy = oy0 + j * P + p;
       const bool in = p < P && j * P + p < nrows && oy < OH && ox0 + px < OW && c0 + cv < C;
-      const uint4* src = reinterpret_cast<const uint4*>(
-          (const T*)g.dy + (in ? (obase + (size_t)oy * OW + ox0 + px) * C + c0 + cv : 0));
-      dyr[u][0] = src[0];
-      if constexpr (WORDS == 2) dyr[u][1] = src[1];
-      if (!in) {
+      const uint32_t off = buf_off(in, (uint32_t)((((size_t)oy * OW + ox0 + px) * C + c0 + cv) * sizeof(T)));
 #pragma unroll
-        for (int w = 0; w < WORDS; ++w) dyr[u][w] = make_uint4(0, 0, 0, 0);
-      }
+      for (int w = 0; w < WORDS; ++w) dyr[u][w] = buf_ld16(rsdy, off + 16 * w);
     }
   };
   auto commit_dy = [&](int j) {
@@ -1321,30 +1320,36 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
 #pragma unroll
     for (int t = 0; t < K * K; ++t) acc[t] = 0.f;
   }
-  auto store_step = [&](int j) {  // fwd output rows of step j from stage buffer j & 1 (after a barrier)
-    for (int e = tid; e < P * TW * 4; e += 256) {
-      const int p = e / (TW * 4), rem = e - p * (TW * 4);
+  // fwd output rows of step j from stage buffer j & 1 (after a barrier): a compile-time number
+  // of range-checked buffer stores per thread, no branch (a store past the image or the strip
+  // takes an out-of-range offset and is dropped).  The variable-count store loop with its
+  // per-vector branch left the wait-count pass unable to count the stores, so the commit of the
+  // prefetched rows after it waited for every memory operation in flight (vmcnt(0)).
+  constexpr int NSE = (P * TW * 4 + 255) / 256;
+  const auto rsy = buf_rsrc((const T*)g.y + obase * C, (long)OH * OW * C * (long)sizeof(T));
+  auto store_step = [&](int j) {
+#pragma unroll
+    for (int u = 0; u < NSE; ++u) {
+      const int e = tid + u * 256, ev = e < P * TW * 4 ? e : 0;
+      const int p = ev / (TW * 4), rem = ev - p * (TW * 4);
       const int px = rem >> 2, cv = (rem & 3) * 8, oy = oy0 + j * P + p;
-      if (j * P + p < nrows && ox0 + px < OW && c0 + cv < C) {
-        T* dst = (T*)g.y + (obase + (size_t)oy * OW + ox0 + px) * C + c0 + cv;
-        const T* src = &ost[WG ? 0 : (j & 1)][(p * TW + px) * DCB + cv];
-        if constexpr (sizeof(T) == 2) {
-          *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
-        } else {
-          reinterpret_cast<float4*>(dst)[0] = reinterpret_cast<const float4*>(src)[0];
-          reinterpret_cast<float4*>(dst)[1] = reinterpret_cast<const float4*>(src)[1];
-        }
-      }
+      const bool ok = j >= 0 && e < P * TW * 4 && j * P + p < nrows && ox0 + px < OW && c0 + cv < C;
+      const uint32_t off = buf_off(ok, (uint32_t)((((size_t)oy * OW + ox0 + px) * C + c0 + cv) * sizeof(T)));
+      const uint4* src = reinterpret_cast<const uint4*>(&ost[WG ? 0 : (j & 1)][(p * TW + px) * DCB + cv]);
+#pragma unroll
+      for (int w = 0; w < WORDS; ++w)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, src[w]), rsy, off + 16 * w, 0, 0);
     }
   };
   auto step = [&](int j, auto& rsj) {
     if constexpr (!WG) {
-      if (j > 0) store_step(j - 1);
+      store_step(j - 1);  // (j = 0: every store is out of range)
     }
-    if (j + 1 < nsteps) {  // rows of step j+1: ring slots and dy buffer step j does not read
-      commit(rsj, rows_of(j + 1), P * S);
-      if constexpr (WG) commit_dy(j + 1);
-    }
+    // rows of step j+1: ring slots and dy buffer step j does not read.  Unconditional (past the
+    // last step they fill slots no step reads): a commit under a branch left the wait-count pass
+    // merging paths, and it waited for the other register set's loads too
+    commit(rsj, rows_of(j + 1), P * S);
+    if constexpr (WG) commit_dy(j + 1);
     // unconditional: a conditional refill joins old and new values in a copy, and the copy
     // waits for the load (rows past the block are real or predicated-off elements)
     fetch(rsj, rows_of(j + 1 + PF), P * S);
@@ -1420,16 +1425,19 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
     }
     __syncthreads();
   };
+  // PF = 2 runs the steps in pairs with no branch between them: an odd count takes one more
+  // step past the block's rows (its outputs fail the row test of the statistics and the stores)
+  const int nrun = PF == 2 ? (nsteps + 1) & ~1 : nsteps;
   if constexpr (PF == 1) {
     for (int j = 0; j < nsteps; ++j) step(j, rs);
   } else {
-    for (int j = 0; j < nsteps; j += 2) {
+    for (int j = 0; j < nrun; j += 2) {
       step(j, rs);
-      if (j + 1 < nsteps) step(j + 1, rs2);
+      step(j + 1, rs2);
     }
   }
   if constexpr (!WG) {
-    store_step(nsteps - 1);
+    store_step(nrun - 1);
     if (g.has_stats) {  // the ring is free after the last barrier
       float* red = ring;
       red[gc * DCB + c] = s;
@@ -2085,7 +2093,12 @@ struct DwtPlan {
   int tpb, ncg;
 };
 
-template <typename T, int K, bool FOLD>
+// GIN (edet_dwconv_bwd_lazy): g.dy is not d(raw y) but the lazy gradient g.dyl -- dv, the
+// value's raw y and its BN-backward tables -- and the dy window is built on load with
+// edet_lazy_bwd_apply's formula (d(raw y) = sc*du + kb*y + kc, du = (dv*gate + dsq)*act'(bn(y))),
+// rounded to T as that pass would store it: the apply's pass over (dv, y) and the write and
+// re-read of d(raw y) are gone (one extra y stream here instead)
+template <typename T, int K, bool FOLD, bool GIN = false>
 __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64 fold) {
   constexpr int P = (K - 1) / 2, IT = DWT_T + K - 1, NPX = IT * IT;
   constexpr int EPV = 16 / (int)sizeof(T);  // elements per 16-byte vector
@@ -2099,6 +2112,8 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
   __shared__ __attribute__((aligned(16))) T xs[FOLD ? DWT_T * DWT_T * DWT_CB : 8];  // raw x, interior
   __shared__ float2 af[DWT_CB];
   __shared__ float gt[DWT_CB];
+  __shared__ float4 gtab[GIN ? DWT_CB : 1];  // GIN: y's (sc, sh, kb, kc) per channel
+  __shared__ float2 ggd[GIN ? DWT_CB : 1];   // GIN: (gate, dsq) of this image per channel
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
   int id = xcd_remap(blockIdx.x, gridDim.x), seg = 0;
@@ -2109,12 +2124,32 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
   const int c0 = cg * DWT_CB, C = g.C;
   const int H = g.pin.H[seg], W = g.pin.W[seg];
   const T* X = (const T*)g.x + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * g.lz.ld + c0;
-  const T* DY = (const T*)g.dy + ((size_t)g.pout.row_off[seg] + (size_t)n * H * W) * C + c0;
+  const T* DY = (const T*)(GIN ? g.dyl.dv : g.dy) + ((size_t)g.pout.row_off[seg] + (size_t)n * H * W) * C + c0;
+  const T* YR = GIN ? (const T*)g.dyl.y.x + ((size_t)g.pout.row_off[seg] + (size_t)n * H * W) * C + c0 : nullptr;
   T* DX = (T*)g.dx + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * C + c0;
   const float inv = 1.f / (float)seg_rows(g.pin, seg);
   if (tid < DWT_CB) {
     af[tid] = bn_affine(g.lz.bn, seg, c0 + tid, inv);
     gt[tid] = g.lz.gate ? g.lz.gate[(size_t)n * C + c0 + tid] : 1.f;
+    if constexpr (GIN) {
+      // edet_lazy_bwd_apply's tables (bn.hip load_tables + the kb / kc fold), same arithmetic
+      const edet_dgrad_lazy& d = g.dyl;
+      const int cc = c0 + tid;
+      float4 t = make_float4(1.f, 0.f, 0.f, 0.f);
+      if (d.y.bn.enabled) {
+        const float2 a = bn_affine(d.y.bn, seg, cc, inv), q = bn_mean_rstd(d.y.bn, seg, cc, inv);
+        const float dgm = (float)(d.acc.dgamma[seg][cc] * (double)inv), dbm = (float)(d.acc.dbeta[seg][cc] * (double)inv);
+        const float kb = -a.x * q.y * dgm;
+        t = make_float4(a.x, a.y, kb, -a.x * dbm - kb * q.x);
+        // one writer per segment and channel: the image-0, first-chunk block
+        if (n == 0 && chunk == 0 && d.grads.a[seg]) {
+          d.grads.a[seg][cc] += (float)d.acc.dgamma[seg][cc];
+          d.grads.b[seg][cc] += (float)d.acc.dbeta[seg][cc];
+        }
+      }
+      gtab[tid] = t;
+      ggd[tid] = make_float2(d.y.gate ? d.y.gate[(size_t)n * C + cc] : 1.f, d.dsq ? d.dsq[(size_t)n * C + cc] : 0.f);
+    }
   }
   // this thread: channel c, the 4 x 4 patch at rows a0 .., columns b0 .. of every tile
   const int c = lane & 15, a0 = (lane >> 4) * 4, b0 = wave * 4;
@@ -2134,7 +2169,7 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
   for (int t = t_begin; t < t_end; ++t) {
     const int y0 = (t / pl.ntx[seg]) * DWT_T, x0 = (t % pl.ntx[seg]) * DWT_T;
     // ---- the halo window of dy and x: every vector requested before any is used
-    uint4 rd[NL], rx[NL];
+    uint4 rd[NL], rx[NL], ry[GIN ? NL : 1];
     uint32_t okm = 0;
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
@@ -2144,7 +2179,12 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
       const uint32_t pix = ok ? (uint32_t)(gy * W + gx) : 0u;
       const uint4 a = *reinterpret_cast<const uint4*>(DY + (size_t)pix * C + (ok ? q * EPV : 0));
       const uint4 b = *reinterpret_cast<const uint4*>(X + (size_t)pix * g.lz.ld + (ok ? q * EPV : 0));
-      rd[u] = ok ? a : make_uint4(0, 0, 0, 0);
+      if constexpr (GIN) {
+        ry[u] = *reinterpret_cast<const uint4*>(YR + (size_t)pix * C + (ok ? q * EPV : 0));
+        rd[u] = a;  // zeroed after the transform (kc != 0 off the plane)
+      } else {
+        rd[u] = ok ? a : make_uint4(0, 0, 0, 0);
+      }
       rx[u] = b;
       okm |= (uint32_t)ok << u;
     }
@@ -2154,9 +2194,30 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
       const int e = tid + u * 256, px = e / VPP, q = e - px * VPP;
       if (e >= NV) break;
       const int i = px / IT, j = px - i * IT;
-      *reinterpret_cast<uint4*>(dys + i * DRS + j * DWT_CB + q * EPV) = rd[u];
-      const T* xe = reinterpret_cast<const T*>(&rx[u]);
       const float m = ((okm >> u) & 1) ? 1.f : 0.f;  // zero padding of the transformed input
+      if constexpr (GIN) {
+        const T* de = reinterpret_cast<const T*>(&rd[u]);
+        const T* ye = reinterpret_cast<const T*>(&ry[u]);
+        const int yact = g.dyl.y.act;
+        T o[EPV];
+#pragma unroll
+        for (int jj = 0; jj < EPV; ++jj) {
+          const int cc = q * EPV + jj;
+          const float4 tb = gtab[cc];
+          const float2 gd = ggd[cc];
+          const float yv = to_f<T>(ye[jj]);
+          float gg = to_f<T>(de[jj]);
+          gg *= gd.x;
+          gg += gd.y;
+          const float du = yact ? gg * dswishf_(yv * tb.x + tb.y) : gg;
+          const float v = tb.x * du + tb.z * yv + tb.w;
+          o[jj] = from_f<T>(v * m);
+        }
+        *reinterpret_cast<uint4*>(dys + i * DRS + j * DWT_CB + q * EPV) = *reinterpret_cast<const uint4*>(o);
+      } else {
+        *reinterpret_cast<uint4*>(dys + i * DRS + j * DWT_CB + q * EPV) = rd[u];
+      }
+      const T* xe = reinterpret_cast<const T*>(&rx[u]);
       float vals[EPV];
 #pragma unroll
       for (int jj = 0; jj < EPV; ++jj) {
@@ -2306,7 +2367,7 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
   }
 }
 
-template <typename T, int K, bool FOLD>
+template <typename T, int K, bool FOLD, bool GIN = false>
 static int launch_dwt(DwArgs g, const edet_bngrad64& fold, hipStream_t s) {
   DwtPlan pl{};
   pl.ncg = g.C / DWT_CB;
@@ -2333,7 +2394,7 @@ static int launch_dwt(DwArgs g, const edet_bngrad64& fold, hipStream_t s) {
   }
   if (total == 0) return EDET_OK;
   EDET_REQUIRE(total < (1L << 31), "dwconv_bwd: grid too large");
-  EDET_LAUNCH((k_dwt<T, K, FOLD>), dim3((unsigned)total), dim3(256), 0, s, g, pl, fold);
+  EDET_LAUNCH((k_dwt<T, K, FOLD, GIN>), dim3((unsigned)total), dim3(256), 0, s, g, pl, fold);
   return check_launch("edet dwconv bwd (tiles)");
 }
 
@@ -2663,6 +2724,34 @@ int edet_dwconv_bwd(int dtype, const edet_lazy* x, const edet_pyramid* pin, int 
   g.x = x->x; g.lz = *x; g.dy = dy; g.w = w; g.dx = dx; g.dw = dw; g.pin = *pin; g.pout = *pout;
   g.C = C; g.accumulate = accumulate; g.ncb = cdiv(C, DCB);
   EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_dwb<T>(k, g, fold, (hipStream_t)stream); });
+}
+
+int edet_dwconv_bwd_lazy(int dtype, const edet_lazy* x, const edet_pyramid* pin, int C, int k,
+                         const edet_dgrad_lazy* dyl, const edet_pyramid* pout, const void* w,
+                         void* dx, int accumulate, float* dw, const edet_bngrad64* fold,
+                         edet_stream_t stream) {
+  EDET_REQUIRE(x && dyl && dyl->dv && dyl->y.x && w && dx && dw, "dwconv_bwd_lazy: null argument");
+  EDET_REQUIRE(C % DWT_CB == 0 && x->ld % 8 == 0 && dyl->y.ld == C,
+               "dwconv_bwd_lazy: need C %% 16 == 0, x->ld %% 8 == 0 and y.ld == C");
+  int rc = check_pyrs(pin, pout, k, 1);
+  if (rc) return rc;
+  EDET_REQUIRE(!fold || (!accumulate && x->gate == nullptr && x->bn.enabled),
+               "dwconv_bwd_lazy: the BN fold needs accumulate == 0, no gate and a BatchNorm on x");
+  if (dyl->y.bn.enabled)
+    for (int i = 0; i < pout->nseg; ++i)
+      EDET_REQUIRE(dyl->acc.dgamma[i] && dyl->acc.dbeta[i] && dyl->y.bn.sum[i] && dyl->y.bn.gamma[i],
+                   "dwconv_bwd_lazy: null BN table of y (segment %d)", i);
+  DwArgs g{};
+  g.x = x->x; g.lz = *x; g.dyl = *dyl; g.w = w; g.dx = dx; g.dw = dw; g.pin = *pin; g.pout = *pout;
+  g.C = C; g.accumulate = accumulate; g.ncb = cdiv(C, DCB);
+  const edet_bngrad64 f = fold ? *fold : edet_bngrad64{};
+  const hipStream_t st = (hipStream_t)stream;
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    if (k == 3) return fold ? launch_dwt<T, 3, true, true>(g, f, st) : launch_dwt<T, 3, false, true>(g, f, st);
+    if (k == 5) return fold ? launch_dwt<T, 5, true, true>(g, f, st) : launch_dwt<T, 5, false, true>(g, f, st);
+    set_error("dwconv_bwd_lazy: unsupported kernel %d", k);
+    return EDET_EUNSUPPORTED;
+  });
 }
 
 }  // extern "C"

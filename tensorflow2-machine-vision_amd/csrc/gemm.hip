@@ -968,6 +968,7 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
   struct Stage {
     uint4 rd[HR], rx[HR];
     int rseg[HR];
+    uint4 rg[LAZY ? HR : 1][2];  // LAZY: the SE gate of the row's image, this thread's 8 columns
   };
   // Branch-free fetches: a dead row (past the range or in a segment's padding) loads a live row
   // of the block and a column vector past the row loads the row's last vector, and commit zeroes
@@ -977,6 +978,13 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
   // (loads under branches made it wait for every stage in flight: s_waitcnt vmcnt(0)).
   const bool dcol = n0 + lc < g.N, xcol = kk0 + lc < g.K;
   const int dc = min(n0 + lc, g.lddy - 8), xc = min(kk0 + lc, g.lda - 8);
+  // LAZY with an SE gate (one segment, the host requires it): the gate vector of each row's
+  // image is fetched with the row, by a range-checked buffer load (no gate: an empty range, the
+  // load reads zeros and is not used).  A gate load in the commit, under the per-image branch,
+  // made every commit wait for all the stages in flight (s_waitcnt vmcnt(0), scripts/wait_scan.py).
+  const bool has_gate = LAZY && g.lz.gate != nullptr;
+  const auto rs_gate = buf_rsrc(LAZY ? g.lz.gate : nullptr, has_gate ? (long)g.pyr.batch * g.K * 4 : 0);
+  const int hw0 = g.pyr.H[0] * g.pyr.W[0], off0 = g.pyr.row_off[0];
   auto fetch = [&](Stage& S, int m0) {
 #pragma unroll
     for (int h = 0; h < HR; ++h) {
@@ -988,47 +996,40 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
       const size_t r = live ? row : m_begin;
       S.rd[h] = *reinterpret_cast<const uint4*>(DY + r * g.lddy + dc);
       S.rx[h] = *reinterpret_cast<const uint4*>(A + r * g.lda + xc);
+      if constexpr (LAZY) {
+        const int img = ((int)r - off0) / hw0;
+        const uint32_t go = buf_off(has_gate && xcol, (uint32_t)((img * g.K + kk0 + lc) * 4));
+        S.rg[h][0] = buf_ld16(rs_gate, go);
+        S.rg[h][1] = buf_ld16(rs_gate, go + 16);
+      }
     }
   };
   auto zsel = [](bool keep, uint4 v) {
     return make_uint4(keep ? v.x : 0u, keep ? v.y : 0u, keep ? v.z : 0u, keep ? v.w : 0u);
   };
-  // SE gate of this thread's 8 columns, cached per image (the image changes every hw rows)
-  int gimg = -1;
-  float gcache[8];
+  // (branch-free: dead rows and columns past K are transformed like live ones and selected out)
   auto commit = [&](const Stage& S, int buf, int m0) {
 #pragma unroll
     for (int h = 0; h < HR; ++h) {
       const int r = lr + 32 * h;
       *reinterpret_cast<uint4*>(&Ds[buf][r * WT_LDM + lc]) = zsel(S.rseg[h] >= 0 && dcol, S.rd[h]);
-      uint4 x = zsel(S.rseg[h] >= 0 && xcol, S.rx[h]);
+      uint4 x;
       if constexpr (LAZY) {
-        if (S.rseg[h] >= 0) {
-          const int row = m0 + r, sg = S.rseg[h];
-          const uint16_t* t = reinterpret_cast<const uint16_t*>(&x);
-          if (g.lz.gate) {
-            const int img = (row - g.pyr.row_off[sg]) / (g.pyr.H[sg] * g.pyr.W[sg]);
-            if (img != gimg) {
-              gimg = img;
-              const int nk = g.K - (kk0 + lc);
-              if (nk >= 8) ld8(g.lz.gate + (size_t)img * g.K + kk0 + lc, gcache);
-              else
+        const int sg = max(S.rseg[h], 0);
+        const bool keep = S.rseg[h] >= 0 && xcol;
+        const uint16_t* t = reinterpret_cast<const uint16_t*>(&S.rx[h]);
+        const float4 g0 = __builtin_bit_cast(float4, S.rg[h][0]), g1 = __builtin_bit_cast(float4, S.rg[h][1]);
+        const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+        uint16_t o[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) gcache[j] = j < nk ? g.lz.gate[(size_t)img * g.K + kk0 + lc + j] : 0.f;
-            }
-          }
-          uint16_t o[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float u = 0.f;
-            if (kk0 + lc + j < g.K) {
-              u = lazy_apply(to_f<uint16_t>(t[j]), xf[sg][lc + j], g.lz.act);
-              if (g.lz.gate) u *= gcache[j];
-            }
-            o[j] = from_f<uint16_t>(u);
-          }
-          x = *reinterpret_cast<uint4*>(o);
+        for (int j = 0; j < 8; ++j) {
+          float u = lazy_apply(to_f<uint16_t>(t[j]), xf[sg][lc + j], g.lz.act);
+          if (has_gate) u *= gv[j];
+          o[j] = from_f<uint16_t>(keep && kk0 + lc + j < g.K ? u : 0.f);
         }
+        x = *reinterpret_cast<uint4*>(o);
+      } else {
+        x = zsel(S.rseg[h] >= 0 && xcol, S.rx[h]);
       }
       *reinterpret_cast<uint4*>(&Xs[buf][r * WT_LDM + lc]) = x;
     }

@@ -582,8 +582,10 @@ class EfficientDetNetTrain(EfficientDetNet):
                vp(self.norm_partials), self.eng.dt, vp(P.wc) if P.wc is not P.w else None, vp(self.step_counter), s)
         P.refresh_compute_copy(cast=False)  # transposed 1x1 copies for the next dgrad
         cfg = self.cfg
+        # a skipped non-finite step (skip_nonfinite) leaves the moving statistics alone as well
+        skip = vp(self.scalars[6:7]) if self.sched.skip_nonfinite else None
         L.call("edet_bn_update_moving", P.n_bn, vp(P.bn_tstats[0]), vp(P.bn_tstats[1]), vp(P.bn_count),
-               float(cfg.batch_norm_momentum), vp(P.bn_mm), vp(P.bn_mv), s)
+               float(cfg.batch_norm_momentum), skip, vp(P.bn_mm), vp(P.bn_mv), s)
 
     def load_state_dict(self, sd):
         """Weights (and BN moving statistics) from a checkpoint, with fresh optimizer state:

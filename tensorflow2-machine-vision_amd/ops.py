@@ -36,11 +36,10 @@ def _bn_grads(bns: List[BNParam]):
     return seg_out([(bn.dgamma, bn.dbeta) for bn in bns])
 
 
-def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor, int]:
-    """d(value) -> d(raw) through the lazy transform act(bn(raw)) * gate (+ SE branch)."""
-    if not out.has_transform and rec.scale is None:
-        return rec.t, rec.ld
-    assert rec.ld == out.C
+def _value_grad_tables(eng: Engine, out: Act, rec: GradRec):
+    """The passes d(value) -> d(raw) needs before its apply: the SE gate gradient and SE backward
+    (dsq), and the BN-backward sums (reduce pass, or folded earlier / into the SE pass).
+    Returns (dsq or None, fp64 edet_bngrad64 sums or None, fp32 gamma/beta gradient SegOut or None)."""
     s = stream()
     lz = out.lazy()
     dsq = None
@@ -80,10 +79,35 @@ def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor
             L.call("edet_se_bwd", *args, s)
     if out.bns is not None and not fused_se and not folded:
         L.call("edet_lazy_bwd_reduce", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, s)
+    return dsq, acc, grads
+
+
+def value_grad_to_raw(eng: Engine, out: Act, rec: GradRec) -> Tuple[torch.Tensor, int]:
+    """d(value) -> d(raw) through the lazy transform act(bn(raw)) * gate (+ SE branch)."""
+    if not out.has_transform and rec.scale is None:
+        return rec.t, rec.ld
+    assert rec.ld == out.C
+    dsq, acc, grads = _value_grad_tables(eng, out, rec)
     dx = eng.empty(out.pyr.rows, out.C)
-    L.call("edet_lazy_bwd_apply", eng.dt, lz, out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, grads,
-           vp(dx), 0, s)
+    L.call("edet_lazy_bwd_apply", eng.dt, out.lazy(), out.pyr.c, out.C, vp(rec.t), vp(rec.scale), vp(dsq), acc, grads,
+           vp(dx), 0, stream())
     return dx, out.C
+
+
+def value_grad_lazy(eng: Engine, out: Act, rec: GradRec) -> Tuple[L.DgradLazy, list]:
+    """d(value) -> the edet_dgrad_lazy descriptor of d(raw): the same passes as
+    value_grad_to_raw without its apply; the consumer builds d(raw) on load
+    (edet_dwconv_bwd_lazy).  Returns the descriptor and the tensors it points into."""
+    assert rec.ld == out.C and rec.scale is None
+    dsq, acc, grads = _value_grad_tables(eng, out, rec)
+    d = L.DgradLazy()
+    d.dv = rec.t.data_ptr()
+    d.y = out.lazy()
+    d.dsq = dsq.data_ptr() if dsq is not None else None
+    if acc is not None:
+        d.acc = acc
+        d.grads = grads
+    return d, [rec.t, dsq]
 
 
 # --------------------------------------------------------------------------- stem
@@ -174,9 +198,12 @@ FOLD_DW_BN = os.environ.get("EDET_FOLD_DW_BN", "1") != "0"
 FOLD_GEMM_BN = os.environ.get("EDET_FOLD_GEMM_BN", "0") != "0"
 # the stride-2 depthwise dgrad with the same fold (edet_dwconv_dgrad_fold)
 FOLD_DWS2_BN = os.environ.get("EDET_FOLD_DWS2_BN", "1") != "0"
-# every switch that takes a BN-backward reduce into the kernel producing the gradient (the test
-# of the folds flips them all: tests/test_model_gpu.py::test_bn_backward_folds_equal_unfused_path)
-FOLD_SWITCHES = ("FUSED_DW_BWD", "FOLD_DW_BN", "FOLD_GEMM_BN", "FOLD_DWS2_BN")
+# the stride-1 SE-gated depthwise output's BN-backward apply inside the fused backward's dy
+# staging (edet_dwconv_bwd_lazy) instead of its own pass
+LAZY_DY_DW = os.environ.get("EDET_LAZY_DY", "1") != "0"
+# every switch that takes a BN-backward pass into the kernel producing or consuming the gradient
+# (the test of the folds flips them all: tests/test_model_gpu.py::test_bn_backward_folds_equal_unfused_path)
+FOLD_SWITCHES = ("FUSED_DW_BWD", "FOLD_DW_BN", "FOLD_GEMM_BN", "FOLD_DWS2_BN", "LAZY_DY_DW")
 
 
 def _fold_dst(eng: Engine, x: Act, acc: int):
@@ -214,6 +241,17 @@ def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
     def bwd():
         rec = eng.tape.take(out)
         if rec is None:
+            return
+        if (stride == 1 and FUSED_DW_BWD and LAZY_DY_DW and not eng.overlap and out.se is not None
+                and rec.scale is None and rec.ld == C and C % 16 == 0):
+            # the SE-gated swish(BN) output: its d(raw) is built inside the fused backward while
+            # the dy window loads (edet_dwconv_bwd_lazy) -- no apply pass, no d(raw) round trip
+            dyl, keep = value_grad_lazy(eng, out, rec)
+            dx, acc = eng.tape.dst(x)
+            fold = _fold_dst(eng, x, acc) if FOLD_DW_BN else None
+            L.call("edet_dwconv_bwd_lazy", eng.dt, x.lazy(), x.pyr.c, C, k, dyl, pout.c, vp(P.wcv(wname)),
+                   vp(dx), acc, vp(P.grad(wname)), fold, stream())
+            del keep
             return
         d, ld = value_grad_to_raw(eng, out, rec)
         assert ld == C

@@ -46,10 +46,13 @@ def test_no_kernel_spills(table):
 
 # (kernel name prefix, waves per SIMD the instance was measured at) -- bf16 storage instances
 FLOORS = [
-    ("void edet::k_dwt<unsigned short, 3, true>", 3),
-    ("void edet::k_dwt<unsigned short, 3, false>", 3),
-    ("void edet::k_dwt<unsigned short, 5, true>", 2),
-    ("void edet::k_dwt<unsigned short, 5, false>", 2),
+    ("void edet::k_dwt<unsigned short, 3, true, false>", 3),
+    ("void edet::k_dwt<unsigned short, 3, false, false>", 3),
+    ("void edet::k_dwt<unsigned short, 5, true, false>", 2),
+    ("void edet::k_dwt<unsigned short, 5, false, false>", 2),
+    # the lazy-dy forms (edet_dwconv_bwd_lazy) at the same occupancy
+    ("void edet::k_dwt<unsigned short, 3, true, true>", 3),
+    ("void edet::k_dwt<unsigned short, 5, true, true>", 2),
     ("void edet::k_fuse_bwd_m<", 3),
     ("void edet::k_fuse_fwd_m<", 3),
 ]

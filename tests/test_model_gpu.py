@@ -281,6 +281,35 @@ def test_training_reduces_loss_bf16():
     assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
 
 
+def test_skip_nonfinite_step_leaves_weights_and_moving_stats():
+    """SURVEY §5 failure detection at model level: with skip_nonfinite a step on a
+    NaN input is reported as skipped and leaves the weights, optimizer slots, step counter AND
+    the BN moving statistics unchanged (the batch statistics of that step are NaN); the next
+    finite step applies normally."""
+    c = cfg()
+    anchors = Anchors(c.min_level, c.max_level, (SIZE, SIZE), c.num_scales, c.aspect_ratios, c.anchor_scale)
+    m = EfficientDetNetTrain(efficientnet_b0_blocks(), c, anchors, dtype="bf16", seed=2,
+                             lr_schedule={"fixed_lr": 0.01}, skip_nonfinite=True)
+    x, boxes, cls, n = synth(4)
+    t, *_ = make_targets(m, anchors, boxes, cls, n)
+    xs = torch.tensor(x).cuda()
+    m.train_step((xs, t))  # one finite step: non-trivial moving statistics and momentum
+    torch.cuda.synchronize()
+    P = m.P
+    before = [a.clone() for a in (P.w, P.v, P.ema, P.bn_mm, P.bn_mv, m.step_counter)]
+    bad = xs.clone()
+    bad[0, 5, 7, 1] = float("nan")
+    out = m.train_step((bad, t))
+    torch.cuda.synchronize()
+    assert float(out["skipped"]) == 1.0 and not np.isfinite(float(out["gnorm"]))
+    for a, b in zip((P.w, P.v, P.ema, P.bn_mm, P.bn_mv, m.step_counter), before):
+        assert torch.equal(a, b)
+    out = m.train_step((xs, t))
+    torch.cuda.synchronize()
+    assert float(out["skipped"]) == 0.0 and np.isfinite(float(out["loss"]))
+    assert not torch.equal(P.bn_mm, before[3]) and bool(torch.isfinite(P.bn_mm).all())
+
+
 def test_dp_two_identical_replicas_equal_double_batch():
     """Data-parallel math on the HIP path: a world-size-2 replica whose N+ and
     gradient all-reduces see two identical replicas (x2) must equal the single-GPU step on the
