@@ -400,6 +400,27 @@ int edet_bn_update_moving(int64_t n, const double* sum, const double* sq, const 
 int edet_dropmask(float* out, int n, float survival, uint64_t seed, const int32_t* step,
                   edet_stream_t stream);
 
+/* ---- input pipeline: training augmentation (datasets/coco_dataset_one.py:99-135) ----
+ * One image, HWC uint8 in the caller's channel order: box blur -> perspective warp (+ noise)
+ * -> proportional resize into an out_w x out_h frame with a border -> /255 in `dtype` (or raw
+ * uint8 with out_raw).  The restated OpenCV algorithms and their parity status are described in
+ * csrc/augment.hip; the random draws and the box-corner geometry are host-side (augment.py).
+ * scratch: 2 * H * W * 3 bytes of device memory. */
+typedef struct edet_aug_params {
+  double warp[9];            /* destination -> source map of the warp, row-major (identity: none) */
+  uint64_t noise_seed;
+  int32_t blur;              /* box-blur window 0..31 (0 or 1: none) */
+  int32_t warp_border;       /* 0: constant warp_bg, 1: replicate */
+  int32_t noise;             /* 1: + U{0..39} - 20 per element, clipped to [0, 255] */
+  int32_t rw, rh, top, left; /* the resized image's size and its place in the output frame */
+  int32_t pad_border;        /* 0: constant pad_bg, 1: replicate the resized image's edge */
+  int32_t out_raw;           /* 1: out is uint8 [out_h][out_w][3] without the /255 */
+  uint8_t warp_bg[4];        /* border values in the image's channel order ([3] unused) */
+  uint8_t pad_bg[4];
+} edet_aug_params;
+int edet_augment_image(int dtype, const uint8_t* src, int H, int W, const edet_aug_params* p,
+                       uint8_t* scratch, void* out, int out_h, int out_w, edet_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

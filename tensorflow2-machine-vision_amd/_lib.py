@@ -73,6 +73,14 @@ class Sched(ctypes.Structure):
                 ("skip_nonfinite", c_int32)]
 
 
+class AugParams(ctypes.Structure):
+    """edet_aug_params: one image's augmentation (include/edet.h, csrc/augment.hip)."""
+    _fields_ = [("warp", ctypes.c_double * 9), ("noise_seed", c_uint64), ("blur", c_int32), ("warp_border", c_int32),
+                ("noise", c_int32), ("rw", c_int32), ("rh", c_int32), ("top", c_int32), ("left", c_int32),
+                ("pad_border", c_int32), ("out_raw", c_int32), ("warp_bg", ctypes.c_uint8 * 4),
+                ("pad_bg", ctypes.c_uint8 * 4)]
+
+
 P = c_void_p
 PPyr, PLazy, PSeg, PStat, PBnG, PFuse, PSched = (POINTER(Pyramid), POINTER(Lazy), POINTER(SegOut), POINTER(StatOut),
                                                  POINTER(BnGrad64), POINTER(FuseInput), POINTER(Sched))
@@ -132,6 +140,7 @@ SIGNATURES = {
     "edet_bn_inference_stats": [c_int64, P, P, P, P, P, P],
     "edet_bn_update_moving": [c_int64, P, P, P, c_float, P, P, P, P],
     "edet_dropmask": [P, c_int, c_float, c_uint64, P, P],
+    "edet_augment_image": [c_int, P, c_int, c_int, POINTER(AugParams), P, P, c_int, c_int, P],
 }
 _RESTYPE = {"edet_last_error": c_char_p}
 

@@ -18,10 +18,10 @@ yields ``[T_y(f1), T_x(f2), T_y(f3), T_x(f4)]`` -- the label fields are (y1, x1,
 effect, whatever the loader's variable names say.
 
 Augmentation: the reference applies random blur, perspective, noise and a random border in
-both its train and eval generators (:94-131).  Those are host-side OpenCV image operations
-(cv2 is not in this image) and outside the measured path; ``prepare`` runs the same chain
-with every random draw at its identity (blur size 0, offset 0, scale 1, no noise), i.e. the
-perspective step maps every point to itself and only the proportional resize remains.
+both its train and eval generators (:94-131).  ``prepare`` runs the chain with every random
+draw at its identity (blur size 0, offset 0, scale 1, no noise), i.e. the perspective step maps
+every point to itself and only the proportional resize remains; ``GetDataSet(augment=True)``
+runs the random chain with its pixel work on the GPU (augment.py, csrc/augment.hip).
 ``cv2.resize(INTER_AREA)`` is restated below (exact area averaging when shrinking, bilinear
 when enlarging); with cv2 absent its pixel values are parity-unpinned, the box geometry is
 pinned by the known-answer tests in tests/test_data.py.
@@ -231,6 +231,14 @@ class DataGenerator:
         """coco_dataset_one.py:156-212: shuffle at the start of every pass; when training,
         take images round-robin over the classes present (an image is used only when it holds
         the class whose turn it is); skip samples left without boxes."""
+        yield from self._sample_order(skip_empty=True)
+
+    def generate_labels(self) -> Iterator[Dict]:
+        """The labels in generate()'s order, before get_random_data (the augmenting GetDataSet
+        runs the chain itself and skips samples whose boxes vanish)."""
+        return self._sample_order(skip_empty=False)
+
+    def _sample_order(self, skip_empty: bool):
         class_list, image_classes = [], {}
         if self.is_train:
             seen = set()
@@ -251,8 +259,11 @@ class DataGenerator:
                     i = (i + 1) % n
                     continue
                 class_index = class_index + 1 if class_index < len(class_list) - 1 else 0
-            image, boxes, classes = self.get_random_data(lab)
             i = (i + 1) % n
+            if not skip_empty:
+                yield lab
+                continue
+            image, boxes, classes = self.get_random_data(lab)
             if len(classes) == 0:
                 continue
             yield image, boxes, classes
@@ -280,8 +291,13 @@ def collate(samples: Sequence[Tuple[np.ndarray, np.ndarray, np.ndarray]], device
 
 
 def GetDataSet(image_path: str, label_path: str, classes_path: str, batch_size: int, anchors,
-               is_train: bool = True, seed: Optional[int] = None):
-    """coco_dataset_one.py:214-246: (iterator of (images, Targets) batches, generator)."""
+               is_train: bool = True, seed: Optional[int] = None, augment: bool = False, dtype: str = "f32"):
+    """coco_dataset_one.py:214-246: (iterator of (images, Targets) batches, generator).
+
+    augment=True runs the reference's random chain (blur, perspective, noise, random borders;
+    augment.py + edet_augment_image on the GPU) instead of the identity chain: images are
+    decoded on the host, augmented on the device straight into the batch tensor (``dtype``
+    storage), and samples whose boxes all vanish are skipped as the reference skips them."""
     gen = DataGenerator(image_path, label_path, classes_path, anchors, is_train, seed)
 
     def batches():
@@ -291,4 +307,30 @@ def GetDataSet(image_path: str, label_path: str, classes_path: str, batch_size: 
             x, gb, gc, n = collate(samples, anchors.device)
             yield x, anchors.generate_targets_batched(gb, gc, n)
 
-    return batches(), gen
+    def augmented():
+        from . import _lib as L
+        from . import augment as AUG
+        it = gen.generate_labels()
+        W, H = gen.image_size
+        tdt = torch.float32 if dtype == "f32" else torch.bfloat16
+        while True:
+            x = torch.empty((batch_size, H, W, 3), dtype=tdt, device=anchors.device)
+            samples = []
+            while len(samples) < batch_size:
+                lab = next(it)
+                r = AUG.augment_one(read_image(lab["image_path"]), lab, AUG.draw(gen.rng), (W, H), x[len(samples)],
+                                    L.F32 if dtype == "f32" else L.BF16)
+                if r is not None:
+                    samples.append((None, r[0], r[1]))
+            B = len(samples)
+            G = max(1, max(len(s[2]) for s in samples))
+            gb = torch.zeros(B, G, 4, dtype=torch.float32)
+            gc = torch.zeros(B, G, dtype=torch.int32)
+            n = torch.zeros(B, dtype=torch.int32)
+            for b, (_, bx, cl) in enumerate(samples):
+                gb[b, :len(cl)] = torch.from_numpy(bx)
+                gc[b, :len(cl)] = torch.from_numpy(cl)
+                n[b] = len(cl)
+            yield x, anchors.generate_targets_batched(gb, gc, n)
+
+    return (augmented() if augment else batches()), gen

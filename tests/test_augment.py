@@ -1,0 +1,116 @@
+"""Training augmentation, host half (coco_dataset_one.py:99-151 with
+utils/image_helper.py:110-197, 293-330): the random draws in the reference's call order and
+the box-corner geometry, CPU.
+
+The geometry restates image_helper.py's float32 numpy arithmetic op for op (the reference
+module imports cv2 at load, so it cannot be imported here -- an ordinary ModuleNotFoundError);
+it is pinned by hand-derived known answers on exactly representable values and by the
+identity draw reproducing data.prepare's geometry bit for bit.
+"""
+import random
+
+import numpy as np
+
+from tf2mv_amd import augment as A
+from tf2mv_amd import data as D
+
+
+def test_draw_follows_reference_call_order():
+    """randint(0, 4); random() x4 (offset x, y, scale x, y); getRandomColor (3 x randint(0,
+    255)) + random() of the warp; the noise seed; getRandomColor + random() of the resize."""
+    r1, r2 = random.Random(5), random.Random(5)
+    d = A.draw(r1)
+    k = r2.randint(0, 4)
+    off = (r2.random() * 90 - 45, r2.random() * 90 - 45)
+    sc = (r2.random() * 1.5 + 0.5, r2.random() * 1.5 + 0.5)
+    wbg = (r2.randint(0, 255), r2.randint(0, 255), r2.randint(0, 255))
+    wrep = r2.random() >= 0.5
+    seed = r2.getrandbits(64)
+    pbg = (r2.randint(0, 255), r2.randint(0, 255), r2.randint(0, 255))
+    prep = r2.random() >= 0.5
+    assert (d.ksize, d.offset, d.scale, d.warp_bg, d.warp_replicate, d.noise_seed, d.pad_bg, d.pad_replicate) == \
+        (k, off, sc, wbg, wrep, seed, pbg, prep)
+    assert 0 <= d.ksize <= 4 and all(-45 <= o <= 45 for o in d.offset) and all(0.5 <= s <= 2 for s in d.scale)
+
+
+def test_perspective_matrix_structure():
+    """Angles 0: the rotations are identities (their -0.0 entries change nothing), so M is the
+    scale with the scaled offset in the last row."""
+    m = A.perspective_matrix((10.0, -5.0, 0.0), (0, 0, 0), (2.0, 0.5, 1.0))
+    assert m.dtype == np.float32
+    np.testing.assert_array_equal(m, np.float32([[2, 0, 0, 0], [0, 0.5, 0, 0], [0, 0, 1, 0], [20, -2.5, 0, 1]]))
+
+
+def test_project_points_known_answer():
+    """Image 100 x 60, offset (10, -5), scale (2, 0.5): (30, 20) - (50, 30) = (-20, -10);
+    @ M = (-20 * 2 + 20, -10 * 0.5 - 2.5) = (-20, -7.5); + centre = (30, 22.5)."""
+    m = A.perspective_matrix((10.0, -5.0, 0.0), (0, 0, 0), (2.0, 0.5, 1.0))
+    p = A.project_points(100, 60, m, [[30.0, 20.0], [0.0, 0.0], [100.0, 60.0]])
+    np.testing.assert_array_equal(p, np.float32([[30, 22.5], [-30, 12.5], [170, 42.5]]))
+
+
+def test_perspective_transform_maps_corners():
+    org = np.float32([[0, 0], [100, 0], [0, 60], [100, 60]])
+    dst = np.float32([[-30, 27.5], [170, 27.5], [-30, 42.5], [170, 42.5]])
+    h = A.perspective_transform(org, dst)
+    for (x, y), (u, v) in zip(org, dst):
+        q = h @ [x, y, 1.0]
+        np.testing.assert_allclose(q[:2] / q[2], [u, v], rtol=0, atol=1e-9)
+    assert h[2, 2] == 1.0
+    # a genuinely projective quad
+    dst2 = np.float32([[3, 2], [97, 8], [-4, 58], [104, 55]])
+    h2 = A.perspective_transform(org, dst2)
+    for (x, y), (u, v) in zip(org, dst2):
+        q = h2 @ [x, y, 1.0]
+        np.testing.assert_allclose(q[:2] / q[2], [u, v], rtol=0, atol=1e-9)
+
+
+def test_identity_draw_is_prepare_geometry():
+    """The identity draw (offset 0, scale 1) through augment_geometry gives data.prepare's
+    points bit for bit (the same float32 projection at M = I), and no warp."""
+    boxes = np.array([[200.0, 100.0, 400.0, 300.0], [20.0, 10.0, 90.0, 60.0]]).reshape(-1, 2)
+    inv, pts, place = A.augment_geometry(640, 480, A.AugmentDraw.identity(), boxes, (512, 512))
+    ref = D.identity_perspective_points((640, 480), boxes)
+    ref, _ = D.proportional_resize_points((640, 480), (512, 512), ref)
+    np.testing.assert_array_equal(pts, ref)
+    np.testing.assert_allclose(inv, np.eye(3), atol=1e-12)
+    assert place == (512, 384, 64, 0)
+
+
+def test_geometry_of_a_random_draw():
+    """A scaled, shifted draw: the points equal the hand composition of the three maps
+    (perspective with w / (w + 0) = 1, then the proportional resize), and the warp's inverse
+    sends every projected corner back to the original corner."""
+    rng = random.Random(3)
+    d = A.draw(rng)
+    W, H = 640, 480
+    boxes = np.array([[100.0, 50.0, 300.0, 200.0]]).reshape(-1, 2)
+    inv, pts, (rw, rh, top, left) = A.augment_geometry(W, H, d, boxes, (512, 512))
+    m = A.perspective_matrix((d.offset[0], d.offset[1], 0), (0, 0, 0), (d.scale[0], d.scale[1], 1))
+    f = np.float32
+    for (px, py), (qx, qy) in zip(boxes, pts):
+        tx, ty = f(f(px) - f(W / 2)), f(f(py) - f(H / 2))
+        x = f(tx * m[0, 0] + m[3, 0]) * W / (W + f(0)) + f(W / 2)
+        y = f(ty * m[1, 1] + m[3, 1]) * H / (H + f(0)) + f(H / 2)
+        np.testing.assert_allclose([qx, qy], [f(x) * rw / W + left, f(y) * rh / H + top], rtol=1e-6)
+    corners = np.float32([[0, 0], [W, 0], [0, H], [W, H]])
+    dst = A.project_points(W, H, m, corners)
+    for (x, y), (u, v) in zip(corners, dst):
+        q = inv @ [u, v, 1.0]
+        np.testing.assert_allclose(q[:2] / q[2], [x, y], rtol=0, atol=1e-6)
+
+
+def test_oracle_box_blur_and_identity_warp():
+    """The CPU restatements the GPU tests check against: k = 1 and the identity map copy the
+    image; a constant image blurs to itself; an integer shift moves it and fills the border."""
+    from oracle import ref_augment as R
+    rng = np.random.default_rng(1)
+    img = rng.integers(0, 256, (9, 13, 3), dtype=np.uint8)
+    np.testing.assert_array_equal(R.box_blur(img, 1), img)
+    c = np.full((7, 8, 3), 77, np.uint8)
+    for k in (2, 3, 4):
+        np.testing.assert_array_equal(R.box_blur(c, k), c)
+    np.testing.assert_array_equal(R.warp_perspective(img, np.eye(3), False, (1, 2, 3)), img)
+    sh = R.warp_perspective(img, np.array([[1, 0, 2], [0, 1, 1], [0, 0, 1.0]]), False, (1, 2, 3))
+    np.testing.assert_array_equal(sh[:-1, :-2], img[1:, 2:])
+    assert (sh[-1] == [1, 2, 3]).all() and (sh[:, -2:] == [1, 2, 3]).all()
