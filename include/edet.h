@@ -194,6 +194,15 @@ int edet_conv1x1_dgrad_fold(int dtype, const void* dy, int lddy, const edet_pyra
                             const void* wkn, int K, void* dx, int lddx, const edet_lazy* xv,
                             const edet_bngrad64* fold, edet_stream_t stream);
 /* dwt[n][k] += sum_m dy[m][n] * v(a)[m][k];  dbias[n] += sum_m dy[m][n]  (valid rows only) */
+/* The MBConv project conv's dgrad (mb_conv_block.py:150-154 backward) with the SE-gated
+ * depthwise output's backward sums taken from its own output tile (ABI 8): dx = dy * W as
+ * edet_conv1x1_dgrad (accumulate 0), and sums5 += edet_gate_bn_reduce(yv, dv = dx)'s five
+ * per-image sums ([5][batch][K] fp64, zeroed by the caller).  yv: the gated value's descriptor
+ * (raw y, BN with batch statistics, swish; its gate is ignored), one segment.  Shapes the
+ * K-loop epilogue does not take run the two passes (same results, same destinations). */
+int edet_conv1x1_dgrad_sesum(int dtype, const void* dy, int lddy, const edet_pyramid* rows, int N,
+                             const void* wkn, int K, void* dx, int lddx, const edet_lazy* yv, double* sums5,
+                             edet_stream_t stream);
 int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, int K,
                        const void* dy, int lddy, int N, float* dwt, float* dbias,
                        edet_stream_t stream);

@@ -100,6 +100,7 @@ SIGNATURES = {
     "edet_conv1x1_fwd": [c_int, PLazy, PPyr, c_int, P, c_int, P, P, c_int, c_int, PStat, P],
     "edet_conv1x1_dgrad": [c_int, P, c_int, PPyr, c_int, P, c_int, P, c_int, c_int, P],
     "edet_conv1x1_dgrad_fold": [c_int, P, c_int, PPyr, c_int, P, c_int, P, c_int, PLazy, PBnG, P],
+    "edet_conv1x1_dgrad_sesum": [c_int, P, c_int, PPyr, c_int, P, c_int, P, c_int, PLazy, P, P],
     "edet_conv1x1_wgrad": [c_int, PLazy, PPyr, c_int, P, c_int, c_int, P, P, P],
     "edet_dwconv_fwd": [c_int, PLazy, PPyr, c_int, c_int, c_int, P, P, PPyr, PStat, P],
     "edet_dwconv_dgrad": [c_int, P, PPyr, c_int, c_int, c_int, P, P, PPyr, c_int, P],

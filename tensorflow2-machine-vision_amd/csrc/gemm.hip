@@ -29,6 +29,8 @@ struct GemmArgs {
   edet_pyramid pyr;
   edet_statout stats;  // BN statistics of y, or (FOLD) the folded sums: sum <- dbeta, sq <- dgamma
   edet_lazy fx;        // FOLD: the value whose gradient y is (raw x, BN, act; no gate)
+  double* se5;         // FOLD == 2: [5][se_batch][N] per-image SE / BN-backward sums (k_gate_bn_reduce's)
+  int se_batch;
   int lda, ldb, ldc, M, K, N;
   int accumulate, has_stats, ntm, ntn;
 };
@@ -133,7 +135,11 @@ __host__ __device__ __forceinline__ int gemm_gate_imgs(int BM, int hw, int batch
 // pipelined: chunk k+1 is fetched global -> registers while chunk k's MFMAs run, LDS is
 // double-buffered, one barrier per chunk (the unpipelined loop exposed the full load latency
 // 36 times per tile: 150 GB/s at M = 8192).  B is the [N][K] weight (k contiguous).
-template <typename T, int BM, int BN, int KC, bool LAZY, bool FOLD = false>
+// FOLD == 1: the BN-backward fold above.  FOLD == 2 (edet_conv1x1_dgrad_sesum, the MBConv
+// project conv's dgrad): y = d(value) of the SE-gated v = swish(bn(x)) * gate, and the epilogue
+// takes k_gate_bn_reduce's five per-image sums from the stored y and the x tile (a tile lies in
+// one image: the host requires H*W % BM == 0), flushed as fp64 atomics per (sum, image, column)
+template <typename T, int BM, int BN, int KC, bool LAZY, int FOLD = 0>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   constexpr int KV = KC / 8, LDK = KC + 8;
@@ -151,7 +157,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   T* Cs = reinterpret_cast<T*>(smem_ab);
   T* Xs = Cs + BM * LDC_S;         // FOLD
   __shared__ float4 ftab[FOLD ? BN : 1];
-  __shared__ float red[2][2][BN];  // [sum|sq][wm][col]: one writer each, summed in fixed order
+  __shared__ float red[FOLD == 2 ? 5 : 2][2][BN];  // [sum|sq (5 SE sums)][wm][col]: one writer each
   extern __shared__ float2 xf[];   // [K] lazy affine per input channel, then [images][K] gate rows
   float* gts = reinterpret_cast<float*>(xf + (LAZY ? g.K : 0));
 
@@ -379,7 +385,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         const int rl = wm * WM + i * 16 + (lane >> 4) * 4 + r, row = row0 + rl;
         const float v = acc[i][j][r] + bv;
         Cs[rl * LDC_S + cl] = from_f<T>(v);
-        if (!FOLD && row < g.M && col < g.N && row < seg_end) { ssum[j] += v; ssq[j] += v * v; }
+        if (FOLD == 0 && row < g.M && col < g.N && row < seg_end) { ssum[j] += v; ssq[j] += v * v; }
       }
     }
   }
@@ -394,7 +400,37 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     }
   }
   __syncthreads();
-  if constexpr (FOLD) {  // sums of the stored (rounded) values, in the statistics' layout
+  float se[FOLD == 2 ? 5 : 1][FOLD == 2 ? FN : 1];
+  if constexpr (FOLD == 2) {  // k_gate_bn_reduce's terms of the stored (rounded) y, same formulas
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) se[q][j] = 0.f;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int cl = wn * WN + j * 16 + (lane & 15), col = col0 + cl;
+      const float4 t = ftab[cl];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rl = wm * WM + i * 16 + (lane >> 4) * 4 + r, row = row0 + rl;
+          const float k = (row < g.M && col < g.N && row < seg_end) ? 1.f : 0.f;
+          const float xv = to_f<T>(Xs[rl * LDC_S + cl]);
+          const float uu = xv * t.x + t.y;
+          const float sg = sigmoidf_(uu);
+          const float sw = uu * sg, dsw = sg * (1.f + uu * (1.f - sg)) * k;
+          const float xh = (xv - t.z) * t.w;
+          const float dd = to_f<T>(Cs[rl * LDC_S + cl]) * k;
+          se[0][j] += dd * sw;
+          se[1][j] += dd * dsw;
+          se[2][j] += dsw;
+          se[3][j] += dd * dsw * xh;
+          se[4][j] += dsw * xh;
+        }
+      }
+    }
+  } else if constexpr (FOLD == 1) {  // sums of the stored (rounded) values, in the statistics' layout
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int cl = wn * WN + j * 16 + (lane & 15), col = col0 + cl;
@@ -426,6 +462,23 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         acc8m(C + (size_t)row * g.ldc + col, g.N - col, vals, g.accumulate);
       }
     }
+  }
+  if constexpr (FOLD == 2) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const float v = row4_sum(se[q][j]);
+        if (lane < 16) red[q][wm][wn * WN + j * 16 + lane] = v;
+      }
+    __syncthreads();
+    const int n = (row0 - seg_off) / hw;
+    for (int e = tid; e < 5 * BN; e += 256) {
+      const int q = e / BN, i = e - q * BN, col = col0 + i;
+      if (col < g.N && row0 < g.M)
+        stat_add(g.se5 + ((size_t)q * g.se_batch + n) * g.N + col, (double)(red[q][0][i] + red[q][1][i]));
+    }
+    return;
   }
   if (g.has_stats) {
 #pragma unroll
@@ -2044,7 +2097,7 @@ static int dispatch_gemm_s(const GemmArgs& g, hipStream_t s, bool& done) {
 }
 
 // ------------------------------------------------------------------ launch helpers
-template <typename T, int BM, int BN, bool LAZY, int KC = 32, bool FOLD = false>
+template <typename T, int BM, int BN, bool LAZY, int KC = 32, int FOLD = 0>
 static int launch_gemm(GemmArgs g, hipStream_t s) {
   g.ntm = cdiv(g.M, BM);
   g.ntn = cdiv(g.N, BN);
@@ -2092,12 +2145,12 @@ static int launch_gemm_r(GemmArgs g, hipStream_t s) {
 }
 
 // K > 512 with one full-N tile (N <= 320): streaming K loop
-template <typename T, bool LAZY, bool FOLD = false>
+template <typename T, bool LAZY, int FOLD = 0>
 static int dispatch_gemm_kloop(GemmArgs g, hipStream_t s) {
   const int NP = cdiv(g.N, 32) * 32;
   // BM = 32 when 64-row tiles would leave the chip under-filled (and for the fp32 fold, whose
   // staged C and x tiles at 64 x 320 would not fit the LDS)
-  constexpr bool only32 = FOLD && sizeof(T) == 4;
+  constexpr bool only32 = FOLD != 0 && sizeof(T) == 4;
   if (only32 || cdiv(g.M, 64) < 512) {
     if (NP <= 64) return launch_gemm<T, 32, 64, LAZY, 32, FOLD>(g, s);
     if (NP <= 96) return launch_gemm<T, 32, 96, LAZY, 32, FOLD>(g, s);
@@ -2319,6 +2372,37 @@ int edet_conv1x1_dgrad_fold(int dtype, const void* dy, int lddy, const edet_pyra
   g.fx = *xv;
   hipStream_t s = (hipStream_t)stream;
   EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_dgrad_fold<T>(g, s); });
+}
+
+int edet_conv1x1_dgrad_sesum(int dtype, const void* dy, int lddy, const edet_pyramid* rows, int N,
+                             const void* wkn, int K, void* dx, int lddx, const edet_lazy* yv, double* sums5,
+                             edet_stream_t stream) {
+  EDET_REQUIRE(dy && rows && wkn && dx && yv && yv->x && sums5, "conv1x1_dgrad_sesum: null argument");
+  EDET_REQUIRE(lddy % 8 == 0 && K % 8 == 0 && N > 0 && lddx % 8 == 0 && yv->ld % 8 == 0,
+               "conv1x1_dgrad_sesum: need lddy, K, lddx, y->ld multiples of 8");
+  EDET_REQUIRE(yv->bn.enabled && yv->act == EDET_ACT_SWISH && rows->nseg == 1 && K <= 2048,
+               "conv1x1_dgrad_sesum: needs swish(bn(y)) on one segment, C <= 2048");
+  const int B = rows->batch, HW = rows->H[0] * rows->W[0];
+  edet_lazy y = *yv;
+  y.gate = nullptr;  // the sums are of the pre-gate value's terms (k_gate_bn_reduce)
+  // Route: the project dgrads the wave-streaming GEMM takes (GEMM K <= 32, N <= 160: the
+  // stage 0-1 convs) and planes whose tiles could straddle images keep the separate pass
+  const bool narrow = dtype == EDET_BF16 && N <= 32 && K <= 160;
+  if (narrow || HW % 64 != 0 || rows->row_off[0] != 0) {
+    int rc = edet_conv1x1_dgrad(dtype, dy, lddy, rows, N, wkn, K, dx, lddx, 0, stream);
+    if (rc) return rc;
+    return edet_gate_bn_reduce(dtype, &y, B, HW, K, dx, sums5, stream);
+  }
+  GemmArgs g{};
+  g.a = dy; g.b = wkn; g.c = dx; g.bias = nullptr; g.pyr = *rows;
+  g.lda = lddy; g.ldb = cdiv(N, 8) * 8; g.ldc = lddx;
+  g.M = pyr_total_rows(*rows); g.K = N; g.N = K;  // GEMM K = conv out channels
+  g.accumulate = 0;
+  g.has_stats = 0;
+  g.fx = y;
+  g.se5 = sums5; g.se_batch = B;
+  hipStream_t s = (hipStream_t)stream;
+  EDET_DTYPE_DISPATCH(dtype, T, { return dispatch_gemm_kloop<T, false, 2>(g, s); });
 }
 
 int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, int K,

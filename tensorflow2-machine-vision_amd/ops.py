@@ -52,7 +52,10 @@ def _value_grad_tables(eng: Engine, out: Act, rec: GradRec):
         se = out.se
         B = out.pyr.batch
         HW = out.pyr.H * out.pyr.W
-        if fused_se:
+        if fused_se and rec.se_sums is not None:  # taken by the dgrad that wrote dv
+            sums5 = rec.se_sums
+            dgate = sums5[0]
+        elif fused_se:
             sums5 = eng.zeros64(5, B, out.C)
             L.call("edet_gate_bn_reduce", eng.dt, lz, B, HW, out.C, vp(rec.t), vp(sums5), s)
             dgate = sums5[0]
@@ -175,6 +178,16 @@ def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optio
                    vp(P.grad(bname) if bname else None), stream())
         s = stream()
         dx, acc = eng.tape.dst(x)
+        src = x.se_source
+        if (SESUM_DGRAD and src is not None and acc == 0 and x.uses == 1 and src.bns is not None
+                and len(src.bns) == 1 and src.act == L.ACT_SWISH and src.C == K and K <= 2048):
+            # x is the materialised SE-gated depthwise output: its backward sums (the gate
+            # gradient and the BN terms, edet_gate_bn_reduce's) come from this dgrad's epilogue
+            sums5 = eng.zeros64(5, x.pyr.batch, K)
+            L.call("edet_conv1x1_dgrad_sesum", eng.dt, vp(d), ld, x.pyr.c, N, vp(P.wtv(wname)), K, vp(dx), K,
+                   src.lazy(), vp(sums5), s)
+            eng.tape.g[x].se_sums = sums5
+            return
         fold = _fold_dst(eng, x, acc) if FOLD_GEMM_BN else None
         if fold is not None:
             L.call("edet_conv1x1_dgrad_fold", eng.dt, vp(d), ld, x.pyr.c, N, vp(P.wtv(wname)), K, vp(dx), K, x.lazy(),
@@ -201,9 +214,12 @@ FOLD_DWS2_BN = os.environ.get("EDET_FOLD_DWS2_BN", "1") != "0"
 # the stride-1 SE-gated depthwise output's BN-backward apply inside the fused backward's dy
 # staging (edet_dwconv_bwd_lazy) instead of its own pass
 LAZY_DY_DW = os.environ.get("EDET_LAZY_DY", "1") != "0"
+# the SE-gated depthwise output's backward sums in the project conv's dgrad epilogue
+# (edet_conv1x1_dgrad_sesum) instead of edet_gate_bn_reduce's pass over (y, dv)
+SESUM_DGRAD = os.environ.get("EDET_SESUM_DGRAD", "1") != "0"
 # every switch that takes a BN-backward pass into the kernel producing or consuming the gradient
 # (the test of the folds flips them all: tests/test_model_gpu.py::test_bn_backward_folds_equal_unfused_path)
-FOLD_SWITCHES = ("FUSED_DW_BWD", "FOLD_DW_BN", "FOLD_GEMM_BN", "FOLD_DWS2_BN", "LAZY_DY_DW")
+FOLD_SWITCHES = ("FUSED_DW_BWD", "FOLD_DW_BN", "FOLD_GEMM_BN", "FOLD_DWS2_BN", "LAZY_DY_DW", "SESUM_DGRAD")
 
 
 def _fold_dst(eng: Engine, x: Act, acc: int):
@@ -310,12 +326,14 @@ def materialize(eng: Engine, x: Act, name: str = "") -> Act:
     y = eng.empty(x.pyr.rows, x.C)
     L.call("edet_lazy_materialize", eng.dt, x.lazy(), x.pyr.c, x.C, vp(y), stream())
     out = Act(y, x.pyr, x.C, training=eng.training, name=name)
+    if x.se is not None:
+        out.se_source = x
 
     def bwd():
         rec = eng.tape.take(out)
         if rec is None:
             return
-        eng.tape.alias(x, rec.t, rec.ld, rec.scale)
+        eng.tape.alias(x, rec.t, rec.ld, rec.scale, se_sums=rec.se_sums)
 
     eng.record(bwd)
     return out

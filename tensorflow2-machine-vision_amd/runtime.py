@@ -114,7 +114,7 @@ class SERec:
 class Act:
     """Raw activation buffer + pending transform v = act(bn(raw)) * gate."""
 
-    __slots__ = ("raw", "pyr", "C", "ld", "bns", "act", "gate", "se", "training", "name", "_lz", "uses")
+    __slots__ = ("raw", "pyr", "C", "ld", "bns", "act", "gate", "se", "training", "name", "_lz", "uses", "se_source")
 
     def __init__(self, raw: torch.Tensor, pyr: Pyr, C: int, bns: Optional[List[BNParam]] = None,
                  act: int = L.ACT_NONE, ld: Optional[int] = None, training: bool = False,
@@ -129,6 +129,9 @@ class Act:
         self.training, self.name = training, name
         self._lz = None
         self.uses = 0  # forward ops that will send a gradient into this value (consume())
+        # a plain copy of an SE-gated value (ops.materialize): that value's Act, whose backward
+        # sums the consumer's dgrad may take in its epilogue (edet_conv1x1_dgrad_sesum)
+        self.se_source = None
 
     def consume(self) -> "Act":
         """Count a training-mode consumer: a backward that owns the whole gradient of the
@@ -389,13 +392,16 @@ def _init_values(sp: ParamSpec, rng: np.random.Generator) -> np.ndarray:
 
 # --------------------------------------------------------------------------- tape
 class GradRec:
-    __slots__ = ("t", "ld", "scale", "bn_sums")
+    __slots__ = ("t", "ld", "scale", "bn_sums", "se_sums")
 
     def __init__(self, t: torch.Tensor, ld: int, scale: Optional[torch.Tensor] = None):
         self.t, self.ld, self.scale = t, ld, scale
         # fp64 [2][nseg][C] (dgamma, dbeta) BN-backward sums of the value's BatchNorm, already
         # accumulated by the kernel that wrote t (edet_dwconv_bwd's fold); None: not yet
         self.bn_sums = None
+        # fp64 [5][B][C] SE-gated value sums (edet_gate_bn_reduce's), taken by the kernel that
+        # wrote t (edet_conv1x1_dgrad_sesum); None: not yet
+        self.se_sums = None
 
 
 class Tape:
@@ -423,9 +429,10 @@ class Tape:
         self.g[act] = GradRec(t, act.C)
         return t, 0
 
-    def alias(self, act: Act, t: torch.Tensor, ld: int, scale=None):
+    def alias(self, act: Act, t: torch.Tensor, ld: int, scale=None, se_sums=None):
         assert act not in self.g, f"grad of {act} already exists"
         self.g[act] = GradRec(t, ld, scale)
+        self.g[act].se_sums = se_sums
 
     def take(self, act: Act) -> Optional[GradRec]:
         rec = self.g.pop(act, None)

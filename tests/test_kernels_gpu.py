@@ -321,6 +321,46 @@ def test_dwconv_bwd_fused(dt, k, H, W, C, act, nseg, fold, acc):
 
 
 @pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("B,H,W,N,K", [(4, 16, 16, 192, 1152), (2, 32, 32, 80, 480), (3, 8, 8, 40, 144),
+                                       (2, 32, 32, 112, 672), (5, 16, 16, 320, 1152),
+                                       # the separate-pass routes: a narrow dgrad, a 7 x 7 plane
+                                       (2, 16, 16, 24, 144), (3, 7, 7, 80, 480)])
+def test_conv1x1_dgrad_sesum_equals_dgrad_then_gate_bn_reduce(dt, B, H, W, N, K):
+    """edet_conv1x1_dgrad_sesum (the project conv's dgrad with the SE-gated depthwise output's
+    five per-image backward sums in its epilogue) against the two passes it replaces:
+    edet_conv1x1_dgrad, then edet_gate_bn_reduce over (y, dv = dx)."""
+    rng = np.random.default_rng(B * 100 + N + K)
+    pyr = Pyr(B, [(H, W)])
+    M = pyr.rows
+    dy = g(rnd(rng, M, N), dt)
+    w = g(rnd(rng, N, K, scale=1 / math.sqrt(N)), dt)
+    ldn = (N + 7) // 8 * 8
+    wkn = torch.zeros(K, ldn)
+    wkn[:, :N] = w.float().cpu().t()
+    wkn = g(wkn, dt)
+    y = pyr_data(rng, pyr, K, dt, scale=1.5)
+    lzy = LazyDesc(y, pyr, K, bn=make_bn(y, pyr, K, rng), act=1, gate=g(torch.rand(B, K) + 0.5, "f32"))
+    dx1 = torch.empty(M, K, dtype=TDT[dt], device=DEV)
+    L.call("edet_conv1x1_dgrad", DT[dt], vp(dy), N, pyr.c, N, vp(wkn), K, vp(dx1), K, 0, stream())
+    s1 = zeros64(5, B, K)
+    L.call("edet_gate_bn_reduce", DT[dt], lzy.c, B, H * W, K, vp(dx1), vp(s1), stream())
+    dx2 = torch.empty(M, K, dtype=TDT[dt], device=DEV)
+    s2 = zeros64(5, B, K)
+    L.call("edet_conv1x1_dgrad_sesum", DT[dt], vp(dy), N, pyr.c, N, vp(wkn), K, vp(dx2), K, lzy.c, vp(s2), stream())
+    torch.cuda.synchronize()
+    close(dx2, dx1.double(), dt, rtol=1e-5 if dt == "f32" else 8e-3, atol=1e-5 if dt == "f32" else 8e-3)
+    # the sums of (slightly) different dx roundings in bf16: compare against the fp64 sums of
+    # each kernel's own dx, then the two paths against each other at the fp32-order level
+    ref2 = zeros64(5, B, K)
+    L.call("edet_gate_bn_reduce", DT[dt], lzy.c, B, H * W, K, vp(dx2), vp(ref2), stream())
+    torch.cuda.synchronize()
+    for q in range(5):
+        close(s2[q], ref2[q], "f32", rtol=1e-4, atol=1e-4 * (H * W) ** 0.5 * float(ref2[q].abs().max() + 1e-30) / 4)
+        if dt == "f32":
+            close(s2[q], s1[q], "f32", rtol=1e-4, atol=1e-4 * (H * W) ** 0.5 * float(s1[q].abs().max() + 1e-30) / 4)
+
+
+@pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("k,H,W,C,B,fold,acc,yact,gate,dsq", [
     (3, 16, 16, 32, 2, True, 0, 1, 1, 1), (5, 11, 12, 48, 2, True, 0, 1, 1, 1), (5, 9, 9, 1152, 2, True, 0, 1, 1, 1),
     (3, 17, 20, 144, 3, False, 1, 1, 1, 1), (3, 40, 33, 96, 2, True, 0, 1, 1, 0), (5, 32, 32, 240, 4, True, 0, 0, 0, 1),
