@@ -226,8 +226,9 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
     for (int j = 0; j < DTS; ++j) {
       otile[(r * DTS + j) * DCB + c] = from_f<T>(acc[j]);
       if (oy < OH && ox0 + j < OW && cvalid) {
-        s += acc[j];
-        q += acc[j] * acc[j];
+        const float vs = stored<T>(acc[j]);
+        s += vs;
+        q += vs * vs;
       }
     }
     __syncthreads();
@@ -634,7 +635,11 @@ __global__ __launch_bounds__(256) void k_dw3(DwArgs g) {
 #pragma unroll
       for (int j = 0; j < DTS; ++j) {
         otile[(r * DTS + j) * DCB + c] = from_f<T>(o[j]);
-        if (oy < OH && tx * DTS + j < OW && cvalid) { s += o[j]; q += o[j] * o[j]; }
+        if (oy < OH && tx * DTS + j < OW && cvalid) {
+          const float vs = stored<T>(o[j]);
+          s += vs;
+          q += vs * vs;
+        }
       }
       __syncthreads();
       {
@@ -769,7 +774,11 @@ __global__ __launch_bounds__(256) void k_dw2_fwd(DwArgs g, DwGeom geo) {
         }
         st8(Y + ((size_t)g.pout.row_off[seg] + p) * C + c, acc);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { s[j] += acc[j]; q[j] += acc[j] * acc[j]; }
+        for (int j = 0; j < 8; ++j) {
+          const float vs = stored<T>(acc[j]);
+          s[j] += vs;
+          q[j] += vs * vs;
+        }
       }
     }
     if (g.has_stats) {  // fixed-order block reduction, one fp64 atomic per channel
@@ -1389,8 +1398,9 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
           const T ov = from_f<T>(o[p][t]);
           ost[j & 1][(p * TW + gc * CPG + t) * DCB + c] = ov;
           if (rowok && cvalid && ox0 + gc * CPG + t < OW) {
-            s += o[p][t];
-            q += o[p][t] * o[p][t];
+            const float vs = to_f<T>(ov);
+            s += vs;
+            q += vs * vs;
             // the squeeze reads y as stored, as edet_se_squeeze would
             if constexpr (SQ) z += lazy_apply(to_f<T>(ov), ya, g.yv.act);
           }

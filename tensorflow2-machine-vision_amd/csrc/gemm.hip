@@ -383,9 +383,16 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rl = wm * WM + i * 16 + (lane >> 4) * 4 + r, row = row0 + rl;
-        const float v = acc[i][j][r] + bv;
+        float v = acc[i][j][r] + bv;
+        // accumulate: the old value is added before the one rounding to the storage type
+        // (staging round(v) and adding it to the old value later rounded twice)
+        if (g.accumulate && row < g.M && col < g.N) v += to_f<T>(((const T*)g.c)[(size_t)row * g.ldc + col]);
         Cs[rl * LDC_S + cl] = from_f<T>(v);
-        if (FOLD == 0 && row < g.M && col < g.N && row < seg_end) { ssum[j] += v; ssq[j] += v * v; }
+        if (FOLD == 0 && row < g.M && col < g.N && row < seg_end) {
+          const float vs = stored<T>(v);
+          ssum[j] += vs;
+          ssq[j] += vs * vs;
+        }
       }
     }
   }
@@ -459,7 +466,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         const T* src = Cs + rl * LDC_S + cv;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) vals[jj] = to_f<T>(src[jj]);
-        acc8m(C + (size_t)row * g.ldc + col, g.N - col, vals, g.accumulate);
+        acc8m(C + (size_t)row * g.ldc + col, g.N - col, vals, 0);  // (accumulated at staging)
       }
     }
   }
@@ -762,8 +769,15 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
         for (int r = 0; r < 4; ++r) {
           const int rl = wm * WM + i * 16 + (lane >> 4) * 4 + r;
           const float v = acc[i][j][r] + bv;
-          if (col - cbase < LDC) Cs[rl * LDC + col - cbase] = from_f<T>(v);
-          if (row0 + rl < seg_end && col < N) { s += v; q += v * v; }
+          // accumulate: the old value joins before the one rounding (see k_gemm)
+          const float va = (g.accumulate && row0 + rl < g.M && col < N)
+                               ? v + to_f<T>(((const T*)g.c)[(size_t)(row0 + rl) * g.ldc + col]) : v;
+          if (col - cbase < LDC) Cs[rl * LDC + col - cbase] = from_f<T>(va);
+          if (row0 + rl < seg_end && col < N) {
+            const float vs = stored<T>(v);
+            s += vs;
+            q += vs * vs;
+          }
         }
       if (g.has_stats) {
         s = row4_sum(s);
@@ -791,11 +805,12 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
       const T* src = Cs + v * 8;
       if constexpr (sizeof(T) == 2) {
         uint4 raw = *reinterpret_cast<const uint4*>(src);
-        if (!g.accumulate) { *reinterpret_cast<uint4*>(dst + v * 8) = raw; continue; }
+        *reinterpret_cast<uint4*>(dst + v * 8) = raw;  // (accumulated at staging)
+        continue;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) vals[j] = to_f<T>(src[j]);
-      acc8m(dst + v * 8, 8, vals, g.accumulate);
+      acc8m(dst + v * 8, 8, vals, 0);
     }
   } else {
     const int cv8 = cdiv(ncols, 8);
@@ -808,9 +823,9 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
       for (int j = 0; j < 8; ++j) vals[j] = to_f<T>(Cs[r * LDC + cv + j]);
       T* dst = C + (size_t)(row0 + r) * g.ldc + cbase + cv;
       if (vec_ok) {
-        acc8m(dst, nn, vals, g.accumulate);
+        acc8m(dst, nn, vals, 0);  // (accumulated at staging)
       } else {
-        for (int j = 0; j < 8 && j < nn; ++j) dst[j] = from_f<T>(g.accumulate ? to_f<T>(dst[j]) + vals[j] : vals[j]);
+        for (int j = 0; j < 8 && j < nn; ++j) dst[j] = from_f<T>(vals[j]);
       }
     }
   }
@@ -1562,8 +1577,15 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
         for (int r = 0; r < 4; ++r) {
           const int rl = i * 16 + (lane >> 4) * 4 + r;
           const float v = acc[i][j][r] + bv;
-          cw[rl * CWLD + j * 16 + (lane & 15)] = from_f<T>(v);
-          if (wrow0 + rl < seg_end) { s += v; q += v * v; }
+          // accumulate: the old value joins before the one rounding (see k_gemm)
+          const int grw = wrow0 + rl, gcl = col_base + cl;
+          const float va = (g.accumulate && grw < M && gcl < N) ? v + to_f<T>(C[(size_t)grw * g.ldc + gcl]) : v;
+          cw[rl * CWLD + j * 16 + (lane & 15)] = from_f<T>(va);
+          if (wrow0 + rl < seg_end) {
+            const float vs = stored<T>(v);
+            s += vs;
+            q += vs * vs;
+          }
         }
       if (g.has_stats) {
         s = row4_sum(s);
@@ -1587,7 +1609,7 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
         const T* src = cw + rr * CWLD + cv;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) vals[jj] = to_f<T>(src[jj]);
-        acc8m(C + (size_t)grow * g.ldc + gcol, N - gcol, vals, g.accumulate);
+        acc8m(C + (size_t)grow * g.ldc + gcol, N - gcol, vals, 0);  // (accumulated at staging)
       }
     }
   };
@@ -1963,8 +1985,9 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
           fold_terms(bf2f(f2bf(v[r])), xf_, ftab[n0 + r], g.fx.act, du, dux);
           if (live && n0 + r < N) { ss[f][r] += du; sq[f][r] += dux; }
         } else if (live) {
-          ss[f][r] += v[r];
-          sq[f][r] += v[r] * v[r];
+          const float vs = bf2f(f2bf(v[r]));  // the stored value
+          ss[f][r] += vs;
+          sq[f][r] += vs * vs;
         }
       }
       *reinterpret_cast<uint2*>(cw + (lane & 15) * LDW + n0) =

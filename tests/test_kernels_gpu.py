@@ -93,7 +93,9 @@ def test_conv1x1_dgrad(dt, M, N, K, ldy):
     dx = g(torch.full((M, K), 0.5), dt)
     L.call("edet_conv1x1_dgrad", DT[dt], vp(dy), ldy, pyr.c, N, vp(wkn), K, vp(dx), K, 1, stream())
     ref = dy[:, :N].double().cpu() @ w.double().cpu() + 0.5
-    close(dx, ref, dt)
+    # accumulate rounds (old + dy W) once to the storage type (the bf16 bar
+    # is one bf16 rounding, 2^-9 relative, with room for the fp32 accumulation order)
+    close(dx, ref, dt, **({} if dt == "f32" else dict(rtol=5e-3, atol=5e-3)))
 
 
 @pytest.mark.parametrize("dt", DTS)
