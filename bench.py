@@ -82,9 +82,15 @@ def algorithmic_bytes(name, args, es):
     if name == "edet_conv1x1_dgrad_fold":  # dy, x of the folded value, dx
         p, N, K = args[3], args[4], args[6]
         return rows(p) * (N + 2 * K) * es + K * N * es
-    if name == "edet_dwconv_dgrad_fold":  # dy, x, dx
-        pout, C, pin = args[2], args[3], args[8]
+    if name == "edet_dwconv_dgrad_fold":  # dy, x, dx (the caller takes this entry only where it
+        pout, C, pin = args[2], args[3], args[8]  # launches the folded kernel: ops._dgrad_fold_kernel_route)
         return (rows(pout) + 2 * rows(pin)) * C * es
+    if name == "edet_conv1x1_dgrad_sesum":  # dy, W, the gated value's raw y, dx
+        p, N, K = args[3], args[4], args[6]
+        return rows(p) * (N + 2 * K) * es + K * N * es
+    if name == "edet_dwconv_bwd_lazy":  # (dtype, lz, pin, C, k, dyl, pout, w, dx, acc, dw, fold, s): dv, y, x, dx
+        pin, C, acc = args[2], args[3], args[9]
+        return rows(pin) * (4 + acc) * C * es
     if name == "edet_conv1x1_wgrad":
         p, K, N = args[2], args[3], args[6]
         return rows(p) * (K + N) * es
@@ -168,6 +174,10 @@ def shape_tag(name, args):
             return f"M={rows(args[3])} N={args[4]} K={args[6]} fold"
         if name == "edet_dwconv_dgrad_fold":
             return f"out={rows(args[2])} C={args[3]} k={args[4]} s={args[5]} fold"
+        if name == "edet_conv1x1_dgrad_sesum":
+            return f"M={rows(args[3])} N={args[4]} K={args[6]} sesum"
+        if name == "edet_dwconv_bwd_lazy":
+            return f"in={rows(args[2])} C={args[3]} k={args[4]} lazy-dy" + (" fold" if args[11] else "")
         if name in ("edet_lazy_bwd_reduce", "edet_lazy_bwd_apply", "edet_lazy_materialize"):
             return f"M={rows(args[2])} C={args[3]} {lazy(args[1])}"
     except Exception:  # noqa: BLE001

@@ -180,7 +180,8 @@ def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optio
         dx, acc = eng.tape.dst(x)
         src = x.se_source
         if (SESUM_DGRAD and src is not None and acc == 0 and x.uses == 1 and src.bns is not None
-                and len(src.bns) == 1 and src.act == L.ACT_SWISH and src.C == K and K <= 2048):
+                and len(src.bns) == 1 and src.act == L.ACT_SWISH and src.C == K and K <= 2048
+                and _sesum_epilogue_route(eng, x.pyr, N, K)):
             # x is the materialised SE-gated depthwise output: its backward sums (the gate
             # gradient and the BN terms, edet_gate_bn_reduce's) come from this dgrad's epilogue
             sums5 = eng.zeros64(5, x.pyr.batch, K)
@@ -220,6 +221,22 @@ SESUM_DGRAD = os.environ.get("EDET_SESUM_DGRAD", "1") != "0"
 # every switch that takes a BN-backward pass into the kernel producing or consuming the gradient
 # (the test of the folds flips them all: tests/test_model_gpu.py::test_bn_backward_folds_equal_unfused_path)
 FOLD_SWITCHES = ("FUSED_DW_BWD", "FOLD_DW_BN", "FOLD_GEMM_BN", "FOLD_DWS2_BN", "LAZY_DY_DW", "SESUM_DGRAD")
+
+
+def _sesum_epilogue_route(eng: Engine, pyr: Pyr, N: int, K: int) -> bool:
+    """edet_conv1x1_dgrad_sesum takes the sums in its K-loop epilogue for these shapes (its
+    route rule, include/edet.h); elsewhere it would run dgrad + edet_gate_bn_reduce itself, so
+    the caller keeps the two passes as separate calls (one kernel per entry point: the bench
+    attributes each call's time and bytes to the kernel it launched)."""
+    narrow = eng.dt == L.BF16 and N <= 32 and K <= 160
+    return pyr.nseg == 1 and not narrow and (pyr.H * pyr.W) % 64 == 0 and pyr.row_off[0] == 0
+
+
+def _dgrad_fold_kernel_route(k: int, pin: Pyr) -> bool:
+    """edet_dwconv_dgrad_fold runs its folded kernel for k3 over >= 2^20 input rows (its route,
+    dwconv.hip); elsewhere it runs dgrad + the reduce itself, so the caller makes them separate
+    calls (one kernel per entry point)."""
+    return k == 3 and sum(pin.seg_rows(s) for s in range(pin.nseg)) >= (1 << 20)
 
 
 def _fold_dst(eng: Engine, x: Act, acc: int):
@@ -284,7 +301,7 @@ def dwconv(eng: Engine, P: ParamStore, x: Act, wname: str, k: int, stride: int,
                    stream())
         s = stream()
         dx, acc = eng.tape.dst(x)
-        fold = _fold_dst(eng, x, acc) if FOLD_DWS2_BN else None
+        fold = _fold_dst(eng, x, acc) if FOLD_DWS2_BN and _dgrad_fold_kernel_route(k, x.pyr) else None
         if fold is not None:
             L.call("edet_dwconv_dgrad_fold", eng.dt, vp(d), pout.c, C, k, stride, vp(P.wcv(wname)), vp(dx), x.pyr.c,
                    x.lazy(), fold, s)
