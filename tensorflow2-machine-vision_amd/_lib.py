@@ -156,7 +156,12 @@ class _Lib:
         self.path = path
         self.dll = ctypes.CDLL(path)
         self.fns = {}
+        # EDET_ALLOW_MISSING=1 (same-box A/B against an older build of the same ABI only): entry
+        # points the library lacks are left unbound instead of failing the import
+        allow_missing = os.environ.get("EDET_ALLOW_MISSING") == "1"
         for name, argtypes in SIGNATURES.items():
+            if allow_missing and not hasattr(self.dll, name):
+                continue
             fn = getattr(self.dll, name)
             fn.argtypes = argtypes
             fn.restype = _RESTYPE.get(name, c_int)

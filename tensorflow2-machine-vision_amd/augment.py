@@ -182,7 +182,7 @@ def augment_one(img: np.ndarray, lab: dict, d: AugmentDraw, size: Tuple[int, int
     if len(classes) == 0:
         return None
     dev = out_b.device
-    src = torch.from_numpy(np.ascontiguousarray(img, np.uint8)).to(dev)
+    src = torch.from_numpy(np.array(img, dtype=np.uint8, order="C", copy=True)).to(dev)
     scratch = torch.empty(2 * h * w * 3, dtype=torch.uint8, device=dev)
     p = aug_params(d, inv, place, L)
     L.call("edet_augment_image", dtype_code, vp(src), h, w, p, vp(scratch), vp(out_b), size[1], size[0], stream())
