@@ -62,10 +62,6 @@ template <typename T> __device__ __forceinline__ T from_f(float v);
 template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
 template <> __device__ __forceinline__ uint16_t from_f<uint16_t>(float v) { return f2bf(v); }
 
-// the value as the storage type holds it: BN statistics are taken of the stored (rounded)
-// outputs, the values their consumers normalise (identity for fp32 storage)
-template <typename T> __device__ __forceinline__ float stored(float v) { return to_f<T>(from_f<T>(v)); }
-
 // 8 contiguous elements -> fp32 (pointer 16-B aligned)
 __device__ __forceinline__ void ld8(const float* p, float* o) {
   float4 a = *reinterpret_cast<const float4*>(p);

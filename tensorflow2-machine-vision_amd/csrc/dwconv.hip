@@ -226,9 +226,8 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
     for (int j = 0; j < DTS; ++j) {
       otile[(r * DTS + j) * DCB + c] = from_f<T>(acc[j]);
       if (oy < OH && ox0 + j < OW && cvalid) {
-        const float vs = stored<T>(acc[j]);
-        s += vs;
-        q += vs * vs;
+        s += acc[j];
+        q += acc[j] * acc[j];
       }
     }
     __syncthreads();
@@ -635,11 +634,7 @@ __global__ __launch_bounds__(256) void k_dw3(DwArgs g) {
 #pragma unroll
       for (int j = 0; j < DTS; ++j) {
         otile[(r * DTS + j) * DCB + c] = from_f<T>(o[j]);
-        if (oy < OH && tx * DTS + j < OW && cvalid) {
-          const float vs = stored<T>(o[j]);
-          s += vs;
-          q += vs * vs;
-        }
+        if (oy < OH && tx * DTS + j < OW && cvalid) { s += o[j]; q += o[j] * o[j]; }
       }
       __syncthreads();
       {
@@ -774,11 +769,7 @@ __global__ __launch_bounds__(256) void k_dw2_fwd(DwArgs g, DwGeom geo) {
         }
         st8(Y + ((size_t)g.pout.row_off[seg] + p) * C + c, acc);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float vs = stored<T>(acc[j]);
-          s[j] += vs;
-          q[j] += vs * vs;
-        }
+        for (int j = 0; j < 8; ++j) { s[j] += acc[j]; q[j] += acc[j] * acc[j]; }
       }
     }
     if (g.has_stats) {  // fixed-order block reduction, one fp64 atomic per channel
@@ -1275,18 +1266,20 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
   // wgrad: the P dy rows of step j; vector e = tid + u*256: row e / (4 TW), pixel, channels
   constexpr int DYV = (P * TW * 4 + 255) / 256;
   uint4 dyr[DYV][WORDS];
-  // range-checked buffer loads: a vector past the rows, the strip or the channels reads zeros
-  // (a select zeroing the loaded value made the compiler wait for every load in flight)
-  const auto rsdy = buf_rsrc(WG ? (const T*)g.dy + obase * C : nullptr, WG ? (long)OH * OW * C * (long)sizeof(T) : 0);
   auto fetch_dy = [&](int j) {
 #pragma unroll
     for (int u = 0; u < DYV; ++u) {
       const int e = tid + u * 256, p = e / (TW * 4), rem = e - p * (TW * 4);
       const int px = rem >> 2, cv = (rem & 3) * 8, oy = oy0 + j * P + p;
       const bool in = p < P && j * P + p < nrows && oy < OH && ox0 + px < OW && c0 + cv < C;
-      const uint32_t off = buf_off(in, (uint32_t)((((size_t)oy * OW + ox0 + px) * C + c0 + cv) * sizeof(T)));
+      const uint4* src = reinterpret_cast<const uint4*>(
+          (const T*)g.dy + (in ? (obase + (size_t)oy * OW + ox0 + px) * C + c0 + cv : 0));
+      dyr[u][0] = src[0];
+      if constexpr (WORDS == 2) dyr[u][1] = src[1];
+      if (!in) {
 #pragma unroll
-      for (int w = 0; w < WORDS; ++w) dyr[u][w] = buf_ld16(rsdy, off + 16 * w);
+        for (int w = 0; w < WORDS; ++w) dyr[u][w] = make_uint4(0, 0, 0, 0);
+      }
     }
   };
   auto commit_dy = [&](int j) {
@@ -1329,36 +1322,30 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
 #pragma unroll
     for (int t = 0; t < K * K; ++t) acc[t] = 0.f;
   }
-  // fwd output rows of step j from stage buffer j & 1 (after a barrier): a compile-time number
-  // of range-checked buffer stores per thread, no branch (a store past the image or the strip
-  // takes an out-of-range offset and is dropped).  The variable-count store loop with its
-  // per-vector branch left the wait-count pass unable to count the stores, so the commit of the
-  // prefetched rows after it waited for every memory operation in flight (vmcnt(0)).
-  constexpr int NSE = (P * TW * 4 + 255) / 256;
-  const auto rsy = buf_rsrc((const T*)g.y + obase * C, (long)OH * OW * C * (long)sizeof(T));
-  auto store_step = [&](int j) {
-#pragma unroll
-    for (int u = 0; u < NSE; ++u) {
-      const int e = tid + u * 256, ev = e < P * TW * 4 ? e : 0;
-      const int p = ev / (TW * 4), rem = ev - p * (TW * 4);
+  auto store_step = [&](int j) {  // fwd output rows of step j from stage buffer j & 1 (after a barrier)
+    for (int e = tid; e < P * TW * 4; e += 256) {
+      const int p = e / (TW * 4), rem = e - p * (TW * 4);
       const int px = rem >> 2, cv = (rem & 3) * 8, oy = oy0 + j * P + p;
-      const bool ok = j >= 0 && e < P * TW * 4 && j * P + p < nrows && ox0 + px < OW && c0 + cv < C;
-      const uint32_t off = buf_off(ok, (uint32_t)((((size_t)oy * OW + ox0 + px) * C + c0 + cv) * sizeof(T)));
-      const uint4* src = reinterpret_cast<const uint4*>(&ost[WG ? 0 : (j & 1)][(p * TW + px) * DCB + cv]);
-#pragma unroll
-      for (int w = 0; w < WORDS; ++w)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, src[w]), rsy, off + 16 * w, 0, 0);
+      if (j * P + p < nrows && ox0 + px < OW && c0 + cv < C) {
+        T* dst = (T*)g.y + (obase + (size_t)oy * OW + ox0 + px) * C + c0 + cv;
+        const T* src = &ost[WG ? 0 : (j & 1)][(p * TW + px) * DCB + cv];
+        if constexpr (sizeof(T) == 2) {
+          *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+        } else {
+          reinterpret_cast<float4*>(dst)[0] = reinterpret_cast<const float4*>(src)[0];
+          reinterpret_cast<float4*>(dst)[1] = reinterpret_cast<const float4*>(src)[1];
+        }
+      }
     }
   };
   auto step = [&](int j, auto& rsj) {
     if constexpr (!WG) {
-      store_step(j - 1);  // (j = 0: every store is out of range)
+      if (j > 0) store_step(j - 1);
     }
-    // rows of step j+1: ring slots and dy buffer step j does not read.  Unconditional (past the
-    // last step they fill slots no step reads): a commit under a branch left the wait-count pass
-    // merging paths, and it waited for the other register set's loads too
-    commit(rsj, rows_of(j + 1), P * S);
-    if constexpr (WG) commit_dy(j + 1);
+    if (j + 1 < nsteps) {  // rows of step j+1: ring slots and dy buffer step j does not read
+      commit(rsj, rows_of(j + 1), P * S);
+      if constexpr (WG) commit_dy(j + 1);
+    }
     // unconditional: a conditional refill joins old and new values in a copy, and the copy
     // waits for the load (rows past the block are real or predicated-off elements)
     fetch(rsj, rows_of(j + 1 + PF), P * S);
@@ -1398,9 +1385,8 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
           const T ov = from_f<T>(o[p][t]);
           ost[j & 1][(p * TW + gc * CPG + t) * DCB + c] = ov;
           if (rowok && cvalid && ox0 + gc * CPG + t < OW) {
-            const float vs = to_f<T>(ov);
-            s += vs;
-            q += vs * vs;
+            s += o[p][t];
+            q += o[p][t] * o[p][t];
             // the squeeze reads y as stored, as edet_se_squeeze would
             if constexpr (SQ) z += lazy_apply(to_f<T>(ov), ya, g.yv.act);
           }
@@ -1435,19 +1421,16 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
     }
     __syncthreads();
   };
-  // PF = 2 runs the steps in pairs with no branch between them: an odd count takes one more
-  // step past the block's rows (its outputs fail the row test of the statistics and the stores)
-  const int nrun = PF == 2 ? (nsteps + 1) & ~1 : nsteps;
   if constexpr (PF == 1) {
     for (int j = 0; j < nsteps; ++j) step(j, rs);
   } else {
-    for (int j = 0; j < nrun; j += 2) {
+    for (int j = 0; j < nsteps; j += 2) {
       step(j, rs);
-      step(j + 1, rs2);
+      if (j + 1 < nsteps) step(j + 1, rs2);
     }
   }
   if constexpr (!WG) {
-    store_step(nrun - 1);
+    store_step(nsteps - 1);
     if (g.has_stats) {  // the ring is free after the last barrier
       float* red = ring;
       red[gc * DCB + c] = s;

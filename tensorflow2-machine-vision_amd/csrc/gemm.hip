@@ -29,10 +29,10 @@ struct GemmArgs {
   edet_pyramid pyr;
   edet_statout stats;  // BN statistics of y, or (FOLD) the folded sums: sum <- dbeta, sq <- dgamma
   edet_lazy fx;        // FOLD: the value whose gradient y is (raw x, BN, act; no gate)
-  double* se5;         // FOLD == 2: [5][se_batch][N] per-image SE / BN-backward sums (k_gate_bn_reduce's)
-  int se_batch;
   int lda, ldb, ldc, M, K, N;
   int accumulate, has_stats, ntm, ntn;
+  double* se5;         // FOLD == 2: [5][se_batch][N] per-image SE / BN-backward sums (k_gate_bn_reduce's)
+  int se_batch;
 };
 
 // BN-backward fold (dgrad epilogues): the output y = d(value) of a lazy value v = act(bn(x)) is
@@ -139,7 +139,11 @@ __host__ __device__ __forceinline__ int gemm_gate_imgs(int BM, int hw, int batch
 // project conv's dgrad): y = d(value) of the SE-gated v = swish(bn(x)) * gate, and the epilogue
 // takes k_gate_bn_reduce's five per-image sums from the stored y and the x tile (a tile lies in
 // one image: the host requires H*W % BM == 0), flushed as fp64 atomics per (sum, image, column)
-template <typename T, int BM, int BN, int KC, bool LAZY, int FOLD = 0>
+// ACC (accumulating dgrads, compile-time: the model's multi-consumer gradients): the C tile is
+// staged in fp32 and the store adds it to the old value, one rounding to the storage type (a
+// staged round(v) added later rounded twice; a runtime accumulate test in the staging loop cost
+// 2-9 us on every K-loop launch, r05c)
+template <typename T, int BM, int BN, int KC, bool LAZY, int FOLD = 0, bool ACC = false>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   constexpr int KV = KC / 8, LDK = KC + 8;
@@ -150,11 +154,12 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   // (FOLD: and the folded value's raw x tile behind it)
   constexpr int LDC_S = BN + 8;
   constexpr int AB_BYTES = 2 * (BM + BN) * LDK * (int)sizeof(T);
-  constexpr int C_BYTES = (FOLD ? 2 : 1) * BM * LDC_S * (int)sizeof(T);
+  constexpr int C_BYTES = (FOLD ? 2 : 1) * BM * LDC_S * (int)(ACC ? sizeof(float) : sizeof(T));
   __shared__ __attribute__((aligned(16))) char smem_ab[AB_BYTES > C_BYTES ? AB_BYTES : C_BYTES];
   T (*As)[BM * LDK] = reinterpret_cast<T (*)[BM * LDK]>(smem_ab);
   T (*Bs)[BN * LDK] = reinterpret_cast<T (*)[BN * LDK]>(smem_ab + 2 * BM * LDK * sizeof(T));
   T* Cs = reinterpret_cast<T*>(smem_ab);
+  float* Cf = reinterpret_cast<float*>(smem_ab);  // ACC: the fp32 C tile
   T* Xs = Cs + BM * LDC_S;         // FOLD
   __shared__ float4 ftab[FOLD ? BN : 1];
   __shared__ float red[FOLD == 2 ? 5 : 2][2][BN];  // [sum|sq (5 SE sums)][wm][col]: one writer each
@@ -383,16 +388,10 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int rl = wm * WM + i * 16 + (lane >> 4) * 4 + r, row = row0 + rl;
-        float v = acc[i][j][r] + bv;
-        // accumulate: the old value is added before the one rounding to the storage type
-        // (staging round(v) and adding it to the old value later rounded twice)
-        if (g.accumulate && row < g.M && col < g.N) v += to_f<T>(((const T*)g.c)[(size_t)row * g.ldc + col]);
-        Cs[rl * LDC_S + cl] = from_f<T>(v);
-        if (FOLD == 0 && row < g.M && col < g.N && row < seg_end) {
-          const float vs = stored<T>(v);
-          ssum[j] += vs;
-          ssq[j] += vs * vs;
-        }
+        const float v = acc[i][j][r] + bv;
+        if constexpr (ACC) Cf[rl * LDC_S + cl] = v;
+        else Cs[rl * LDC_S + cl] = from_f<T>(v);
+        if (FOLD == 0 && row < g.M && col < g.N && row < seg_end) { ssum[j] += v; ssq[j] += v * v; }
       }
     }
   }
@@ -464,9 +463,14 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
       if (row < g.M && col < g.N) {
         float vals[8];
         const T* src = Cs + rl * LDC_S + cv;
+        if constexpr (ACC) {
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) vals[jj] = to_f<T>(src[jj]);
-        acc8m(C + (size_t)row * g.ldc + col, g.N - col, vals, 0);  // (accumulated at staging)
+          for (int jj = 0; jj < 8; ++jj) vals[jj] = Cf[rl * LDC_S + cv + jj];
+        } else {
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) vals[jj] = to_f<T>(src[jj]);
+        }
+        acc8m(C + (size_t)row * g.ldc + col, g.N - col, vals, ACC ? 1 : 0);
       }
     }
   }
@@ -769,15 +773,8 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
         for (int r = 0; r < 4; ++r) {
           const int rl = wm * WM + i * 16 + (lane >> 4) * 4 + r;
           const float v = acc[i][j][r] + bv;
-          // accumulate: the old value joins before the one rounding (see k_gemm)
-          const float va = (g.accumulate && row0 + rl < g.M && col < N)
-                               ? v + to_f<T>(((const T*)g.c)[(size_t)(row0 + rl) * g.ldc + col]) : v;
-          if (col - cbase < LDC) Cs[rl * LDC + col - cbase] = from_f<T>(va);
-          if (row0 + rl < seg_end && col < N) {
-            const float vs = stored<T>(v);
-            s += vs;
-            q += vs * vs;
-          }
+          if (col - cbase < LDC) Cs[rl * LDC + col - cbase] = from_f<T>(v);
+          if (row0 + rl < seg_end && col < N) { s += v; q += v * v; }
         }
       if (g.has_stats) {
         s = row4_sum(s);
@@ -805,12 +802,11 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
       const T* src = Cs + v * 8;
       if constexpr (sizeof(T) == 2) {
         uint4 raw = *reinterpret_cast<const uint4*>(src);
-        *reinterpret_cast<uint4*>(dst + v * 8) = raw;  // (accumulated at staging)
-        continue;
+        if (!g.accumulate) { *reinterpret_cast<uint4*>(dst + v * 8) = raw; continue; }
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) vals[j] = to_f<T>(src[j]);
-      acc8m(dst + v * 8, 8, vals, 0);
+      acc8m(dst + v * 8, 8, vals, g.accumulate);
     }
   } else {
     const int cv8 = cdiv(ncols, 8);
@@ -823,9 +819,9 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
       for (int j = 0; j < 8; ++j) vals[j] = to_f<T>(Cs[r * LDC + cv + j]);
       T* dst = C + (size_t)(row0 + r) * g.ldc + cbase + cv;
       if (vec_ok) {
-        acc8m(dst, nn, vals, 0);  // (accumulated at staging)
+        acc8m(dst, nn, vals, g.accumulate);
       } else {
-        for (int j = 0; j < 8 && j < nn; ++j) dst[j] = from_f<T>(vals[j]);
+        for (int j = 0; j < 8 && j < nn; ++j) dst[j] = from_f<T>(g.accumulate ? to_f<T>(dst[j]) + vals[j] : vals[j]);
       }
     }
   }
@@ -1577,15 +1573,8 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
         for (int r = 0; r < 4; ++r) {
           const int rl = i * 16 + (lane >> 4) * 4 + r;
           const float v = acc[i][j][r] + bv;
-          // accumulate: the old value joins before the one rounding (see k_gemm)
-          const int grw = wrow0 + rl, gcl = col_base + cl;
-          const float va = (g.accumulate && grw < M && gcl < N) ? v + to_f<T>(C[(size_t)grw * g.ldc + gcl]) : v;
-          cw[rl * CWLD + j * 16 + (lane & 15)] = from_f<T>(va);
-          if (wrow0 + rl < seg_end) {
-            const float vs = stored<T>(v);
-            s += vs;
-            q += vs * vs;
-          }
+          cw[rl * CWLD + j * 16 + (lane & 15)] = from_f<T>(v);
+          if (wrow0 + rl < seg_end) { s += v; q += v * v; }
         }
       if (g.has_stats) {
         s = row4_sum(s);
@@ -1609,7 +1598,7 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
         const T* src = cw + rr * CWLD + cv;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) vals[jj] = to_f<T>(src[jj]);
-        acc8m(C + (size_t)grow * g.ldc + gcol, N - gcol, vals, 0);  // (accumulated at staging)
+        acc8m(C + (size_t)grow * g.ldc + gcol, N - gcol, vals, g.accumulate);
       }
     }
   };
@@ -1985,9 +1974,8 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
           fold_terms(bf2f(f2bf(v[r])), xf_, ftab[n0 + r], g.fx.act, du, dux);
           if (live && n0 + r < N) { ss[f][r] += du; sq[f][r] += dux; }
         } else if (live) {
-          const float vs = bf2f(f2bf(v[r]));  // the stored value
-          ss[f][r] += vs;
-          sq[f][r] += vs * vs;
+          ss[f][r] += v[r];
+          sq[f][r] += v[r] * v[r];
         }
       }
       *reinterpret_cast<uint2*>(cw + (lane & 15) * LDW + n0) =
@@ -2122,6 +2110,17 @@ static int dispatch_gemm_s(const GemmArgs& g, hipStream_t s, bool& done) {
 // ------------------------------------------------------------------ launch helpers
 template <typename T, int BM, int BN, bool LAZY, int KC = 32, int FOLD = 0>
 static int launch_gemm(GemmArgs g, hipStream_t s) {
+  // accumulating launches (the plain dgrads of multi-consumer values) take the ACC instance
+  if constexpr (!LAZY && FOLD == 0) {
+    if (g.accumulate) {
+      g.ntm = cdiv(g.M, BM);
+      g.ntn = cdiv(g.N, BN);
+      const int nwg = g.ntm * g.ntn;
+      if (nwg == 0) return EDET_OK;
+      EDET_LAUNCH((k_gemm<T, BM, BN, KC, false, 0, true>), dim3(nwg), dim3(256), 0, s, g);
+      return check_launch("edet gemm (accumulate)");
+    }
+  }
   g.ntm = cdiv(g.M, BM);
   g.ntn = cdiv(g.N, BN);
   const int nwg = g.ntm * g.ntn;

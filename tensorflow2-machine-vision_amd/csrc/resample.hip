@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const T* x, int B, int H, int 
     if (valid) st8(y + (size_t)p * Cout + co0, acc);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float a = valid ? stored<T>(acc[j]) : 0.f;  // the stored value
+      const float a = valid ? acc[j] : 0.f;
       const float s = wave_sum(a), q = wave_sum(a * a);
       if (lane == 0) { red[0][wave][co0 + j] = s; red[1][wave][co0 + j] = q; }
     }
@@ -221,11 +221,7 @@ __global__ __launch_bounds__(256) void k_stem2_fwd(const uint16_t* x, int B, int
         uint32_t hi = (uint32_t)f2bf(acc[2]) | ((uint32_t)f2bf(acc[3]) << 16);
         *reinterpret_cast<uint2*>(y + (pix0 + pix) * Cout + t * 16 + 4 * g4) = make_uint2(lo, hi);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float vs = bf2f(f2bf(acc[r]));  // the stored value
-          s[t][r] += vs;
-          q[t][r] += vs * vs;
-        }
+        for (int r = 0; r < 4; ++r) { s[t][r] += acc[r]; q[t][r] += acc[r] * acc[r]; }
       }
     }
   }

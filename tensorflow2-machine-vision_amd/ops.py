@@ -213,11 +213,17 @@ FOLD_GEMM_BN = os.environ.get("EDET_FOLD_GEMM_BN", "0") != "0"
 # the stride-2 depthwise dgrad with the same fold (edet_dwconv_dgrad_fold)
 FOLD_DWS2_BN = os.environ.get("EDET_FOLD_DWS2_BN", "1") != "0"
 # the stride-1 SE-gated depthwise output's BN-backward apply inside the fused backward's dy
-# staging (edet_dwconv_bwd_lazy) instead of its own pass
-LAZY_DY_DW = os.environ.get("EDET_LAZY_DY", "1") != "0"
+# staging (edet_dwconv_bwd_lazy) instead of its own pass.  Off by default: it removes the 12
+# applies (-417 us of kernel time) but the tiled backward grows by as much (+427 us: the
+# transform -- a sigmoid per halo element -- sits between its loads and its stencil), and the
+# whole D0 step measured 13.30 (off) vs 13.33 ms (on), same-box A/B r05b
+LAZY_DY_DW = os.environ.get("EDET_LAZY_DY", "0") != "0"
 # the SE-gated depthwise output's backward sums in the project conv's dgrad epilogue
-# (edet_conv1x1_dgrad_sesum) instead of edet_gate_bn_reduce's pass over (y, dv)
-SESUM_DGRAD = os.environ.get("EDET_SESUM_DGRAD", "1") != "0"
+# (edet_conv1x1_dgrad_sesum) instead of edet_gate_bn_reduce's pass over (y, dv).  Off by
+# default: the 13 K-loop dgrads grew by 361 us (per element a sigmoid and the x tile in LDS,
+# 3 -> 2 waves per SIMD at 64 x 128) against the 300 us of reduce passes removed (r05b kbench),
+# whole step even to +0.03 ms
+SESUM_DGRAD = os.environ.get("EDET_SESUM_DGRAD", "0") != "0"
 # every switch that takes a BN-backward pass into the kernel producing or consuming the gradient
 # (the test of the folds flips them all: tests/test_model_gpu.py::test_bn_backward_folds_equal_unfused_path)
 FOLD_SWITCHES = ("FUSED_DW_BWD", "FOLD_DW_BN", "FOLD_GEMM_BN", "FOLD_DWS2_BN", "LAZY_DY_DW", "SESUM_DGRAD")
