@@ -66,20 +66,52 @@ struct LArgs {
   RowGeom geo;
 };
 
-// per-channel tables in dynamic LDS: af (sc, sh), mr (mean, rstd), gb (dgamma/M, dbeta/M)
+// per-channel tables in dynamic LDS: af (sc, sh), mr (mean, rstd), gb (dgamma/M, dbeta/M).
+// A thread builds channels tid, tid + blockDim, ... : TU = 2 of them with every statistic
+// load issued before any is used (the plain loop waited for each channel's fp64 loads in turn:
+// C / blockDim dependent L2 round trips per block, 8 for the 1152-channel rows; TU = 4 cost
+// the light apply instances 1-2 waves per SIMD)
 __device__ __forceinline__ void load_tables(const edet_lazy& lz, int seg, float inv, int C, float2* af, float2* mr,
                                             float2* gb, const edet_bngrad64* acc) {
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float2 a = make_float2(1.f, 0.f), b = make_float2(0.f, 1.f);
-    if (lz.bn.enabled) {
-      a = bn_affine(lz.bn, seg, c, inv);
-      b = bn_mean_rstd(lz.bn, seg, c, inv);
+  constexpr int TU = 2;
+  const bool bn = lz.bn.enabled;
+  for (int c0 = threadIdx.x; c0 < C; c0 += TU * blockDim.x) {
+    double su[TU], sq[TU], dg[TU], db[TU];
+    float ga[TU], be[TU];
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      const int c = min(c0 + u * (int)blockDim.x, C - 1);  // clamped: loads are unconditional
+      su[u] = sq[u] = dg[u] = db[u] = 0.0;
+      ga[u] = 1.f;
+      be[u] = 0.f;
+      if (bn) {
+        su[u] = lz.bn.sum[seg][c];
+        sq[u] = lz.bn.sq[seg][c];
+        ga[u] = lz.bn.gamma[seg][c];
+        be[u] = lz.bn.beta[seg][c];
+        if (gb) {
+          dg[u] = acc->dgamma[seg][c];
+          db[u] = acc->dbeta[seg][c];
+        }
+      }
     }
-    af[c] = a;
-    if (mr) mr[c] = b;
-    if (gb)
-      gb[c] = lz.bn.enabled ? make_float2((float)(acc->dgamma[seg][c] * (double)inv), (float)(acc->dbeta[seg][c] * (double)inv))
-                            : make_float2(0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < TU; ++u) {
+      const int c = c0 + u * (int)blockDim.x;
+      if (c >= C) break;
+      float2 a = make_float2(1.f, 0.f), b = make_float2(0.f, 1.f);
+      if (bn) {  // bn_affine / bn_mean_rstd (common.hpp), the same arithmetic
+        const double mean = su[u] * (double)inv;
+        const double var = fmax(sq[u] * (double)inv - mean * mean, 0.0);
+        const float r = rsqrtf((float)var + lz.bn.eps);
+        const float sc = ga[u] * r;
+        a = make_float2(sc, be[u] - (float)mean * sc);
+        b = make_float2((float)mean, r);
+      }
+      af[c] = a;
+      if (mr) mr[c] = b;
+      if (gb) gb[c] = bn ? make_float2((float)(dg[u] * (double)inv), (float)(db[u] * (double)inv)) : make_float2(0.f, 0.f);
+    }
   }
 }
 
