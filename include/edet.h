@@ -167,10 +167,10 @@ int edet_wall_clock_khz(int* khz);
  * comma-separated base names (e.g. "k_wgrad_tr,k_sum_partials") into buf; returns the number
  * of launches (not a status). */
 int edet_launched_kernels(char* buf, size_t size);
-/* development: A/B slots 0..31 read by some launchers' plan choices (0 = the production plan),
+/* development: A/B slots 0..63 read by some launchers' plan choices (0 = the production plan),
  * compiled only into the EDET_DEV build (`make dev` -> lib/libedet_dev.so, for
- * scripts/kbench.py --dev).  Returns the previous value there; the production library has no
- * slots and returns EDET_EUNSUPPORTED. */
+ * scripts/kbench.py --dev).  Returns EDET_OK there (EDET_EINVAL for a slot outside 0..63); the
+ * production library has no slots and returns EDET_EUNSUPPORTED. */
 int edet_dev_set(int slot, int value);
 
 /* ---- pointwise (1x1) convolution: y[m][n] = sum_k v(a)[m][k] * wt[n][k] + bias[n] ----

@@ -83,7 +83,7 @@ def main():
     torch.cuda.synchronize()
     L.call = orig
     if args.dev:
-        for i in range(32):
+        for i in range(64):
             L.lib().fns["edet_dev_set"](i, 0)
 
     rows, agg = [], {}

@@ -174,8 +174,11 @@ class _Lib:
         # EDET_DEV_SLOTS="29=2,30=1024"; the production library refuses them (edet_dev_set errors)
         for kv in filter(None, os.environ.get("EDET_DEV_SLOTS", "").split(",")):
             slot, val = (int(v) for v in kv.split("="))
-            if self.fns["edet_dev_set"](slot, val) < 0:
+            rc = self.fns["edet_dev_set"](slot, val)
+            if rc == -2:  # EDET_EUNSUPPORTED
                 raise ImportError(f"EDET_DEV_SLOTS needs a development build (make dev): {path}")
+            if rc != 0:
+                raise ImportError(f"EDET_DEV_SLOTS: {self.last_error()}")
 
     def last_error(self) -> str:
         return self.fns["edet_last_error"]().decode(errors="replace")

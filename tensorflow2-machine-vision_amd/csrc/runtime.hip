@@ -124,10 +124,11 @@ int edet_launched_kernels(char* buf, size_t size) {
 
 int edet_dev_set(int slot, int value) {
 #ifdef EDET_DEV
-  if (slot < 0 || slot >= 64) return 0;
-  const int old = edet::g_dev[slot];
+  // a status like every entry point (returning the old value made a slot set to a
+  // negative value read as "not a development build", and a bad slot number passed silently)
+  EDET_REQUIRE(slot >= 0 && slot < 64, "edet_dev_set: slot %d outside 0..63", slot);
   edet::g_dev[slot] = value;
-  return old;
+  return EDET_OK;
 #else
   (void)slot;
   (void)value;
