@@ -5,6 +5,9 @@ each, and the tiled form's dx / filter gradient / fold sums against the producti
 (fp32 summation order only: relative differences ~1e-6 in fp32, a few bf16 ulp in bf16).
 
     EDET_LIB=tensorflow2-machine-vision_amd/lib/libedet_dev.so python tools/dwt_ab.py [bf16|f32] ["30=1024,31=2"]
+
+DWT_A / DWT_B (slot=value lists, default "29=2" / "29=1") choose the two forms, e.g.
+DWT_A=29=1 DWT_B=29=1,41=2 for the tiled form against its next-tile DMA variant.
 """
 import os
 import sys
@@ -57,9 +60,10 @@ def main():
         w = (torch.randn(k * k, C, device="cuda") * 0.3).to(tdt)
         dy = torch.randn(pin.rows, C, device="cuda").to(tdt)
         outs, us = [], []
-        for form in (2, 1):
-            dev(29, form)
-            for a, b in extra:
+        forms = [os.environ.get("DWT_A", "29=2"), os.environ.get("DWT_B", "29=1")]
+        for form in forms:
+            slots = [tuple(int(v) for v in kv.split("=")) for kv in form.split(",") if kv] + extra
+            for a, b in slots:
                 dev(a, b)
             dx = torch.empty(pin.rows, C, device="cuda", dtype=tdt)
             dw = torch.zeros(k * k, C, device="cuda")
@@ -69,19 +73,18 @@ def main():
             outs.append((dx.clone(), dw.clone(), acc_t.clone()))
             us.append(timeit(lambda: L.call("edet_dwconv_bwd", edt, lz.c, pin.c, C, k, 1, vp(dy), pin.c, vp(w),
                                             vp(dx), 0, vp(dw), acc, s)))
-            for a, _ in extra:
+            for a, _ in slots:
                 dev(a, 0)
-            dev(29, 0)
         valid = torch.cat([torch.arange(pin.row_off[i], pin.row_off[i] + pin.seg_rows(i)) for i in range(pin.nseg)])
         (dx0, dw0, f0), (dx1, dw1, f1) = outs
         e_dx, e_dw, e_f = rel(dx1[valid], dx0[valid]), rel(dw1, dw0), rel(f1, f0)
         mb = pin.rows * C * 2 / 1e6
         bad = "" if (e_dx < (2e-2 if dt == "bf16" else 1e-5) and e_dw < 1e-3 and e_f < 1e-3) else "  <<< MISMATCH"
-        print(f"H={H:3d} C={C:5d} k={k} ({mb:6.1f} MB): rows {us[0]:7.1f} us  tiles {us[1]:7.1f} us  "
+        print(f"H={H:3d} C={C:5d} k={k} ({mb:6.1f} MB): A {us[0]:7.1f} us  B {us[1]:7.1f} us  "
               f"x{us[0] / us[1]:.2f} | dx {e_dx:.1e} dw {e_dw:.1e} fold {e_f:.1e}{bad}", flush=True)
         tot[0] += us[0]
         tot[1] += us[1]
-    print(f"total rows {tot[0]:.1f} us  tiles {tot[1]:.1f} us")
+    print(f"total A {tot[0]:.1f} us  B {tot[1]:.1f} us  (A = {forms[0]}, B = {forms[1]})")
 
 
 if __name__ == "__main__":

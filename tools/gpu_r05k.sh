@@ -1,0 +1,7 @@
+#!/bin/bash
+# k_dwt next-tile DMA variant (dev slot 41 = 2) against the production tiled form, per D0 shape
+set -o pipefail
+mkdir -p gpurun_out/r05k
+export EDET_LIB=tensorflow2-machine-vision_amd/lib/libedet_dev.so
+DWT_A=29=1 DWT_B=29=1,41=2 timeout -k 10 240 python -u tools/dwt_ab.py bf16 > gpurun_out/r05k/dwt_dma_ab.txt 2>&1 &&
+DWT_A=29=1 DWT_B=29=1,41=1 timeout -k 10 240 python -u tools/dwt_ab.py bf16 > gpurun_out/r05k/dwt_split_ab.txt 2>&1
