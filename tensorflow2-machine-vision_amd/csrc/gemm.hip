@@ -2173,6 +2173,22 @@ static int dispatch_gemm_kloop(GemmArgs g, hipStream_t s) {
   // BM = 32 when 64-row tiles would leave the chip under-filled (and for the fp32 fold, whose
   // staged C and x tiles at 64 x 320 would not fit the LDS)
   constexpr bool only32 = FOLD != 0 && sizeof(T) == 4;
+#ifdef EDET_DEV
+  // development slots 42 / 43: force the row / column tile (32, 64, 128 / 64, 128, 256)
+  if constexpr (!only32 && FOLD == 0) {
+    if (const int bm = dev_knob(42)) {
+      const int bn = dev_knob(43) ? dev_knob(43) : (NP <= 64 ? 64 : 128);
+      if (bm == 128 && bn == 64) return launch_gemm<T, 128, 64, LAZY, 32, FOLD>(g, s);
+      if (bm == 128 && bn == 128) return launch_gemm<T, 128, 128, LAZY, 32, FOLD>(g, s);
+      if (bm == 64 && bn == 64) return launch_gemm<T, 64, 64, LAZY, 32, FOLD>(g, s);
+      if (bm == 64 && bn == 128) return launch_gemm<T, 64, 128, LAZY, 32, FOLD>(g, s);
+      if (bm == 64 && bn == 256) return launch_gemm<T, 64, 256, LAZY, 32, FOLD>(g, s);
+      if (bm == 32 && bn == 64) return launch_gemm<T, 32, 64, LAZY, 32, FOLD>(g, s);
+      if (bm == 32 && bn == 128) return launch_gemm<T, 32, 128, LAZY, 32, FOLD>(g, s);
+      if (bm == 32 && bn == 256) return launch_gemm<T, 32, 256, LAZY, 32, FOLD>(g, s);
+    }
+  }
+#endif
   if (only32 || cdiv(g.M, 64) < 512) {
     if (NP <= 64) return launch_gemm<T, 32, 64, LAZY, 32, FOLD>(g, s);
     if (NP <= 96) return launch_gemm<T, 32, 96, LAZY, 32, FOLD>(g, s);
@@ -2275,6 +2291,24 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
   // wins K = 224 into N >= 192 with statistics at M <= 8192 (8192 x 224 -> 224: 33 -> 24 us);
   // the B-resident form wins the D0 class predict (174592 x 64 -> 729: 114 -> 93 us)
   if constexpr (sizeof(T) == 2) {
+    // Round-5 K-loop tile sweep over the mid-size D0 products (8192 / 32768 rows: the 16^2 and
+    // 32^2 stages, 0.4-1.6 TB/s; tools/gpu_r05l.sh, profiles/r05/r05l_gemm_tiles.txt): 64-column
+    // tiles with more rows per tile -- more blocks than the one full-N tile, and fewer blocks
+    // per output column flushing BN statistics (one fp64 atomic per column per block)
+    if (g.M >= 8192 && g.M <= 65536) {
+      // plain A with statistics, deep K (the project convs): 8192 x 1152 -> 192 24.5 -> 16.0 us,
+      // 32768 x 672 -> 112 26.7 -> 21.0
+      if (!LAZY && g.has_stats && g.K > 256 && g.N <= 320)
+        return g.M <= 16384 ? launch_gemm<T, 64, 64, LAZY>(g, s) : launch_gemm<T, 128, 64, LAZY>(g, s);
+      // plain dgrads at 8192 rows: 8192 x 1152 -> 320 25.0 -> 20.1 us, 192 -> 1152 18.9 -> 13.9
+      if (!LAZY && !g.has_stats && g.M <= 16384 && g.K >= 64 && g.N >= 64)
+        return g.N <= 192 ? launch_gemm<T, 64, 64, LAZY>(g, s) : launch_gemm<T, 128, 64, LAZY>(g, s);
+      // lazy A into wide outputs at 8192 rows (the stage-6 expand convs): 29.5 -> 25.7 us
+      if (LAZY && g.M <= 16384 && g.K > 64 && g.N > 320) return launch_gemm<T, 64, 128, LAZY>(g, s);
+      // lazy A with statistics into 64 columns (the BiFPN input projections): 17.4 -> 13.8 us
+      if (LAZY && g.has_stats && g.K > 64 && g.N <= 64 && g.M <= 32768)
+        return g.M <= 8192 ? launch_gemm<T, 64, 64, LAZY>(g, s) : launch_gemm<T, 128, 64, LAZY>(g, s);
+    }
     const int KPr = cdiv(g.K, 32) * 32;
     const bool w224 = g.N >= 192 && KPr > 192 && KPr <= 224;
     if (!LAZY && !g.has_stats && w224) return dispatch_gemm_kloop<T, LAZY>(g, s);

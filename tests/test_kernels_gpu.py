@@ -48,7 +48,13 @@ def pyr_data(rng, pyr, C, dt, scale=1.0):
                                             # M <= 8192 (A-resident; without them the K loop), the
                                             # class predict's K = 64 into N = 729 over M >= 131072
                                             # without statistics (B-resident)
-                                            (800, 160, 224, 3, 1), (800, 160, 224, 1, 1), (131072, 64, 729, 0, 1)])
+                                            (800, 160, 224, 3, 1), (800, 160, 224, 1, 1), (131072, 64, 729, 0, 1),
+                                            # round-5 K-loop tiles at 8192 / 32768 rows: plain with
+                                            # statistics 64 x 64 / 128 x 64 (and stats-free 8192
+                                            # rows), lazy into N > 320 64 x 128, lazy with
+                                            # statistics into 64 columns 64 x 64 / 128 x 64
+                                            (8192, 1152, 192, 0, 1), (32768, 480, 112, 0, 1),
+                                            (8192, 192, 1152, 1, 1), (8192, 320, 64, 3, 1), (32768, 112, 64, 2, 1)])
 def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
     """conv1x1 forward with BN statistics (and without them for plain inputs: the stats-free
     route) against fp64."""
@@ -78,7 +84,9 @@ def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("M,N,K,ldy", [(300, 40, 24, 40), (777, 729, 64, 736), (2048, 1152, 192, 1152),
                                        (500, 320, 1152, 320), (300, 36, 64, 40), (1000, 224, 224, 224),
-                                       (600, 729, 224, 736), (2000, 96, 16, 96), (1500, 144, 24, 144)])
+                                       (600, 729, 224, 736), (2000, 96, 16, 96), (1500, 144, 24, 144),
+                                       # round-5 K-loop tiles at 8192 rows: 128 x 64 / 64 x 64
+                                       (8192, 320, 1152, 320), (8192, 1152, 192, 1152)])
 def test_conv1x1_dgrad(dt, M, N, K, ldy):
     rng = np.random.default_rng(M * 7 + N)
     pyr = Pyr(1, [(M, 1)])
