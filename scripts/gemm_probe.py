@@ -1,7 +1,7 @@
 """Isolated timing of edet_conv1x1_fwd / dgrad / wgrad variants at one shape.
 
   python scripts/gemm_probe.py M K N
-Prints us per launch for: plain fwd, fwd+stats, lazy bn+swish fwd, lazy bn+swish+gate fwd,
+Prints us per launch for: plain fwd, fwd+stats, lazy bn fwd, lazy bn+swish fwd, lazy bn+swish+gate fwd,
 dgrad, wgrad (plain and lazy).  Timing: 20 back-to-back launches between HIP events.
 """
 import math
@@ -60,6 +60,7 @@ def main():
         bn = make_bn(x, pyr, K, rng)
         gate = torch.rand(pyr.batch, K, device="cuda")
         plain = LazyDesc(x, pyr, K)
+        lz_b = LazyDesc(x, pyr, K, bn=bn, act=0)
         lz_bs = LazyDesc(x, pyr, K, bn=bn, act=1)
         lz_bsg = LazyDesc(x, pyr, K, bn=bn, act=1, gate=gate)
         st = [(zeros64(N), zeros64(N))]
@@ -74,6 +75,9 @@ def main():
         if (not only or only == "fwd +stats"):
             res["fwd +stats"] = timeit(lambda: L.call("edet_conv1x1_fwd", L.BF16, plain.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, so, s))
             kern["fwd +stats"] = KERN["last"]
+        if (not only or only == "fwd bn"):
+            res["fwd bn"] = timeit(lambda: L.call("edet_conv1x1_fwd", L.BF16, lz_b.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, so, s))
+            kern["fwd bn"] = KERN["last"]
         if (not only or only == "fwd bn+sw"):
             res["fwd bn+sw"] = timeit(lambda: L.call("edet_conv1x1_fwd", L.BF16, lz_bs.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, so, s))
             kern["fwd bn+sw"] = KERN["last"]

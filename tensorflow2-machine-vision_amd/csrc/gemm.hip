@@ -1001,7 +1001,8 @@ constexpr int WT_BM = 64, WT_LDM = 64 + 8;  // WT_BM: the unit the row splits ar
 // committed.  A block's stage chain is latency-bound on the mid-M shapes (~1.2 us per 64-row
 // stage at 2 in flight, whatever the tile count: profiles/r03ab_wgrad_plan_sweep.txt), so more
 // bytes in flight per block shorten it without adding splits (= fp32 atomic bytes).
-template <bool LAZY, int BM = 64, int PF = 2>
+// ACT (LAZY): the activation as a compile-time case (0 none, 1 swish), as k_gemm_s
+template <bool LAZY, int BM = 64, int PF = 2, int ACT = 0>
 __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
   static_assert(BM % 64 == 0 && PF >= 1, "stage rows: multiple of 64");
   constexpr int HR = BM / 32;  // rows per thread per stage (32 rows per pass of the 256 threads)
@@ -1087,7 +1088,9 @@ __global__ __launch_bounds__(256) void k_wgrad_tr(WgradArgs g) {
         uint16_t o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float u = lazy_apply(to_f<uint16_t>(t[j]), xf[sg][lc + j], g.lz.act);
+          const float2 a = xf[sg][lc + j];
+          float u = to_f<uint16_t>(t[j]) * a.x + a.y;
+          if constexpr (ACT == 1) u = swishf_(u);
           if (has_gate) u *= gv[j];
           o[j] = from_f<uint16_t>(keep && kk0 + lc + j < g.K ? u : 0.f);
         }
@@ -1794,7 +1797,10 @@ static int dispatch_pwb_forced(const GemmArgs& g, hipStream_t s, bool& done) {
 // stores, whole rows written by one wave back to back.  BN statistics stay in registers per
 // lane until the end (one lane tree, one LDS pass and one fp64 atomic per channel per block).
 constexpr int GS_PF = 2;  // row groups in flight ahead of the one being computed
-template <typename T, int NF, int KS, bool LAZY, bool FOLD = false>
+// ACT (LAZY): the activation as a compile-time case (0 none, 1 swish).  The runtime test per
+// element left the act = 0 instances slower than the swish ones (2M x 16 -> 96 with BN only:
+// 152 -> 139 us, r05p)
+template <typename T, int NF, int KS, bool LAZY, bool FOLD = false, int ACT = 0>
 __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   // BN statistics: per wave and segment (a wave's groups ascend, so it meets each segment
   // once), summed over the block's waves in a fixed order at the end.  FOLD (one segment): the
@@ -1944,7 +1950,8 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
         uint16_t o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float u = lazy_apply(x[j], af[ks][j], g.lz.act);
+          float u = x[j] * af[ks][j].x + af[ks][j].y;
+          if constexpr (ACT == 1) u = swishf_(u);
           if (has_gate) u *= gt[j];
           o[j] = k0 + j < K ? f2bf(u) : (uint16_t)0;
         }
@@ -2036,7 +2043,8 @@ static int launch_gemm_s(const GemmArgs& g, hipStream_t s) {
   else if (g.M >= (1 << 21)) cap = 1024;
   if (dev_knob(7) > 0) cap = dev_knob(7);
   const int grid = std::max(1, std::min(cdiv(ngroups, 4), cap));
-  EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY, FOLD>), dim3(grid), dim3(256), 0, s, g);
+  if (LAZY && g.lz.act) EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY, FOLD, 1>), dim3(grid), dim3(256), 0, s, g);
+  else EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY, FOLD, 0>), dim3(grid), dim3(256), 0, s, g);
   return check_launch("edet gemm_s");
 }
 
@@ -2545,7 +2553,8 @@ int edet_conv1x1_wgrad(int dtype, const edet_lazy* a, const edet_pyramid* rows, 
 #define EDET_WGT(BM_, PF_)                                                            \
   do {                                                                                \
     if (plain) EDET_LAUNCH((k_wgrad_tr<false, BM_, PF_>), grid, dim3(256), 0, s, g); \
-    else EDET_LAUNCH((k_wgrad_tr<true, BM_, PF_>), grid, dim3(256), 0, s, g);        \
+    else if (a->act) EDET_LAUNCH((k_wgrad_tr<true, BM_, PF_, 1>), grid, dim3(256), 0, s, g); \
+    else EDET_LAUNCH((k_wgrad_tr<true, BM_, PF_, 0>), grid, dim3(256), 0, s, g);     \
   } while (0)
     switch (form) {
       case 1: EDET_WGT(64, 3); break;

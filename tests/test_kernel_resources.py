@@ -76,8 +76,8 @@ def test_wgrad_pipeline_waits_are_partial():
     ws = pytest.importorskip("wait_scan")
     if not os.path.exists(ws.OBJDUMP):
         pytest.skip("llvm-objdump not available")
-    found = ws.scan(LIB, "void edet::k_wgrad_tr<false, 64, 2>")
-    assert found, "k_wgrad_tr<false, 64, 2> not in the library"
+    found = ws.scan(LIB, "void edet::k_wgrad_tr<false, 64, 2, 0>")
+    assert found, "k_wgrad_tr<false, 64, 2, 0> not in the library"
     (_, loops), = found
     main = loops[0]
     assert main["loads"] >= 8 and main["vmcnt"], main
