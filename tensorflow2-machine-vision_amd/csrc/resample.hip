@@ -633,7 +633,19 @@ __device__ __forceinline__ void unpack_bf8(const uint4& q, float* o) {
     o[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
   }
 }
-template <int M>
+// ACT: the inputs' activation as a compile-time case (0 none, 1 swish) when every input of the
+// node shares it, -1 = read fi.v.act (the runtime test per element sat in the pool's 72-value
+// compare loop)
+template <int ACT>
+__device__ __forceinline__ float fuse_act(float x, float2 a, int act) {
+  if constexpr (ACT < 0) {
+    return lazy_apply(x, a, act);
+  } else {
+    const float u = x * a.x + a.y;
+    return ACT == 1 ? swishf_(u) : u;
+  }
+}
+template <int M, int ACT = -1>
 __device__ __forceinline__ void fuse_raw_value(const FuseRaw<M>& s, const edet_fuse_input& fi, const float2* af,
                                                size_t pix, int C, int c, float* v) {
   if constexpr (M == EDET_MODE_MAXPOOL) {
@@ -648,7 +660,7 @@ __device__ __forceinline__ void fuse_raw_value(const FuseRaw<M>& s, const edet_f
       unpack_bf8(s.r[k], x);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float t = lazy_apply(x[j], af[j], fi.v.act);
+        const float t = fuse_act<ACT>(x[j], af[j], fi.v.act);
         if (arg[j] < 0 || t > best[j]) { best[j] = t; arg[j] = k; tk[j] = k; }
       }
     }
@@ -659,10 +671,10 @@ __device__ __forceinline__ void fuse_raw_value(const FuseRaw<M>& s, const edet_f
     float x[8];
     unpack_bf8(s.r[0], x);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = lazy_apply(x[j], af[j], fi.v.act);
+    for (int j = 0; j < 8; ++j) v[j] = fuse_act<ACT>(x[j], af[j], fi.v.act);
   }
 }
-template <int M0, int M1, int M2>
+template <int M0, int M1, int M2, int ACT = -1>
 __global__ __launch_bounds__(256) void k_fuse_fwd_m(FuseArgs g) {
   using T = uint16_t;
   extern __shared__ float2 aft[];  // [n_in][C]
@@ -691,16 +703,16 @@ __global__ __launch_bounds__(256) void k_fuse_fwd_m(FuseArgs g) {
     float o[8], v[8];
     float2 af[8];
     affine8_lds(aft, cv * 8, af);
-    fuse_raw_value<M0>(r0, g.in[0], af, (size_t)pix, g.C, cv * 8, v);
+    fuse_raw_value<M0, ACT>(r0, g.in[0], af, (size_t)pix, g.C, cv * 8, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = v[j] * wn[0];
     affine8_lds(aft + g.C, cv * 8, af);
-    fuse_raw_value<M1>(r1, g.in[1], af, (size_t)pix, g.C, cv * 8, v);
+    fuse_raw_value<M1, ACT>(r1, g.in[1], af, (size_t)pix, g.C, cv * 8, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = o[j] + v[j] * wn[1];
     if constexpr (M2 >= 0) {
       affine8_lds(aft + 2 * g.C, cv * 8, af);
-      fuse_raw_value<M2>(r2, g.in[2], af, (size_t)pix, g.C, cv * 8, v);
+      fuse_raw_value<M2, ACT>(r2, g.in[2], af, (size_t)pix, g.C, cv * 8, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = o[j] + v[j] * wn[2];
     }
@@ -879,7 +891,7 @@ __global__ __launch_bounds__(256) void k_fuse_bwd(FuseArgs g) {
 // with a bounded grid of long-lived blocks those serial round trips were the launch's tail, D4
 // 130-138 us per call); a max-pooled input recomputes its 3x3 window (nine loads at once)
 // instead of chaining a tap load and the tap-indexed rows.  The dx blocks are k_fuse_bwd's.
-template <int M0, int M1, int M2>
+template <int M0, int M1, int M2, int ACT = -1>
 __global__ __launch_bounds__(256) void k_fuse_bwd_m(FuseArgs g) {
   using T = uint16_t;
   __shared__ float red[3][4];
@@ -927,14 +939,14 @@ __global__ __launch_bounds__(256) void k_fuse_bwd_m(FuseArgs g) {
     edet_fuse_input f0 = g.in[0], f1 = g.in[1], f2 = g.in[NIN - 1];
     f0.pool_arg = nullptr; f1.pool_arg = nullptr; f2.pool_arg = nullptr;
     affine8_lds(aft, cv * 8, af);
-    fuse_raw_value<M0>(r0, f0, af, (size_t)pix, g.C, cv * 8, v);
+    fuse_raw_value<M0, ACT>(r0, f0, af, (size_t)pix, g.C, cv * 8, v);
     acc(0);
     affine8_lds(aft + g.C, cv * 8, af);
-    fuse_raw_value<M1>(r1, f1, af, (size_t)pix, g.C, cv * 8, v);
+    fuse_raw_value<M1, ACT>(r1, f1, af, (size_t)pix, g.C, cv * 8, v);
     acc(1);
     if constexpr (M2 >= 0) {
       affine8_lds(aft + 2 * g.C, cv * 8, af);
-      fuse_raw_value<M2>(r2, f2, af, (size_t)pix, g.C, cv * 8, v);
+      fuse_raw_value<M2, ACT>(r2, f2, af, (size_t)pix, g.C, cv * 8, v);
       acc(2);
     }
   }
@@ -1068,6 +1080,14 @@ static int fuse_setup(FuseArgs& g, int n_in, const edet_fuse_input* ins, const f
   return EDET_OK;
 }
 
+// the activation every input shares (0 none, 1 swish), -1 if they differ
+static int fuse_common_act(int n_in, const edet_fuse_input* ins) {
+  const int a = ins[0].v.act ? 1 : 0;
+  for (int i = 1; i < n_in; ++i)
+    if ((ins[i].v.act ? 1 : 0) != a) return -1;
+  return a;
+}
+
 int edet_bifpn_fuse_fwd(int dtype, int n_in, const edet_fuse_input* ins, const float* w,
                         int B, int H, int W, int C, void* out, edet_stream_t stream) {
   FuseArgs g{};
@@ -1090,12 +1110,20 @@ int edet_bifpn_fuse_fwd(int dtype, int n_in, const edet_fuse_input* ins, const f
     constexpr int S_ = EDET_MODE_SAME, U_ = EDET_MODE_UPSAMPLE, P_ = EDET_MODE_MAXPOOL;
     hipStream_t st = (hipStream_t)stream;
     bool hit = true;
-    if (m0 == S_ && m1 == U_ && m2 == -1) EDET_LAUNCH((k_fuse_fwd_m<S_, U_, -1>), dim3(nb), dim3(256), lds, st, g);
-    else if (m0 == S_ && m1 == S_ && m2 == P_) EDET_LAUNCH((k_fuse_fwd_m<S_, S_, P_>), dim3(nb), dim3(256), lds, st, g);
-    else if (m0 == S_ && m1 == P_ && m2 == -1) EDET_LAUNCH((k_fuse_fwd_m<S_, P_, -1>), dim3(nb), dim3(256), lds, st, g);
-    else if (m0 == S_ && m1 == S_ && m2 == U_) EDET_LAUNCH((k_fuse_fwd_m<S_, S_, U_>), dim3(nb), dim3(256), lds, st, g);
-    else if (m0 == S_ && m1 == S_ && m2 == -1) EDET_LAUNCH((k_fuse_fwd_m<S_, S_, -1>), dim3(nb), dim3(256), lds, st, g);
+    const int act = fuse_common_act(n_in, ins);
+#define EDET_FUSE_M(A, B, C)                                                                              \
+  do {                                                                                                    \
+    if (act == 0) EDET_LAUNCH((k_fuse_fwd_m<A, B, C, 0>), dim3(nb), dim3(256), lds, st, g);                  \
+    else if (act == 1) EDET_LAUNCH((k_fuse_fwd_m<A, B, C, 1>), dim3(nb), dim3(256), lds, st, g);             \
+    else EDET_LAUNCH((k_fuse_fwd_m<A, B, C, -1>), dim3(nb), dim3(256), lds, st, g);                          \
+  } while (0)
+    if (m0 == S_ && m1 == U_ && m2 == -1) EDET_FUSE_M(S_, U_, -1);
+    else if (m0 == S_ && m1 == S_ && m2 == P_) EDET_FUSE_M(S_, S_, P_);
+    else if (m0 == S_ && m1 == P_ && m2 == -1) EDET_FUSE_M(S_, P_, -1);
+    else if (m0 == S_ && m1 == S_ && m2 == U_) EDET_FUSE_M(S_, S_, U_);
+    else if (m0 == S_ && m1 == S_ && m2 == -1) EDET_FUSE_M(S_, S_, -1);
     else hit = false;
+#undef EDET_FUSE_M
     if (hit) return check_launch("edet bifpn_fuse_fwd");
   }
   EDET_DTYPE_DISPATCH(dtype, T, {
@@ -1125,12 +1153,20 @@ int edet_bifpn_fuse_bwd(int dtype, int n_in, const edet_fuse_input* ins, const f
     constexpr int S_ = EDET_MODE_SAME, U_ = EDET_MODE_UPSAMPLE, P_ = EDET_MODE_MAXPOOL;
     hipStream_t st = (hipStream_t)stream;
     bool hit = true;
-    if (m0 == S_ && m1 == U_ && m2 == -1) EDET_LAUNCH((k_fuse_bwd_m<S_, U_, -1>), dim3(nb), dim3(256), lds, st, g);
-    else if (m0 == S_ && m1 == S_ && m2 == P_) EDET_LAUNCH((k_fuse_bwd_m<S_, S_, P_>), dim3(nb), dim3(256), lds, st, g);
-    else if (m0 == S_ && m1 == P_ && m2 == -1) EDET_LAUNCH((k_fuse_bwd_m<S_, P_, -1>), dim3(nb), dim3(256), lds, st, g);
-    else if (m0 == S_ && m1 == S_ && m2 == U_) EDET_LAUNCH((k_fuse_bwd_m<S_, S_, U_>), dim3(nb), dim3(256), lds, st, g);
-    else if (m0 == S_ && m1 == S_ && m2 == -1) EDET_LAUNCH((k_fuse_bwd_m<S_, S_, -1>), dim3(nb), dim3(256), lds, st, g);
+    const int act = fuse_common_act(n_in, ins);
+#define EDET_FUSE_M(A, B, C)                                                                              \
+  do {                                                                                                    \
+    if (act == 0) EDET_LAUNCH((k_fuse_bwd_m<A, B, C, 0>), dim3(nb), dim3(256), lds, st, g);                  \
+    else if (act == 1) EDET_LAUNCH((k_fuse_bwd_m<A, B, C, 1>), dim3(nb), dim3(256), lds, st, g);             \
+    else EDET_LAUNCH((k_fuse_bwd_m<A, B, C, -1>), dim3(nb), dim3(256), lds, st, g);                          \
+  } while (0)
+    if (m0 == S_ && m1 == U_ && m2 == -1) EDET_FUSE_M(S_, U_, -1);
+    else if (m0 == S_ && m1 == S_ && m2 == P_) EDET_FUSE_M(S_, S_, P_);
+    else if (m0 == S_ && m1 == P_ && m2 == -1) EDET_FUSE_M(S_, P_, -1);
+    else if (m0 == S_ && m1 == S_ && m2 == U_) EDET_FUSE_M(S_, S_, U_);
+    else if (m0 == S_ && m1 == S_ && m2 == -1) EDET_FUSE_M(S_, S_, -1);
     else hit = false;
+#undef EDET_FUSE_M
     if (hit) return check_launch("edet bifpn_fuse_bwd");
   }
   EDET_DTYPE_DISPATCH(dtype, T, {
