@@ -64,6 +64,7 @@ struct LArgs {
   double* out64;  // se_squeeze / gate_grad output [batch][C]
   int C, accumulate, hw, chunks_per_img;
   RowGeom geo;
+  int cslices;  // k_gate_bn_reduce: channel slices of geo.TPR * 8 channels (1 = whole rows)
 };
 
 // per-channel tables in dynamic LDS: af (sc, sh), mr (mean, rstd), gb (dgamma/M, dbeta/M).
@@ -391,15 +392,17 @@ __global__ __launch_bounds__(256) void k_gate_bn_reduce(LArgs g) {
   const int C = g.C;
   float2* af = reinterpret_cast<float2*>(smem);
   float2* mr = af + C;
-  float* red = reinterpret_cast<float*>(mr + C);  // [R][C] per quantity, reused 5 times
   const RowGeom geo = g.geo;
+  const int CSW = geo.TPR * 8;  // channels of this block's slice (all of C when cslices == 1)
+  float* red = reinterpret_cast<float*>(mr + C);  // [R][CSW] per quantity, reused 5 times
   const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
-  const int n = blockIdx.x / g.chunks_per_img, chunk = blockIdx.x - n * g.chunks_per_img;
+  const int cs = blockIdx.x % g.cslices, bi = blockIdx.x / g.cslices;
+  const int n = bi / g.chunks_per_img, chunk = bi - n * g.chunks_per_img;
   load_tables(g.lz, 0, 1.f / (float)seg_rows(g.p, 0), C, af, mr, nullptr, nullptr);
   __syncthreads();
   const int m_begin = n * g.hw + chunk * geo.CH, m_end = min((n + 1) * g.hw, m_begin + geo.CH);
-  const int c = tv * 8;
-  const bool live = rr < geo.R && tv < C / 8;
+  const int c0 = cs * CSW, c = c0 + tv * 8;
+  const bool live = rr < geo.R && c < C;
   float a[5][8];
 #pragma unroll
   for (int q = 0; q < 5; ++q)
@@ -439,17 +442,23 @@ __global__ __launch_bounds__(256) void k_gate_bn_reduce(LArgs g) {
       }
     }
   }
+  // one block per (image, slice) over the whole image owns its outputs: plain read-add-write
+  // instead of fp64 atomics (C = 1152: 5C atomics from each of 8 blocks per image)
+  const bool owner = g.chunks_per_img == 1;
 #pragma unroll
   for (int q = 0; q < 5; ++q) {
     __syncthreads();
     if (live)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) red[rr * C + c + j] = a[q][j];
+      for (int j = 0; j < 8; ++j) red[rr * CSW + tv * 8 + j] = a[q][j];
     __syncthreads();
-    for (int cc = tid; cc < C; cc += blockDim.x) {
+    for (int cc = tid; cc < CSW; cc += blockDim.x) {
+      if (c0 + cc >= C) break;
       float ss = 0.f;
-      for (int i = 0; i < geo.R; ++i) ss += red[i * C + cc];
-      atomicAdd(g.out64 + ((size_t)q * g.p.batch + n) * C + cc, (double)ss);
+      for (int i = 0; i < geo.R; ++i) ss += red[i * CSW + cc];
+      double* o = g.out64 + ((size_t)q * g.p.batch + n) * C + c0 + cc;
+      if (owner) *o += (double)ss;
+      else atomicAdd(o, (double)ss);
     }
   }
 }
@@ -926,9 +935,19 @@ int edet_gate_bn_reduce(int dtype, const edet_lazy* x, int B, int HW, int C, con
   // long chunks: every block ends in 5C fp64 atomics (0.69 -> 0.54 ms/step at 16 passes vs ~8;
   // 32 passes: 0.58 in round 1, 0.45 against 0.48 in the round-2 sweep after the table hoists)
   g.geo = row_geom(C, dev_knob(12) > 0 ? dev_knob(12) : 32);
+  g.cslices = 1;
+  // wide rows over short images (C >= 480, H*W <= 4096: the 16^2 / 32^2 / 64^2 stages): a block
+  // per (image, 64-channel slice) walks the whole image, 32 rows per pass, and owns its outputs
+  // (development slot 46: 1 = always, 2 = never)
+  const bool sliced = dev_knob(46) == 1 || (dev_knob(46) != 2 && C >= 480 && HW <= 4096);
+  if (sliced) {
+    const int tpr = dev_knob(47) > 0 ? dev_knob(47) : 8;  // development slot 47: vectors per slice
+    g.geo.TPR = tpr; g.geo.R = 256 / tpr; g.geo.VPT = 1; g.geo.CH = HW;
+    g.cslices = cdiv(C / 8, tpr);
+  }
   g.chunks_per_img = cdiv(HW, g.geo.CH);
-  const int nb = B * g.chunks_per_img;
-  const size_t lds = 2 * C * sizeof(float2) + (size_t)g.geo.R * C * sizeof(float);
+  const int nb = B * g.chunks_per_img * g.cslices;
+  const size_t lds = 2 * C * sizeof(float2) + (size_t)g.geo.R * g.geo.TPR * 8 * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
     EDET_LAUNCH(k_gate_bn_reduce<T>, dim3(nb), row_block(g.geo), lds, (hipStream_t)stream, g);
     return check_launch("edet gate_bn_reduce");

@@ -1080,7 +1080,10 @@ def test_transpose_cast(dt):
 
 
 @pytest.mark.parametrize("dt", DTS)
-@pytest.mark.parametrize("C,HW", [(48, 9 * 10), (144, 23 * 17)])
+@pytest.mark.parametrize("C,HW", [(48, 9 * 10), (144, 23 * 17),
+                                  # round 5: C >= 480 over H*W <= 4096 takes one block per (image,
+                                  # 64-channel slice) with plain stores; a partial last slice (520)
+                                  (480, 16 * 16), (1152, 7 * 9), (520, 10 * 10), (672, 64 * 64)])
 def test_gate_bn_reduce_equals_separate_passes(dt, C, HW):
     """edet_gate_bn_reduce + edet_se_bn_combine (one pass) == edet_gate_grad + se_bwd's dsq +
     edet_lazy_bwd_reduce (two passes) on an SE-gated swish(BN) value."""
@@ -1104,7 +1107,9 @@ def test_gate_bn_reduce_equals_separate_passes(dt, C, HW):
     acc2_t, acc2 = bngrad64(1, C)
     L.call("edet_se_bn_combine", B, C, vp(gt), vp(dsq), vp(s5), acc2, stream())
     torch.cuda.synchronize()
-    torch.testing.assert_close(s5[0], dg, rtol=1e-5, atol=1e-6)
+    # fp32 partial sums over the image in another order than edet_gate_grad's: the bar grows
+    # with the terms summed (the sliced form sums 32 row groups of H*W / 32 rows)
+    torch.testing.assert_close(s5[0], dg, rtol=1e-5, atol=1e-6 * max(1.0, HW / 64))
     scale = float(acc_t.abs().max())
     torch.testing.assert_close(acc2_t, acc_t, rtol=1e-4, atol=1e-5 * scale)
     # edet_se_bwd_bn == edet_se_bwd then edet_se_bn_combine (its dsq): the SE gradients bit for
