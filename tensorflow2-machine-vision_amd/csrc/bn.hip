@@ -150,7 +150,10 @@ __device__ __forceinline__ void flush_reduce(const LArgs& g, const RowGeom& geo,
 }
 
 // compile-time cases of the lazy backward row kernels
-enum { AF_BN = 1, AF_ACT = 2, AF_GATE = 4, AF_DSQ = 8 };
+// AF_DVS: a per-image drop-connect scale of dv; AF_ACC (apply): dx accumulates.  Compile-time,
+// so the row loop has no load under a runtime branch (the compiler's wait counts then drained
+// every row's loads: s_waitcnt vmcnt(0) in the loop)
+enum { AF_BN = 1, AF_ACT = 2, AF_GATE = 4, AF_DSQ = 8, AF_DVS = 16, AF_ACC = 32 };
 
 template <typename T, int F>
 __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
@@ -203,7 +206,7 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
             const int n = (mu - off) / hw;
             ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
             ld8((const T*)g.dv + (size_t)mu * C + c, d[u]);
-            dvs[u] = dvsp ? dvsp[n] : 1.f;
+            dvs[u] = (F & AF_DVS) ? dvsp[n] : 1.f;
             if (F & AF_GATE) ld8(g.lz.gate + (size_t)n * C + c, gt[u]);
             if (F & AF_DSQ) ld8(g.dsq + (size_t)n * C + c, ds[u]);
           }
@@ -291,7 +294,7 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g, int nchunks) {
           const int n = (mu - off) / hw;
           ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
           ld8((const T*)g.dv + (size_t)mu * C + c, d[u]);
-          dvs[u] = dvsp ? dvsp[n] : 1.f;
+          dvs[u] = (F & AF_DVS) ? dvsp[n] : 1.f;
           if (F & AF_GATE) ld8(g.lz.gate + (size_t)n * C + c, gt[u]);
           if (F & AF_DSQ) ld8(g.dsq + (size_t)n * C + c, ds[u]);
         }
@@ -308,7 +311,7 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g, int nchunks) {
             const float du = (F & AF_ACT) ? gg * dswishf_(x[u][j] * sc[j] + sh[j]) : gg;
             o[j] = (F & AF_BN) ? sc[j] * du + kb[j] * x[u][j] + kc[j] : du;
           }
-          acc8m(DX + (size_t)mu * C + c, 8, o, g.accumulate);
+          acc8m(DX + (size_t)mu * C + c, 8, o, (F & AF_ACC) ? 1 : 0);
         }
       }
     }
@@ -796,14 +799,14 @@ static int lazy_checks(const edet_lazy* x, const edet_pyramid* p, int C) {
 
 template <typename T, int F = 0>
 static void launch_reduce(int f, dim3 grid, dim3 block, size_t lds, hipStream_t s, const LArgs& g, int nb) {
-  if constexpr (F < 16) {
+  if constexpr (F < 32) {
     if (f == F) EDET_LAUNCH((k_lazy_bwd_reduce<T, F>), grid, block, lds, s, g, nb);
     else launch_reduce<T, F + 2>(f, grid, block, lds, s, g, nb);
   }
 }
 template <typename T, int F = 0>
 static void launch_apply(int f, dim3 grid, dim3 block, size_t lds, hipStream_t s, const LArgs& g, int nb) {
-  if constexpr (F < 16) {
+  if constexpr (F < 64) {
     if (f == F) EDET_LAUNCH((k_lazy_bwd_apply<T, F>), grid, block, lds, s, g, nb);
     else launch_apply<T, F + 1>(f, grid, block, lds, s, g, nb);
   }
@@ -846,7 +849,7 @@ int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, i
     // persistent blocks (r01h sweep: 1.51 -> 1.43 ms/step against 1024)
     const int rcap = dev_knob(11) > 0 ? dev_knob(11) : (C <= 24 ? 256 : 512);
     const int grid = nb < rcap ? nb : rcap;
-    const int f = (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0);
+    const int f = (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0) | (dv_scale ? AF_DVS : 0);
     if (nb) launch_reduce<T>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
     return check_launch("edet lazy_bwd_reduce");
   });
@@ -886,7 +889,8 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
     // 235.6 -> 222.9 us, 524288 x 144 180.5 -> 176.4, r05i sweep), 2048 elsewhere
     const int gcap = dev_knob(9) > 0 ? dev_knob(9) : ((M >= 524288 && C >= 96 && !x->gate) ? 512 : 2048);
     const int grid = nb > gcap ? gcap : nb;
-    const int f = (x->bn.enabled ? AF_BN : 0) | (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0);
+    const int f = (x->bn.enabled ? AF_BN : 0) | (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0) |
+                  (dv_scale ? AF_DVS : 0) | (accumulate ? AF_ACC : 0);
     if (nb) launch_apply<T>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
     return check_launch("edet lazy_bwd_apply");
   });
