@@ -324,10 +324,14 @@ __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int C = g.C;
   float2* af = reinterpret_cast<float2*>(smem);
-  float* red = reinterpret_cast<float*>(af + C);  // [R][C]
   const RowGeom geo = g.geo;
+  // channel slices (as k_gate_bn_reduce): block = (image, slice of geo.TPR vectors), VPT = 1
+  const int CSW = g.cslices > 1 ? geo.TPR * 8 : C;
+  float* red = reinterpret_cast<float*>(af + C);  // [R][CSW]
   const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
-  const int n = blockIdx.x / g.chunks_per_img, chunk = blockIdx.x - n * g.chunks_per_img;
+  const int cs = blockIdx.x % g.cslices, bi = blockIdx.x / g.cslices;
+  const int n = bi / g.chunks_per_img, chunk = bi - n * g.chunks_per_img;
+  const int cvb = cs * geo.TPR;
   load_tables(g.lz, 0, 1.f / (float)seg_rows(g.p, 0), C, af, nullptr, nullptr, nullptr);
   __syncthreads();
   const int m_begin = n * g.hw + chunk * geo.CH, m_end = min((n + 1) * g.hw, m_begin + geo.CH);
@@ -340,7 +344,7 @@ __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
   if (rr < geo.R) {
 #pragma unroll
     for (int v = 0; v < RVPT; ++v) {
-      const int cv = tv + v * geo.TPR;
+      const int cv = cvb + tv + v * geo.TPR;
       if (!(v < geo.VPT && cv < NV)) continue;
       const int c = cv * 8;
       float2 a8[8];  // the 8 channels' affine in registers
@@ -367,18 +371,24 @@ __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
     }
 #pragma unroll
     for (int v = 0; v < RVPT; ++v) {
-      const int cv = tv + v * geo.TPR;
+      const int cv = cvb + tv + v * geo.TPR;
       if (v < geo.VPT && cv < NV)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) red[rr * C + cv * 8 + j] = s[v][j];
+        for (int j = 0; j < 8; ++j) red[rr * CSW + (cv - cvb) * 8 + j] = s[v][j];
     }
   }
   __syncthreads();
-  for (int c = tid; c < C; c += blockDim.x) {
+  // a block over the whole image owns its (image, channel) outputs: read-add-write, no atomics
+  const bool owner = g.chunks_per_img == 1;
+  for (int cc = tid; cc < CSW; cc += blockDim.x) {
+    const int c = cvb * 8 + cc;
+    if (c >= C) break;
     float ss = 0.f;
-    for (int i = 0; i < geo.R; ++i) ss += red[i * C + c];
-    if constexpr (GATEGRAD) atomicAdd(g.out64 + (size_t)n * C + c, (double)ss);
-    else atomicAdd(g.out64 + (size_t)n * C + c, (double)ss / (double)g.hw);
+    for (int i = 0; i < geo.R; ++i) ss += red[i * CSW + cc];
+    const double val = GATEGRAD ? (double)ss : (double)ss / (double)g.hw;
+    double* o = g.out64 + (size_t)n * C + c;
+    if (owner) *o += val;
+    else atomicAdd(o, val);
   }
 }
 
@@ -905,9 +915,16 @@ static int img_reduce(int dtype, bool gategrad, const edet_lazy* x, int B, int H
   g.p.nseg = 1; g.p.batch = B; g.p.row_off[0] = 0; g.p.H[0] = HW; g.p.W[0] = 1;
   g.dv = dv; g.out64 = out64; g.C = C; g.hw = HW;
   g.geo = row_geom(C, 16);  // long chunks: each block ends in C fp64 atomics
+  g.cslices = 1;
+  // C >= 480 over H*W <= 4096: a block per (image, 64-channel slice) over the whole image, as
+  // edet_gate_bn_reduce (development slot 46 = 2: off)
+  if (dev_knob(46) != 2 && C >= 480 && C <= 2048 && HW <= 4096) {
+    g.geo.TPR = 8; g.geo.R = 32; g.geo.VPT = 1; g.geo.CH = HW;
+    g.cslices = cdiv(C / 8, 8);
+  }
   g.chunks_per_img = cdiv(HW, g.geo.CH);
-  const int nb = B * g.chunks_per_img;
-  const size_t lds = C * sizeof(float2) + (size_t)g.geo.R * C * sizeof(float);
+  const int nb = B * g.chunks_per_img * g.cslices;
+  const size_t lds = C * sizeof(float2) + (size_t)g.geo.R * (g.cslices > 1 ? g.geo.TPR * 8 : C) * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
     if (gategrad && x->act) EDET_LAUNCH((k_img_reduce<T, true, true>), dim3(nb), row_block(g.geo), lds, s, g);
     else if (gategrad) EDET_LAUNCH((k_img_reduce<T, true, false>), dim3(nb), row_block(g.geo), lds, s, g);
