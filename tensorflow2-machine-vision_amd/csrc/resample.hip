@@ -1002,10 +1002,13 @@ int edet_stem_wgrad(int dtype, const void* x, int B, int H, int W, const void* d
   const long px = (long)B * cdiv(H, 2) * cdiv(W, 2);
   if (dtype == EDET_BF16 && Cout % 16 == 0 && px > 0) {
     const int OH = cdiv(H, 2), OW = cdiv(W, 2);
-    const int R = std::max(1, std::min(8, 512 / OW));
+    // strips of <= 256 output pixels and 1024 blocks: at 256^2 outputs one row per strip holds the
+    // LDS image at 29 KB (5 blocks per CU instead of 2), 120 -> 91 us (r05y sweep).  Development
+    // slots 48 / 49: output rows per strip / block cap
+    const int R = dev_knob(48) > 0 ? dev_knob(48) : std::max(1, std::min(8, 256 / OW));
     const size_t lds = std::max((size_t)(2 * R + 1) * cdiv(W * 3, 8) * 8 * 2 + (size_t)R * OW * (Cout + 8) * 2,
                                 (size_t)4 * 32 * Cout * 4);
-    const int grid = std::min(B * cdiv(OH, R), 512);
+    const int grid = std::min(B * cdiv(OH, R), dev_knob(49) > 0 ? dev_knob(49) : 1024);
     float* part = workspace_f32((size_t)grid * 27 * Cout);
     if (part && lds <= 96 * 1024) {
       const uint16_t* xb = (const uint16_t*)x;

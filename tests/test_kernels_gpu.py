@@ -807,7 +807,9 @@ def test_residual(dt):
 
 
 @pytest.mark.parametrize("dt", DTS)
-@pytest.mark.parametrize("shape", [(2, 21, 18, 32), (3, 34, 40, 48), (2, 64, 64, 32)])
+@pytest.mark.parametrize("shape", [(2, 21, 18, 32), (3, 34, 40, 48), (2, 64, 64, 32),
+                                   # one output row per weight-gradient strip (OW >= 129)
+                                   (1, 8, 512, 32), (2, 7, 300, 32)])
 def test_stem(dt, shape, workspace_mode):
     rng = np.random.default_rng(9)
     B, H, W, Co = shape
