@@ -13,7 +13,8 @@ Prints ONE JSON line on rank 0 with value = images/s over all ranks, plus
   roofline       : the device kernel with the most time in the step (by base name; the
                    library reports which kernel each call launched): its algorithmic bytes per
                    launch / its average launch duration, timed by wall-clock probes around its
-                   launches inside the captured step graph, vs 8 TB/s HBM; `traffic` = PMC
+                   launches inside the captured step graph (less the interval of an empty probe
+                   pair in the same graph), vs 8 TB/s HBM; `traffic` = PMC
                    HBM bytes per launch from profiles/pmc_traffic.json
   roofline_table : every kernel above 2 % of the step's kernel time (instrumented eager step,
                    HIP events per call): calls, ms, avg us, bytes/launch, GB/s, fraction, PMC ratio
@@ -219,6 +220,18 @@ class KernelTimer:
     def __exit__(self, *exc):
         self.L.call = self.orig
 
+    def empty_pairs(self):
+        """N_EMPTY begin/end pairs with nothing between them, on the current stream (captured with
+        the step): their average interval is the dependent-launch boundary the end probe adds to
+        every timed launch (the begin probe runs before the kernel's own boundary)."""
+        import ctypes
+        from tf2mv_amd.runtime import stream
+        st = stream()
+        for k in range(self.N_EMPTY):
+            slot = ctypes.c_void_p(self.slots.data_ptr() + 24 * (self.max_calls + k))
+            self.orig("edet_probe", slot, 0, st)
+            self.orig("edet_probe", slot, 1, st)
+
     def detail(self, path, top=2000):
         """Per-call table (slowest first): name, shape, us, achieved GB/s."""
         torch.cuda.synchronize()
@@ -257,10 +270,12 @@ class ProbeTimer:
     GPU's constant-rate wall clock.  Only calls that launched exactly the device kernel
     ``kernel`` count in the result (an entry point may pick different kernels per shape)."""
 
+    N_EMPTY = 64  # back-to-back begin/end probe pairs: the probes' own boundary, subtracted
+
     def __init__(self, funcs, kernel, es, max_calls=1024):
         from tf2mv_amd import _lib as L
         self.L, self.funcs, self.kernel, self.es = L, set(funcs), kernel, es
-        self.slots = torch.zeros(max_calls * 3, dtype=torch.int64, device="cuda")
+        self.slots = torch.zeros((max_calls + self.N_EMPTY) * 3, dtype=torch.int64, device="cuda")
         self.max_calls = max_calls
         self.bytes, self.match = [], []
         self.orig = L.call
@@ -294,6 +309,18 @@ class ProbeTimer:
     def __exit__(self, *exc):
         self.L.call = self.orig
 
+    def empty_pairs(self):
+        """N_EMPTY begin/end pairs with nothing between them, on the current stream (captured with
+        the step): their average interval is the dependent-launch boundary the end probe adds to
+        every timed launch (the begin probe runs before the kernel's own boundary)."""
+        import ctypes
+        from tf2mv_amd.runtime import stream
+        st = stream()
+        for k in range(self.N_EMPTY):
+            slot = ctypes.c_void_p(self.slots.data_ptr() + 24 * (self.max_calls + k))
+            self.orig("edet_probe", slot, 0, st)
+            self.orig("edet_probe", slot, 1, st)
+
     def result(self):
         import ctypes
         torch.cuda.synchronize()
@@ -304,9 +331,14 @@ class ProbeTimer:
         sel = [i for i in range(n) if self.match[i] and self.bytes[i] is not None]
         launches = int(sum(int(sl[i, 2]) for i in sel))
         ticks = int(sum(int(sl[i, 1]) for i in sel))
-        avg_us = ticks / max(launches, 1) / (khz.value / 1000.0)
+        raw_us = ticks / max(launches, 1) / (khz.value / 1000.0)
+        em = self.slots.view(-1, 3)[self.max_calls:self.max_calls + self.N_EMPTY].cpu()
+        e_n = int(em[:, 2].sum())
+        overhead_us = (int(em[:, 1].sum()) / e_n / (khz.value / 1000.0)) if e_n else 0.0
+        avg_us = raw_us - overhead_us if raw_us > overhead_us else raw_us
         bpl = sum(self.bytes[i] for i in sel) / max(len(sel), 1)
-        return {"launches": launches, "calls_per_step": len(sel), "avg_launch_us": avg_us, "bytes_per_launch": bpl,
+        return {"launches": launches, "calls_per_step": len(sel), "avg_launch_us": avg_us,
+                "avg_launch_us_raw": raw_us, "probe_overhead_us": overhead_us, "bytes_per_launch": bpl,
                 "achieved_GBps": bpl / avg_us * 1e-3 if avg_us > 0 else None, "clock_khz": khz.value}
 
 
@@ -319,6 +351,7 @@ def probe_roofline(step_fn, funcs, kernel, steps, es):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             step_fn()
+            pt.empty_pairs()
     g.replay()  # warm
     torch.cuda.synchronize()
     pt.slots.zero_()
@@ -522,10 +555,14 @@ def kernel_tables(step_fn, args, el):
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": None if traffic is None else round(traffic),
                     "bytes_per_launch": round(pr["bytes_per_launch"]), "avg_launch_us": round(pr["avg_launch_us"], 2),
+                    "avg_launch_us_raw": round(pr["avg_launch_us_raw"], 2),
+                    "probe_overhead_us": round(pr["probe_overhead_us"], 2),
                     "launches": pr["launches"], "share_of_kernel_time": round(a[1] / total_ms, 4),
                     "timing": "wall-clock probes in the captured step graph, "
-                    f"{args.steps} replays ({pr['ms_per_step']:.2f} ms/step with probes)"}
-        log(f"[bench] roofline {kname}: {pr['launches']} launches, avg {pr['avg_launch_us']:.2f} us, "
+                    f"{args.steps} replays ({pr['ms_per_step']:.2f} ms/step with probes); the interval of "
+                    f"{ProbeTimer.N_EMPTY} empty begin/end probe pairs in the same graph subtracted"}
+        log(f"[bench] roofline {kname}: {pr['launches']} launches, avg {pr['avg_launch_us']:.2f} us "
+            f"({pr['avg_launch_us_raw']:.2f} raw - {pr['probe_overhead_us']:.2f} probe pair), "
             f"{pr['bytes_per_launch'] / 1e6:.2f} MB/launch -> {ach:.1f} GB/s")
     return roofline, table, step_level, kernels
 

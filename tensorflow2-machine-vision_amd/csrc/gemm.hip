@@ -2043,8 +2043,12 @@ static int launch_gemm_s(const GemmArgs& g, hipStream_t s) {
   else if (g.M >= (1 << 21)) cap = 1024;
   if (dev_knob(7) > 0) cap = dev_knob(7);
   const int grid = std::max(1, std::min(cdiv(ngroups, 4), cap));
-  if (LAZY && g.lz.act) EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY, FOLD, 1>), dim3(grid), dim3(256), 0, s, g);
-  else EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY, FOLD, 0>), dim3(grid), dim3(256), 0, s, g);
+  if constexpr (LAZY) {
+    if (g.lz.act) EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY, FOLD, 1>), dim3(grid), dim3(256), 0, s, g);
+    else EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY, FOLD, 0>), dim3(grid), dim3(256), 0, s, g);
+  } else {
+    EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY, FOLD, 0>), dim3(grid), dim3(256), 0, s, g);
+  }
   return check_launch("edet gemm_s");
 }
 
