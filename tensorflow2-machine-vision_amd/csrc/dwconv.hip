@@ -2081,7 +2081,7 @@ constexpr int DWT_CB = 16;  // channels per block
 struct DwtPlan {
   int ntx[EDET_MAX_SEG];     // tiles across an image
   int ntiles[EDET_MAX_SEG];  // tiles per image
-  int chunks[EDET_MAX_SEG];  // tile chunks (of tpb tiles) per image
+  int chunks[EDET_MAX_SEG];  // chunks of tpb consecutive (image, tile) tiles per segment (GIN: per image)
   int nblk[EDET_MAX_SEG];    // blocks of the segment: batch * chunks * ncg
   int tpb, ncg;
 };
@@ -2113,17 +2113,22 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
   while (seg < g.pin.nseg - 1 && id >= pl.nblk[seg]) id -= pl.nblk[seg++];
   const int cg = id % pl.ncg;
   id /= pl.ncg;
-  const int chunk = id % pl.chunks[seg], n = id / pl.chunks[seg];
+  // a chunk is tpb consecutive tiles of the segment's (image, tile) sequence: on the small
+  // planes (one to four tiles per image) a block walks several images of its channel group
+  // (GIN keeps one image per block: its per-image tables would cost the k5 fold form its
+  // second wave per SIMD)
+  const int chunk = GIN ? id % pl.chunks[seg] : id;
+  const int n_gin = GIN ? id / pl.chunks[seg] : 0;
   const int c0 = cg * DWT_CB, C = g.C;
   const int H = g.pin.H[seg], W = g.pin.W[seg];
-  const T* X = (const T*)g.x + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * g.lz.ld + c0;
-  const T* DY = (const T*)(GIN ? g.dyl.dv : g.dy) + ((size_t)g.pout.row_off[seg] + (size_t)n * H * W) * C + c0;
-  const T* YR = GIN ? (const T*)g.dyl.y.x + ((size_t)g.pout.row_off[seg] + (size_t)n * H * W) * C + c0 : nullptr;
-  T* DX = (T*)g.dx + ((size_t)g.pin.row_off[seg] + (size_t)n * H * W) * C + c0;
+  const size_t HW = (size_t)H * W;
+  const T* X0 = (const T*)g.x + (size_t)g.pin.row_off[seg] * g.lz.ld + c0;
+  const T* DY0 = (const T*)(GIN ? g.dyl.dv : g.dy) + (size_t)g.pout.row_off[seg] * C + c0;
+  const T* YR0 = GIN ? (const T*)g.dyl.y.x + (size_t)g.pout.row_off[seg] * C + c0 : nullptr;
+  T* DX0 = (T*)g.dx + (size_t)g.pin.row_off[seg] * C + c0;
   const float inv = 1.f / (float)seg_rows(g.pin, seg);
   if (tid < DWT_CB) {
     af[tid] = bn_affine(g.lz.bn, seg, c0 + tid, inv);
-    gt[tid] = g.lz.gate ? g.lz.gate[(size_t)n * C + c0 + tid] : 1.f;
     if constexpr (GIN) {
       // edet_lazy_bwd_apply's tables (bn.hip load_tables + the kb / kc fold), same arithmetic
       const edet_dgrad_lazy& d = g.dyl;
@@ -2134,14 +2139,16 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
         const float dgm = (float)(d.acc.dgamma[seg][cc] * (double)inv), dbm = (float)(d.acc.dbeta[seg][cc] * (double)inv);
         const float kb = -a.x * q.y * dgm;
         t = make_float4(a.x, a.y, kb, -a.x * dbm - kb * q.x);
-        // one writer per segment and channel: the image-0, first-chunk block
-        if (n == 0 && chunk == 0 && d.grads.a[seg]) {
+        // one writer per segment and channel: the first chunk's block
+        if (n_gin == 0 && chunk == 0 && d.grads.a[seg]) {
           d.grads.a[seg][cc] += (float)d.acc.dgamma[seg][cc];
           d.grads.b[seg][cc] += (float)d.acc.dbeta[seg][cc];
         }
       }
       gtab[tid] = t;
-      ggd[tid] = make_float2(d.y.gate ? d.y.gate[(size_t)n * C + cc] : 1.f, d.dsq ? d.dsq[(size_t)n * C + cc] : 0.f);
+      gt[tid] = g.lz.gate ? g.lz.gate[(size_t)n_gin * C + cc] : 1.f;
+      ggd[tid] = make_float2(d.y.gate ? d.y.gate[(size_t)n_gin * C + cc] : 1.f,
+                             d.dsq ? d.dsq[(size_t)n_gin * C + cc] : 0.f);
     }
   }
   // this thread: channel c, the 4 x 4 patch at rows a0 .., columns b0 .. of every tile
@@ -2158,9 +2165,22 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
   for (int i = 0; i < KK; ++i) dwa[i] = 0.f;
   float fs = 0.f, fq = 0.f;
   const int act = g.lz.act;
-  const int t_begin = chunk * pl.tpb, t_end = min(pl.ntiles[seg], t_begin + pl.tpb);
+  const int nt = pl.ntiles[seg];
+  const int t_begin = chunk * pl.tpb, t_end = min((GIN ? 1 : g.pin.batch) * nt, t_begin + pl.tpb);
+  int cur_n = -1;
   for (int t = t_begin; t < t_end; ++t) {
-    const int y0 = (t / pl.ntx[seg]) * DWT_T, x0 = (t % pl.ntx[seg]) * DWT_T;
+    const int n = GIN ? n_gin : t / nt, tl = GIN ? t : t - n * nt;
+    const int y0 = (tl / pl.ntx[seg]) * DWT_T, x0 = (tl % pl.ntx[seg]) * DWT_T;
+    const T* X = X0 + n * HW * g.lz.ld;
+    const T* DY = DY0 + n * HW * C;
+    const T* YR = GIN ? YR0 + n * HW * C : nullptr;
+    T* DX = DX0 + n * HW * C;
+    if constexpr (!GIN) {
+      if (n != cur_n) {  // this image's SE gate (read in the commit, after the barrier below)
+        cur_n = n;
+        if (tid < DWT_CB) gt[tid] = g.lz.gate ? g.lz.gate[(size_t)n * C + c0 + tid] : 1.f;
+      }
+    }
     // ---- the halo window of dy and x: every vector requested before any is used
     uint4 rd[NL], rx[NL], ry[GIN ? NL : 1];
     uint32_t okm = 0;
@@ -2381,8 +2401,9 @@ static int launch_dwt(DwArgs g, const edet_bngrad64& fold, hipStream_t s) {
   pl.tpb = tpb;
   long total = 0;
   for (int i = 0; i < g.pin.nseg; ++i) {
-    pl.chunks[i] = cdiv(pl.ntiles[i], tpb);
-    pl.nblk[i] = g.pin.batch * pl.chunks[i] * pl.ncg;
+    // chunks span images (GIN: chunks of one image, per image)
+    pl.chunks[i] = cdiv((GIN ? 1 : g.pin.batch) * pl.ntiles[i], tpb);
+    pl.nblk[i] = (GIN ? g.pin.batch : 1) * pl.chunks[i] * pl.ncg;
     total += pl.nblk[i];
   }
   if (total == 0) return EDET_OK;

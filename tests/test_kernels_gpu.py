@@ -264,16 +264,18 @@ def test_dwconv_fwd_bwd(dt, k, s, H, W, C, lazy, nseg, workspace_mode):
 
 
 @pytest.mark.parametrize("dt", DTS)
-@pytest.mark.parametrize("k,H,W,C,act,nseg,fold,acc", [
-    (3, 16, 16, 32, 1, 1, True, 0), (5, 11, 12, 40, 1, 1, True, 0), (3, 9, 9, 64, 1, 2, True, 0),
-    (5, 10, 11, 1152, 1, 1, True, 0), (3, 34, 37, 96, 0, 1, True, 0), (5, 33, 20, 144, 1, 1, False, 1),
-    (3, 8, 9, 480, 1, 1, False, 0), (5, 70, 66, 64, 1, 1, True, 0)])
-def test_dwconv_bwd_fused(dt, k, H, W, C, act, nseg, fold, acc):
+@pytest.mark.parametrize("k,H,W,C,act,nseg,fold,acc,B", [
+    (3, 16, 16, 32, 1, 1, True, 0, 2), (5, 11, 12, 40, 1, 1, True, 0, 2), (3, 9, 9, 64, 1, 2, True, 0, 2),
+    (5, 10, 11, 1152, 1, 1, True, 0, 2), (3, 34, 37, 96, 0, 1, True, 0, 2), (5, 33, 20, 144, 1, 1, False, 1, 2),
+    (3, 8, 9, 480, 1, 1, False, 0, 2), (5, 70, 66, 64, 1, 1, True, 0, 2),
+    # enough tiles for several tiles per block: the tiled form's chunks then span images
+    # (one 16 x 16 tile per image; a two-level pyramid of one-tile planes)
+    (5, 16, 16, 1152, 1, 1, True, 0, 64), (3, 8, 8, 64, 1, 2, True, 0, 400)])
+def test_dwconv_bwd_fused(dt, k, H, W, C, act, nseg, fold, acc, B):
     """edet_dwconv_bwd (stride 1): dx, the filter gradient and the folded BN-backward sums of
     the input's BatchNorm from one pass, against fp64 autograd and against the separate entry
     points (dgrad, wgrad, lazy_bwd_reduce over the same dx)."""
     rng = np.random.default_rng(k * 1000 + H * 10 + C)
-    B = 2
     pin = Pyr(B, [(H, W), ((H + 1) // 2, (W + 1) // 2)]) if nseg == 2 else Pyr(B, [(H, W)])
     x = pyr_data(rng, pin, C, dt, scale=2.0)
     bn = make_bn(x, pin, C, rng)
