@@ -67,17 +67,19 @@ def test_hot_kernel_occupancy(table, prefix, floor):
         assert w >= floor, f"{r['pretty']}: {w} waves/SIMD (VGPR {r.get('vgpr_count')}, AGPR {r.get('agpr_count')}) < {floor}"
 
 
-def test_wgrad_pipeline_waits_are_partial():
-    """The plain bf16 weight gradient's stage loop (round 4, DESIGN.md "Loads the compiler can
-    count") waits for one stage's loads at a time: no s_waitcnt vmcnt(0) in the loop, which
-    would drain the stage fetched ahead as well (scripts/wait_scan.py)."""
+@pytest.mark.parametrize("inst", ["false, 64, 2, 0", "true, 64, 2, 0", "true, 64, 2, 1"])
+def test_wgrad_pipeline_waits_are_partial(inst):
+    """The bf16 weight gradient's stage loop (round 4, DESIGN.md "Loads the compiler can count";
+    the lazy instances since the round-5 gate fetch) waits for one stage's loads at a time: no
+    s_waitcnt vmcnt(0) in the loop, which would drain the stage fetched ahead as well
+    (scripts/wait_scan.py).  Plain A, lazy BN-only A and lazy BN + swish A."""
     if not os.path.exists(LIB) or not os.path.exists(kr.READELF):
         pytest.skip("libedet.so or llvm tools not available")
     ws = pytest.importorskip("wait_scan")
     if not os.path.exists(ws.OBJDUMP):
         pytest.skip("llvm-objdump not available")
-    found = ws.scan(LIB, "void edet::k_wgrad_tr<false, 64, 2, 0>")
-    assert found, "k_wgrad_tr<false, 64, 2, 0> not in the library"
+    found = ws.scan(LIB, f"void edet::k_wgrad_tr<{inst}>")
+    assert found, f"k_wgrad_tr<{inst}> not in the library"
     (_, loops), = found
     main = loops[0]
     assert main["loads"] >= 8 and main["vmcnt"], main
