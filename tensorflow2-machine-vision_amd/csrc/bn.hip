@@ -155,6 +155,27 @@ __device__ __forceinline__ void flush_reduce(const LArgs& g, const RowGeom& geo,
 // every row's loads: s_waitcnt vmcnt(0) in the loop)
 enum { AF_BN = 1, AF_ACT = 2, AF_GATE = 4, AF_DSQ = 8, AF_DVS = 16, AF_ACC = 32 };
 
+// streaming (nontemporal) 16-byte row accesses for the applies over tensors far larger than the
+// caches (development slot 53 = 1)
+typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void ld8_nt(const uint16_t* p, float* o) {
+  const u32x4_nt v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(p));
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(w[i] << 16);
+    o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void st8_nt(uint16_t* p, const float* v) {
+  u32x4_nt w;
+  w.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  w.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  w.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+  w.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4_nt*>(p));
+}
+
 template <typename T, int F>
 __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -237,7 +258,7 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
 //   u = x*sc + sh,   dx = sc*du + kb*x + kc   with kb = -sc*rstd*dgamma/M,
 //   kc = -sc*dbeta/M + sc*rstd*mean*dgamma/M   (= sc*(du - dbeta/M - xhat*dgamma/M))
 // so the row loop is loads, ~10 VALU per element and stores (no LDS, no per-element branches).
-template <typename T, int F>
+template <typename T, int F, bool NT = false>
 __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g, int nchunks) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int C = g.C;
@@ -292,8 +313,13 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g, int nchunks) {
         for (int u = 0; u < EU; ++u) {
           const int mu = min(m + u * geo.R, m_end - 1);
           const int n = (mu - off) / hw;
-          ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
-          ld8((const T*)g.dv + (size_t)mu * C + c, d[u]);
+          if constexpr (NT && sizeof(T) == 2) {
+            ld8_nt((const uint16_t*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
+            ld8_nt((const uint16_t*)g.dv + (size_t)mu * C + c, d[u]);
+          } else {
+            ld8((const T*)g.lz.x + (size_t)mu * g.lz.ld + c, x[u]);
+            ld8((const T*)g.dv + (size_t)mu * C + c, d[u]);
+          }
           dvs[u] = (F & AF_DVS) ? dvsp[n] : 1.f;
           if (F & AF_GATE) ld8(g.lz.gate + (size_t)n * C + c, gt[u]);
           if (F & AF_DSQ) ld8(g.dsq + (size_t)n * C + c, ds[u]);
@@ -311,7 +337,8 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g, int nchunks) {
             const float du = (F & AF_ACT) ? gg * dswishf_(x[u][j] * sc[j] + sh[j]) : gg;
             o[j] = (F & AF_BN) ? sc[j] * du + kb[j] * x[u][j] + kc[j] : du;
           }
-          acc8m(DX + (size_t)mu * C + c, 8, o, (F & AF_ACC) ? 1 : 0);
+          if constexpr (NT && sizeof(T) == 2 && !(F & AF_ACC)) st8_nt((uint16_t*)(DX + (size_t)mu * C + c), o);
+          else acc8m(DX + (size_t)mu * C + c, 8, o, (F & AF_ACC) ? 1 : 0);
         }
       }
     }
@@ -814,11 +841,11 @@ static void launch_reduce(int f, dim3 grid, dim3 block, size_t lds, hipStream_t 
     else launch_reduce<T, F + 2>(f, grid, block, lds, s, g, nb);
   }
 }
-template <typename T, int F = 0>
+template <typename T, bool NT = false, int F = 0>
 static void launch_apply(int f, dim3 grid, dim3 block, size_t lds, hipStream_t s, const LArgs& g, int nb) {
   if constexpr (F < 64) {
-    if (f == F) EDET_LAUNCH((k_lazy_bwd_apply<T, F>), grid, block, lds, s, g, nb);
-    else launch_apply<T, F + 1>(f, grid, block, lds, s, g, nb);
+    if (f == F) EDET_LAUNCH((k_lazy_bwd_apply<T, F, NT>), grid, block, lds, s, g, nb);
+    else launch_apply<T, NT, F + 1>(f, grid, block, lds, s, g, nb);
   }
 }
 
@@ -901,6 +928,14 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
     const int grid = nb > gcap ? gcap : nb;
     const int f = (x->bn.enabled ? AF_BN : 0) | (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0) |
                   (dv_scale ? AF_DVS : 0) | (accumulate ? AF_ACC : 0);
+    // nontemporal row loads / stores over >= 524288 rows (2M x 96: 222 -> 215 us, 524288 x 144:
+    // 87 -> 83; on every apply they cost the small ones their cache hits, r05an).  Development
+    // slot 53: 1 = from slot 54's row count, 2 = never
+    const long nt_rows = dev_knob(53) == 1 ? dev_knob(54) : 524288;
+    if (nb && sizeof(T) == 2 && !accumulate && dev_knob(53) != 2 && M >= nt_rows) {
+      launch_apply<T, true>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
+      return check_launch("edet lazy_bwd_apply");
+    }
     if (nb) launch_apply<T>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);
     return check_launch("edet lazy_bwd_apply");
   });
