@@ -335,10 +335,15 @@ class ProbeTimer:
         em = self.slots.view(-1, 3)[self.max_calls:self.max_calls + self.N_EMPTY].cpu()
         e_n = int(em[:, 2].sum())
         overhead_us = (int(em[:, 1].sum()) / e_n / (khz.value / 1000.0)) if e_n else 0.0
-        avg_us = raw_us - overhead_us if raw_us > overhead_us else raw_us
+        # the headline is the raw probe interval (subtracting the empty pair's whole
+        # interval took the average below rocprof's kernel duration); the corrected figure is
+        # reported beside it, never used for `achieved`
+        avg_us = raw_us
+        corr_us = raw_us - overhead_us if raw_us > overhead_us else raw_us
         bpl = sum(self.bytes[i] for i in sel) / max(len(sel), 1)
         return {"launches": launches, "calls_per_step": len(sel), "avg_launch_us": avg_us,
-                "avg_launch_us_raw": raw_us, "probe_overhead_us": overhead_us, "bytes_per_launch": bpl,
+                "avg_launch_us_raw": raw_us, "avg_launch_us_less_probe_pair": corr_us,
+                "probe_overhead_us": overhead_us, "bytes_per_launch": bpl,
                 "achieved_GBps": bpl / avg_us * 1e-3 if avg_us > 0 else None, "clock_khz": khz.value}
 
 
@@ -555,14 +560,16 @@ def kernel_tables(step_fn, args, el):
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": None if traffic is None else round(traffic),
                     "bytes_per_launch": round(pr["bytes_per_launch"]), "avg_launch_us": round(pr["avg_launch_us"], 2),
-                    "avg_launch_us_raw": round(pr["avg_launch_us_raw"], 2),
+                    "avg_launch_us_less_probe_pair": round(pr["avg_launch_us_less_probe_pair"], 2),
                     "probe_overhead_us": round(pr["probe_overhead_us"], 2),
                     "launches": pr["launches"], "share_of_kernel_time": round(a[1] / total_ms, 4),
                     "timing": "wall-clock probes in the captured step graph, "
-                    f"{args.steps} replays ({pr['ms_per_step']:.2f} ms/step with probes); the interval of "
-                    f"{ProbeTimer.N_EMPTY} empty begin/end probe pairs in the same graph subtracted"}
-        log(f"[bench] roofline {kname}: {pr['launches']} launches, avg {pr['avg_launch_us']:.2f} us "
-            f"({pr['avg_launch_us_raw']:.2f} raw - {pr['probe_overhead_us']:.2f} probe pair), "
+                    f"{args.steps} replays ({pr['ms_per_step']:.2f} ms/step with probes); avg_launch_us is "
+                    "the raw begin-to-end probe interval (it includes the probes' own launch boundary, so "
+                    "it is an upper bound on the kernel's duration); avg_launch_us_less_probe_pair "
+                    f"subtracts the interval of {ProbeTimer.N_EMPTY} empty begin/end pairs in the same graph"}
+        log(f"[bench] roofline {kname}: {pr['launches']} launches, avg {pr['avg_launch_us']:.2f} us raw "
+            f"({pr['avg_launch_us_less_probe_pair']:.2f} less {pr['probe_overhead_us']:.2f} probe pair), "
             f"{pr['bytes_per_launch'] / 1e6:.2f} MB/launch -> {ach:.1f} GB/s")
     return roofline, table, step_level, kernels
 

@@ -174,7 +174,8 @@ int edet_launched_kernels(char* buf, size_t size);
 int edet_dev_set(int slot, int value);
 
 /* ---- pointwise (1x1) convolution: y[m][n] = sum_k v(a)[m][k] * wt[n][k] + bias[n] ----
- * wt is [N][K] in `dtype`.  `stats` (nullable) receives per-segment column sums of y. */
+ * wt is [N][K] in `dtype`.  `stats` (nullable) receives per-segment column sums of y.
+ * accumulate = 1 needs a plain A (a->bn disabled, no act, no gate): EDET_EINVAL otherwise. */
 int edet_conv1x1_fwd(int dtype, const edet_lazy* a, const edet_pyramid* rows, int K,
                      const void* wt, int N, const float* bias, void* y, int ldy,
                      int accumulate, const edet_statout* stats, edet_stream_t stream);

@@ -179,6 +179,28 @@ def _cki(kh, kw, out):
     return ("normal", math.sqrt(2.0 / (kh * kw * out)))
 
 
+def bf16_store(t):
+    """bf16 storage of a tensor the product keeps in HBM, both directions: the value is rounded
+    on the forward, and (through .to's autograd) the incoming gradient on the backward."""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class _GradBF16(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+def bf16_grad(t):
+    """Identity forward, bf16 rounding of the gradient: a value the product never stores (a lazy
+    BN / swish output) whose gradient its consumer's dgrad writes in bf16."""
+    return _GradBF16.apply(t)
+
+
 class RefEfficientDet:
     """Restatement of EfficientDetNet (efficientdet_net.py:10-95) + EfficientDetNetTrain."""
 
@@ -205,6 +227,7 @@ class RefEfficientDet:
         self.routes = None  # name -> values deciding max-pool winners (see maxpool_same)
         self.route_stats = {}
         self.store = None  # storage rounding of every tensor the product keeps in HBM (bf16 emulation)
+        self.gstore = None  # gradient rounding at every conv / resample input (the stored dv)
         self._names = {}
         self.p = {}
         if params is not None:
@@ -225,6 +248,16 @@ class RefEfficientDet:
         """A tensor the product stores (conv outputs, SE output, fusion sums, residual sums,
         pooled values): rounded by ``store`` when emulating a storage precision."""
         return x if self.store is None or self.recording is not None else self.store(x)
+
+    def _gin(self, x):
+        """A conv or resample input: its gradient is what the product's dgrad / fusion backward
+        stores, rounded by ``gstore`` when emulating a storage precision."""
+        if self.gstore is None or self.recording is not None:
+            return x
+        y = self.gstore(x)
+        if id(x) in self._names:  # keep the pool routing's name on the wrapped value
+            self._names[id(y)] = self._names[id(x)]
+        return y
 
     def _pool(self, x, stored):
         route = None
@@ -288,10 +321,10 @@ class RefEfficientDet:
         cin, e = b["cin"], b["cin"] * b["e"]
         if b["e"] != 1:
             n = conv_name()
-            x = self._st(Fn.conv2d(x, self.w1x1(f"{pre}/{n}/kernel", e, cin, _cki(1, 1, e))))
+            x = self._st(Fn.conv2d(self._gin(x), self.w1x1(f"{pre}/{n}/kernel", e, cin, _cki(1, 1, e))))
             x = self._t(f"{pre}/expand", swish(self.bn(x, f"{pre}/{bn_name()}", training, st)))
         k = b["k"]
-        x = self._st(conv_same(x, self.wdw(f"{pre}/depthwise_conv2d/depthwise_kernel", k, e, _cki(k, k, 1)), b["s"],
+        x = self._st(conv_same(self._gin(x), self.wdw(f"{pre}/depthwise_conv2d/depthwise_kernel", k, e, _cki(k, k, 1)), b["s"],
                                groups=e))
         x = swish(self.bn(x, f"{pre}/{bn_name()}", training, st))
         # SE (layers/se.py:35-39), width mb_conv_block.py:98-101
@@ -303,7 +336,7 @@ class RefEfficientDet:
                       self.w(f"{pre}/se/conv2d_1/bias", (e,), ("const", 0.0)))
         x = self._t(f"{pre}/se_out", self._st(torch.sigmoid(s) * x))
         n = conv_name()
-        x = self._st(Fn.conv2d(x, self.w1x1(f"{pre}/{n}/kernel", b["cout"], e, _cki(1, 1, b["cout"]))))
+        x = self._st(Fn.conv2d(self._gin(x), self.w1x1(f"{pre}/{n}/kernel", b["cout"], e, _cki(1, 1, b["cout"]))))
         return self._t(f"{pre}/project", self.bn(x, f"{pre}/{bn_name()}", training, st))
 
     def resample(self, x, prefix, level_size, training, st):
@@ -311,6 +344,7 @@ class RefEfficientDet:
         tensor's channels and height, as its lazy build() makes them."""
         F = self.F
         C = x.shape[1]
+        x = self._gin(x)
         if C != F:
             x = self._st(Fn.conv2d(x, self.w1x1(f"{prefix}/conv2d/kernel", F, C, ("glorot", C, F)),
                                    self.w(f"{prefix}/conv2d/bias", (F,), ("const", 0.0))))
@@ -323,8 +357,8 @@ class RefEfficientDet:
 
     def sepconv(self, x, pre, dwname, pwname, bname, nout, dw_init, pw_init, b_init):
         C = x.shape[1]
-        x = self._st(conv_same(x, self.wdw(f"{pre}/{dwname}", 3, C, dw_init), 1, groups=C))
-        return self._st(Fn.conv2d(x, self.w1x1(f"{pre}/{pwname}", nout, C, pw_init),
+        x = self._st(conv_same(self._gin(x), self.wdw(f"{pre}/{dwname}", 3, C, dw_init), 1, groups=C))
+        return self._st(Fn.conv2d(self._gin(x), self.w1x1(f"{pre}/{pwname}", nout, C, pw_init),
                                   self.w(f"{pre}/{bname}", (nout,), b_init)))
 
     # bifpn.py:108-116: (level, input node ids); ids 0..4 = P3..P7 inputs, 5.. = nodes

@@ -13,7 +13,9 @@ Reference chain (all OpenCV, cv2 is not in this image):
                    293-330), then BGR->RGB and /255
   5. boxes         clip to the frame, drop < 2 px, reorder (coco_dataset_one.py:138-151)
 
-Here the draws (Python ``random``, in the reference's order), the transform matrices and the
+Here the draws (Python ``random``, exactly the reference's calls in its order; the noise seed from
+a separate numpy stream, as the reference's noise comes from numpy's global RNG and consumes
+nothing from ``random``), the transform matrices and the
 box-corner geometry run on the host in numpy float32 / float64, op for op as the reference
 computes them (bit-exact against that restatement: tests/test_augment.py), and the pixel work
 -- blur, warp, noise, resize + border + normalisation -- is one ``edet_augment_image`` call
@@ -52,10 +54,13 @@ class AugmentDraw:
         return AugmentDraw(0, (0.0, 0.0), (1.0, 1.0), (0, 0, 0), False, 0, tuple(pad_bg), False)
 
 
-def draw(rng: random.Random) -> AugmentDraw:
-    """coco_dataset_one.py:99-126 / image_helper.py:207-214, 312-318: the same calls in the
-    same order (randint(0, 4); four random(); getRandomColor + random() in the warp; the
-    noise; getRandomColor + random() in the resize)."""
+def draw(rng: random.Random, np_rng: Optional[np.random.Generator] = None) -> AugmentDraw:
+    """coco_dataset_one.py:99-126 / image_helper.py:207-214, 312-318: the same calls on the
+    Python ``random`` stream in the same order (randint(0, 4); four random(); getRandomColor +
+    random() in the warp; getRandomColor + random() in the resize). The noise
+    (image_helper.py:249) draws from numpy's RNG, not from ``random``: its seed comes from
+    ``np_rng`` (default: numpy's global RNG, as the reference), so the ``random`` sequence --
+    and with it the next image's draws and the generator's shuffle -- is the reference's."""
     ksize = rng.randint(0, 4)
     ox = rng.random() * 90 - 45
     oy = rng.random() * 90 - 45
@@ -63,7 +68,8 @@ def draw(rng: random.Random) -> AugmentDraw:
     sy = rng.random() * 1.5 + 0.5
     wbg = (rng.randint(0, 255), rng.randint(0, 255), rng.randint(0, 255))
     wrep = rng.random() >= 0.5
-    seed = rng.getrandbits(64)
+    seed = (int(np_rng.integers(0, 2**63, dtype=np.int64)) if np_rng is not None
+            else int(np.random.randint(0, 2**63, dtype=np.int64)))
     pbg = (rng.randint(0, 255), rng.randint(0, 255), rng.randint(0, 255))
     prep = rng.random() >= 0.5
     return AugmentDraw(ksize, (ox, oy), (sx, sy), wbg, wrep, seed, pbg, prep)
@@ -190,8 +196,8 @@ def augment_one(img: np.ndarray, lab: dict, d: AugmentDraw, size: Tuple[int, int
 
 
 def augment_batch(images: Sequence[np.ndarray], labels: Sequence[dict], rng: random.Random, size: Tuple[int, int],
-                  out, dtype_code: int, identity: bool = False):
+                  out, dtype_code: int, identity: bool = False, np_rng: Optional[np.random.Generator] = None):
     """augment_one over a batch, one draw per image (identity: the deterministic chain).
     Samples left without boxes give None and leave their slot of ``out`` unwritten."""
-    return [augment_one(img, lab, AugmentDraw.identity() if identity else draw(rng), size, out[b], dtype_code,
-                        identity) for b, (img, lab) in enumerate(zip(images, labels))]
+    return [augment_one(img, lab, AugmentDraw.identity() if identity else draw(rng, np_rng), size, out[b],
+                        dtype_code, identity) for b, (img, lab) in enumerate(zip(images, labels))]

@@ -2401,6 +2401,9 @@ int edet_conv1x1_fwd(int dtype, const edet_lazy* a, const edet_pyramid* rows, in
   if (stats) g.stats = *stats;
   hipStream_t s = (hipStream_t)stream;
   const bool plain = lazy_is_plain(a);
+  // the lazy K-loop instances store without reading C (the accumulating instance is the plain
+  // dgrads' compile-time case): an accumulating forward needs a plain A
+  EDET_REQUIRE(!accumulate || plain, "conv1x1_fwd: accumulate=1 needs a plain A (no BN / act / gate)");
   EDET_DTYPE_DISPATCH(dtype, T, {
     return plain ? dispatch_gemm<T, false>(g, s) : dispatch_gemm<T, true>(g, s);
   });

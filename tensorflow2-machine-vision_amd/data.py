@@ -213,6 +213,9 @@ class DataGenerator:
         self.image_size = tuple(anchors.image_size)
         self.is_train = is_train
         self.rng = random.Random(seed)
+        # the augmentation noise's stream (numpy's RNG in the reference, image_helper.py:249):
+        # seeded alongside rng for reproducible runs, numpy's global RNG otherwise
+        self.np_rng = np.random.default_rng(seed) if seed is not None else None
         self.LoadClasses()
         self.LoadLabels()
 
@@ -318,7 +321,7 @@ def GetDataSet(image_path: str, label_path: str, classes_path: str, batch_size: 
             samples = []
             while len(samples) < batch_size:
                 lab = next(it)
-                r = AUG.augment_one(read_image(lab["image_path"]), lab, AUG.draw(gen.rng), (W, H), x[len(samples)],
+                r = AUG.augment_one(read_image(lab["image_path"]), lab, AUG.draw(gen.rng, gen.np_rng), (W, H), x[len(samples)],
                                     L.F32 if dtype == "f32" else L.BF16)
                 if r is not None:
                     samples.append((None, r[0], r[1]))

@@ -15,22 +15,74 @@ from tf2mv_amd import augment as A
 from tf2mv_amd import data as D
 
 
+class _Recorder(random.Random):
+    """A random.Random that logs each public call made on it."""
+
+    def __init__(self, seed):
+        self.calls, self._depth = [], 0
+        super().__init__(seed)
+
+    def _log(self, name, fn, *a):
+        if self._depth == 0:  # top-level calls only (randint draws through getrandbits)
+            self.calls.append((name,) + a if a else name)
+        self._depth += 1
+        try:
+            return fn(*a)
+        finally:
+            self._depth -= 1
+
+    def random(self):
+        return self._log("random", super().random)
+
+    def randint(self, a, b):
+        return self._log("randint", super().randint, a, b)
+
+    def getrandbits(self, k):
+        return self._log("getrandbits", super().getrandbits, k)
+
+
+# coco_dataset_one.py:99 (ksize), :106-107 (offset x, y), :110-111 (scale x, y);
+# image_helper.py:211 + :223-227 getRandomColor, :213 border mode (the warp);
+# opencvNoise (image_helper.py:249) draws from numpy, not from random;
+# image_helper.py:312-318 getRandomColor + border mode (the resize).
+_REFERENCE_CALLS = ([("randint", 0, 4)] + ["random"] * 4 + [("randint", 0, 255)] * 3 + ["random"]
+                    + [("randint", 0, 255)] * 3 + ["random"])
+
+
 def test_draw_follows_reference_call_order():
-    """randint(0, 4); random() x4 (offset x, y, scale x, y); getRandomColor (3 x randint(0,
-    255)) + random() of the warp; the noise seed; getRandomColor + random() of the resize."""
-    r1, r2 = random.Random(5), random.Random(5)
-    d = A.draw(r1)
+    """The Python random stream sees exactly the reference's calls, in its order, and nothing
+    for the noise (written out by hand from the reference above, not re-derived from draw)."""
+    r = _Recorder(5)
+    d = A.draw(r, np.random.default_rng(0))
+    assert r.calls == _REFERENCE_CALLS
+    # the values are the ones those calls return, in that order
+    r2 = random.Random(5)
     k = r2.randint(0, 4)
     off = (r2.random() * 90 - 45, r2.random() * 90 - 45)
     sc = (r2.random() * 1.5 + 0.5, r2.random() * 1.5 + 0.5)
     wbg = (r2.randint(0, 255), r2.randint(0, 255), r2.randint(0, 255))
     wrep = r2.random() >= 0.5
-    seed = r2.getrandbits(64)
     pbg = (r2.randint(0, 255), r2.randint(0, 255), r2.randint(0, 255))
     prep = r2.random() >= 0.5
-    assert (d.ksize, d.offset, d.scale, d.warp_bg, d.warp_replicate, d.noise_seed, d.pad_bg, d.pad_replicate) == \
-        (k, off, sc, wbg, wrep, seed, pbg, prep)
+    assert (d.ksize, d.offset, d.scale, d.warp_bg, d.warp_replicate, d.pad_bg, d.pad_replicate) == \
+        (k, off, sc, wbg, wrep, pbg, prep)
     assert 0 <= d.ksize <= 4 and all(-45 <= o <= 45 for o in d.offset) and all(0.5 <= s <= 2 for s in d.scale)
+
+
+def test_noise_seed_uses_numpy_stream_only():
+    """The noise seed comes from the numpy generator (or numpy's global RNG): the same Python
+    stream gives the same draws whatever the numpy stream, and the next draw from the Python
+    stream is the one the reference would make next."""
+    r1, r2 = random.Random(9), random.Random(9)
+    d1 = A.draw(r1, np.random.default_rng(1))
+    d2 = A.draw(r2, np.random.default_rng(2))
+    assert d1.noise_seed != d2.noise_seed
+    assert (d1.ksize, d1.offset, d1.scale, d1.pad_bg) == (d2.ksize, d2.offset, d2.scale, d2.pad_bg)
+    assert r1.random() == r2.random()
+    np.random.seed(3)
+    a = A.draw(random.Random(1)).noise_seed
+    np.random.seed(3)
+    assert A.draw(random.Random(1)).noise_seed == a
 
 
 def test_perspective_matrix_structure():

@@ -144,3 +144,52 @@ def test_augment_batch_on_the_label_sample(tmp_path):
         assert boxes.shape[1] == 4 and len(boxes) == len(cls)
         assert (boxes[:, 2] - boxes[:, 0] >= 2).all() and (boxes[:, 3] - boxes[:, 1] >= 2).all()
         assert (boxes >= 0).all() and (boxes <= 512).all()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_getdataset_augment_end_to_end(tmp_path, dtype):
+    """GetDataSet(augment=True) (coco_dataset_one.py:214-246 with get_random_data's chain): a
+    batch pulled from the generator has the batch shape and storage dtype, pixels in [0, 1],
+    and targets equal to generate_targets_batched of the draws' own boxes -- the augmented
+    boxes are recomputed here from the same seeded streams through augment_geometry."""
+    from PIL import Image
+    from tf2mv_amd.anchors import Anchors
+    here = os.path.dirname(os.path.abspath(__file__))
+    rng = np.random.default_rng(0)
+    Image.fromarray(rng.integers(0, 256, (480, 640, 3), dtype=np.uint8)).save(tmp_path / "img_a.png")
+    Image.fromarray(rng.integers(0, 256, (640, 480, 3), dtype=np.uint8)).save(tmp_path / "img_b.png")
+    S = 128
+    anchors = Anchors(3, 7, (S, S), 3, [(1.0, 1.0), (1.4, 0.7), (0.7, 1.4)], 4.0, device="cuda")
+    it, gen = D.GetDataSet(str(tmp_path), os.path.join(here, "golden", "data", "labels.txt"),
+                           os.path.join(here, "golden", "data", "classes.txt"), 3, anchors, is_train=True,
+                           seed=11, augment=True, dtype=dtype)
+    x, t = next(it)
+    torch.cuda.synchronize()
+    assert x.shape == (3, S, S, 3) and x.is_cuda
+    assert x.dtype == (torch.float32 if dtype == "f32" else torch.bfloat16)
+    xf = x.float().cpu().numpy()
+    assert np.isfinite(xf).all() and xf.min() >= 0 and xf.max() <= 1 and xf.std() > 0.05
+    # replay the generator's streams on the host: same label order, same draws, same geometry
+    ref_gen = D.DataGenerator(str(tmp_path), os.path.join(here, "golden", "data", "labels.txt"),
+                              os.path.join(here, "golden", "data", "classes.txt"), anchors, True, 11)
+    labs = ref_gen.generate_labels()
+    samples = []
+    while len(samples) < 3:
+        lab = next(labs)
+        img = D.read_image(lab["image_path"])
+        d = A.draw(ref_gen.rng, ref_gen.np_rng)
+        h, w = img.shape[:2]
+        _, pts, _ = A.augment_geometry(w, h, d, np.array(lab["boxes"], np.float64).reshape(-1, 2), (S, S))
+        bx = pts.reshape(-1, 4)
+        bx[:, 0][bx[:, 0] < 0] = 0
+        bx[:, 1][bx[:, 1] < 0] = 0
+        bx[:, 2][bx[:, 2] > S] = S
+        bx[:, 3][bx[:, 3] > S] = S
+        keep = np.logical_and(bx[:, 2] - bx[:, 0] >= 2, bx[:, 3] - bx[:, 1] >= 2)
+        if keep.any():
+            samples.append((None, bx[keep][:, [1, 0, 3, 2]], np.array(lab["classes"], np.int32)[keep]))
+    _, gb, gc, n = D.collate([(np.zeros((1,)), b, c) for _, b, c in samples])
+    ref = anchors.generate_targets_batched(gb, gc, n)
+    for f in ("cls", "mask"):
+        np.testing.assert_array_equal(getattr(t, f).cpu().numpy(), getattr(ref, f).cpu().numpy())
+    np.testing.assert_array_equal(t.box.cpu().numpy(), ref.box.cpu().numpy())

@@ -44,3 +44,18 @@ def test_error_path_without_gpu():
         assert "dwconv_fwd" in str(e)
     else:
         raise AssertionError("expected EdetError")
+
+
+def test_conv1x1_fwd_rejects_accumulate_with_lazy_a():
+    """the lazy K-loop instances overwrite C, so an accumulating forward with a BN /
+    swish / gated A is refused before any launch (EDET_EINVAL) instead of silently overwriting;
+    a plain A with accumulate passes the check (and fails later, at the null output)."""
+    lib = _lib.lib()
+    lz = _lib.Lazy()
+    lz.x, lz.ld, lz.act = 16, 8, _lib.ACT_SWISH
+    pyr = _lib.Pyramid()
+    pyr.nseg, pyr.batch, pyr.H[0], pyr.W[0] = 1, 1, 4, 4
+    dummy = ctypes.c_void_p(16)
+    rc = lib.fns["edet_conv1x1_fwd"](0, ctypes.byref(lz), ctypes.byref(pyr), 8, dummy, 8, None, dummy, 8, 1,
+                                     None, None)
+    assert rc == -1 and "plain A" in lib.last_error()

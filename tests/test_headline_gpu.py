@@ -5,7 +5,8 @@
   the fp64 oracle: loss within 1e-4, per-tensor gradients within 1e-3, the training-mode
   outputs elementwise;
 * the same model in bf16 storage: forward outputs against the oracle run on bf16-rounded
-  weights and input;
+  weights and input, and one full train step (loss, every per-tensor gradient) against the
+  oracle with bf16 storage emulated in both directions;
 * config 5's model: EfficientDet-D4 at 1024x1024 (deep BiFPN, C up to 2688), B = 1, fp32, one
   train step against the oracle (outputs, loss, gradient norm, per-tensor gradients);
 * the headline workload itself (D0 512x512, B = 32, bf16): five train steps on one batch stay
@@ -20,6 +21,9 @@ Tolerances (stated here, used below):
                 the level's RMS on the box outputs); loss 1e-4; gnorm and every per-tensor
                 gradient 1e-3 (+1e-6 gnorm for analytically-zero gradients)
   D4 fp32       noise floor: at most 3x the fp32 oracle's deviation from the fp64 oracle
+  bf16 step     loss and every per-tensor gradient: deviation from fp64 at most BF16_STEP = 1.5x
+                that of the oracle with bf16 storage emulated forward and backward (+2e-5 of the
+                loss, +1e-6 of the gradient norm)
   bf16          RMS deviation at most 1.5x that of the oracle with bf16 storage rounding;
                 inference mode also max <= BF16_OUT * RMS, BF16_OUT = 0.1, RMS <= 2 %;
                 training mode also max <= BF16_TRAIN_MAX = 3x the emulation's max (+1e-3 max|ref|)
@@ -46,6 +50,7 @@ pytestmark = pytest.mark.gpu
 OUT_FLOOR = 3e-5
 BF16_OUT = 0.1
 BF16_TRAIN_MAX = 3.0
+BF16_STEP = 1.5
 POOL_REROUTE, POOL_GAP = 1e-4, 1e-5            # absolute bars (D0)
 POOL_REROUTE_FLOOR, POOL_GAP_FLOOR = 1e-3, 3e-3  # noise-floor bars (D4)
 REPORT = os.environ.get("EDET_REPORT_DIR")
@@ -168,9 +173,15 @@ class ActCapture:
         return routes
 
 
-def oracle_step(cfg, sd, x, masks, targets, routes, dtype=torch.float64):
-    """Oracle forward (training) with the product's pool routing, loss and every gradient."""
+def oracle_step(cfg, sd, x, masks, targets, routes, dtype=torch.float64, bf16_emulation=False):
+    """Oracle forward (training) with the product's pool routing, loss and every gradient.
+    bf16_emulation: every tensor the product stores is rounded to bf16 on the forward value and
+    on its incoming gradient, and every conv / resample input's gradient (the dv the product's
+    dgrads store) is rounded too -- bf16 storage of the reference semantics in both directions."""
+    from oracle.ref_model import bf16_grad, bf16_store
     ref = RefEfficientDet(cfg, sd, dtype=dtype)
+    if bf16_emulation:
+        ref.store, ref.gstore = bf16_store, bf16_grad
     ref.routes = routes
     keys = [k for k in ref.p if not k.endswith(("/moving_mean", "/moving_variance"))]
     for k in keys:
@@ -286,6 +297,61 @@ def test_d4_1024_train_step_parity_fp32():
     rep = train_parity("efficientdet-d4", 1024, 1, 81, seed=12, with_fp32_floor=True)
     _report("d4_1024_train_fp32", rep)
     check_train_report(rep, floor_mult=3.0)
+
+
+@pytest.mark.timeout(900)
+def test_d0_512_nc81_train_step_bf16_emulated():
+    """The metric's train step in its own dtype (bf16 storage, fp32 arithmetic) at BASELINE
+    config 3's geometry (512x512, 81 classes), B = 2, against two fp64 oracles on the same
+    bf16-rounded weights and input, both following the product's max-pool routes (ActCapture,
+    as the fp32 test): ref = fp64 throughout; emu = ref with bf16 storage emulated in BOTH
+    directions (oracle_step's bf16_emulation).  Bars: the GPU's loss
+    deviation from ref at most BF16_STEP x emu's (+2e-5 of the loss: both deviations are ~1e-4
+    of it), and for every parameter tensor the GPU's gradient deviation from ref at most
+    BF16_STEP x emu's + 1e-6 of the gradient norm.  A bf16-only backward defect that moved a
+    tensor's gradient by more than bf16 storage itself does cannot pass."""
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    S, B, NC, seed = 512, 2, 81, 15
+    cfg = get_efficientdet_config("efficientdet-d0", {"image_size": S, "num_classes": NC})
+    anchors = Anchors(cfg.min_level, cfg.max_level, (S, S), cfg.num_scales, cfg.aspect_ratios, cfg.anchor_scale)
+    m = EfficientDetNetTrain(efficientnet_b0_blocks(), cfg, anchors, dtype="bf16", seed=seed,
+                             lr_schedule={"fixed_lr": 0.01})
+    m.load_state_dict(_bf16_round_sd(perturb(m.state_dict(), seed + 100)))
+    sd0 = m.state_dict()
+    x, boxes, cls, n = synth(B, S, NC, seed)
+    xr = torch.tensor(x).to(torch.bfloat16)
+    x64 = xr.float().numpy()
+    t = anchors.generate_targets_batched(torch.tensor(boxes), torch.tensor(cls), torch.tensor(n))
+    targets = ref_targets(m, t, B, NC)
+    fm = drop_masks(m, B, seed)
+    masks = {"class_net": torch.tensor(fm[0]).cuda(), "box_net": torch.tensor(fm[1]).cuda()}
+    xs = xr.cuda()
+    with ActCapture() as cap:
+        m.call(xs, training=True, masks=masks)
+    routes = cap.pool_routes(m)
+    del cap
+    m.fixed_masks = masks
+    out = m.train_step((xs, t))
+    loss = float(out["loss"])
+    g = m.P.grads_dict()
+    omasks = {"class_net": fm[0], "box_net": fm[1]}
+    _, _, rloss, rg, rgn, rstats = oracle_step(cfg, sd0, x64, omasks, targets, routes)
+    _, _, eloss, eg, egn, _ = oracle_step(cfg, sd0, x64, omasks, targets, routes, bf16_emulation=True)
+    rep = {"loss": loss, "ref_loss": rloss, "emu_loss": eloss, "gnorm": float(out["gnorm"]), "ref_gnorm": rgn,
+           "emu_gnorm": egn, "pool_windows": rstats.get("windows", 0), "pool_rerouted": rstats.get("rerouted", 0),
+           "grads": {}}
+    for k, gr in rg.items():
+        gg = torch.tensor(g[k], dtype=torch.float64)
+        if m.P.specs[k].l2:
+            gg = gg + 4e-5 * torch.tensor(sd0[k], dtype=torch.float64)
+        rep["grads"][k] = {"err": float((gg - gr).norm()), "emu_err": float((eg[k] - gr).norm()),
+                           "norm": float(gr.norm())}
+    ratios = sorted(e["err"] / max(e["emu_err"], 1e-30) for e in rep["grads"].values())
+    rep["err_ratio_median"], rep["err_ratio_max"] = ratios[len(ratios) // 2], ratios[-1]
+    _report("d0_512_nc81_train_bf16_emulated", rep)
+    assert abs(loss - rloss) <= BF16_STEP * abs(eloss - rloss) + 2e-5 * abs(rloss), (loss, rloss, eloss)
+    bad = [(k, e) for k, e in rep["grads"].items() if e["err"] > BF16_STEP * e["emu_err"] + 1e-6 * rgn]
+    assert not bad, (len(bad), bad[:10])
 
 
 def _bf16_round_sd(sd):
@@ -431,3 +497,44 @@ def test_d4_1024_b8_bf16_three_steps():
     assert 0.5 <= gb[0] / gf[0] <= 2.0, (gb[0], gf[0])
     assert all(abs(v - lb[0]) / lb[0] < 0.02 for v in lb), lb
     assert all(10.0 <= v <= 5000.0 for v in gb), gb
+
+
+@pytest.mark.timeout(600)
+def test_b0_224_b64_backbone_bf16_inference():
+    """BASELINE config 2 at its own configuration: the EfficientNet-B0 backbone at 224x224,
+    B = 64, bf16 storage, inference BN (the SE squeeze in the depthwise epilogue,
+    edet_dwconv_fwd_squeeze, and the B = 64 launch plans: stage-0 M = 802,816 rows).  Inference
+    BN makes the images independent, so images 0 and 37 are compared, on every output
+    ([features, reduction_1..5]), with the fp64 oracle and with the oracle emulating bf16
+    storage (its outputs stored in bf16, as the product's are) on the same bf16-rounded weights
+    (perturbed BN statistics) and input.  Bars of test_d0_512_nc81_forward_bf16(False): RMS
+    deviation at most 1.5x the emulation's (+1e-3 RMS), max <= BF16_OUT * RMS, RMS error <= 2 %."""
+    from oracle.ref_model import bf16_store
+    torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
+    S, B = 224, 64
+    cfg = get_efficientdet_config("efficientdet-d0", {"image_size": S})
+    m = EfficientDetNet(efficientnet_b0_blocks(), cfg, dtype="bf16", seed=21)
+    assert m.fused_squeeze
+    m.load_state_dict(_bf16_round_sd(perturb(m.state_dict(), 121)))
+    x = np.random.default_rng(21).random((B, S, S, 3), dtype=np.float32)
+    xr = torch.tensor(x).to(torch.bfloat16)
+    outs = [o.float().cpu() for o in m.backbone(xr.cuda(), training=False)]
+    torch.cuda.synchronize()
+    pick = [0, 37]
+    xs = xr[pick].float().numpy()
+    ref = RefEfficientDet(cfg, m.state_dict())
+    emu = RefEfficientDet(cfg, m.state_dict())
+    emu.store = bf16_store
+    with torch.no_grad():
+        rs = ref.backbone(xs, False)
+        es = [bf16_store(t) for t in emu.backbone(xs, False)]
+    assert [tuple(o.shape) for o in outs] == [(B, 7, 7, 320), (B, 112, 112, 16), (B, 56, 56, 24), (B, 28, 28, 40),
+                                               (B, 14, 14, 112), (B, 7, 7, 320)]
+    rep = []
+    for i, (o, r, f) in enumerate(zip(outs, rs, es)):
+        rep.append((i, out_errors(o[pick], r, f)))
+    _report("b0_224_b64_backbone_bf16_infer", {"outputs": rep})
+    for i, e in rep:
+        assert e["rms_err"] <= 1.5 * e["floor_rms_err"] + 1e-3 * e["rms_ref"], (i, e)
+        assert e["max_abs"] <= BF16_OUT * e["rms_ref"], (i, e)
+        assert e["rms_err"] <= 0.02 * e["rms_ref"], (i, e)

@@ -3,12 +3,10 @@ libedet vs the fp64 CPU oracle (oracle/ref_model.py) on identical parameters and
 
 Reduced size for oracle speed: D0 topology at 128x128, batch 2, 5 classes; drop-connect
 masks injected (the reference draws them randomly).  fp32 storage: outputs within 1e-3
-relative (north_star tolerance).  bf16 storage: measured against the fp32 path's own noise
-floor (the same step on bf16-rounded weights and input; the gradient at initialisation moves
-by cosine ~0.85 under that perturbation alone): gradient deviation within 3x that floor
-+ 0.02, loss within 3x the floor's loss change or 0.2 %, predict-layer cosine > 0.95 (see
-test_train_step_bf16_within_fp32_noise_floor).  The headline geometry (512^2, NC=81) and the
-bf16 forward against a bf16-emulating oracle are in test_headline_gpu.py.
+relative (north_star tolerance).  The bf16 train step is pinned at the headline geometry
+(512^2, NC=81) against the oracle with bf16 storage emulated forward and backward
+(test_headline_gpu.py::test_d0_512_nc81_train_step_bf16_emulated, which replaced round 5's
+cosine-against-a-noise-floor bar here); the bf16 forward likewise in test_headline_gpu.py.
 """
 import numpy as np
 import pytest
@@ -223,53 +221,6 @@ def test_train_step_reference_format_equals_compact():
     for k, sp in m.P.specs.items():
         a, b = g1[sp.offset: sp.offset + sp.size], m.P.g[sp.offset: sp.offset + sp.size]
         assert float((a - b).norm()) <= 1e-3 * float(a.norm()) + 1e-6 * float(g1.norm()), k
-
-
-def _bf16_round(a):
-    return torch.tensor(np.asarray(a, np.float32)).to(torch.bfloat16).float().numpy()
-
-
-def test_train_step_bf16_within_fp32_noise_floor():
-    """bf16 storage vs the fp32 path (itself pinned to the fp64 oracle by
-    test_train_step_parity_fp32).  The EfficientDet gradient at initialisation is chaotic: the
-    fp32 path run on bf16-ROUNDED weights and input -- the smallest perturbation bf16 storage
-    implies (2^-9 relative) -- already moves the gradient (cosine ~0.85, median per-tensor
-    change ~50 %, tools/dev/debug_bf16b.py).  That run defines the noise floor; the
-    bf16 step must stay within a small multiple of it, its loss within 3x the floor's loss
-    change (or 0.2 %), and the loss-adjacent predict-layer gradients likewise (and cosine > 0.95)."""
-    x, boxes, cls, n = synth(5)
-
-    def run(dtype, sd=None, xin=x):
-        m, anchors = _train_model(dtype)  # same seed: identical fp32 master weights
-        if sd is not None:
-            m.load_state_dict(sd)
-        t, *_ = make_targets(m, anchors, boxes, cls, n)
-        fm = fixed_masks(m)
-        m.fixed_masks = {"class_net": torch.tensor(fm[0]).cuda(), "box_net": torch.tensor(fm[1]).cuda()}
-        m.forward_backward((torch.tensor(xin).cuda(), t))
-        torch.cuda.synchronize()
-        return float(m.scalars[0]), m.P.grads_dict(), m
-
-    l32, g32, m32 = run("f32")
-    sd = m32.state_dict()
-    sdr = {k: (_bf16_round(v) if not (k.endswith("moving_mean") or k.endswith("moving_variance")) else v)
-           for k, v in sd.items()}
-    l32r, g32r, _ = run("f32", sdr, _bf16_round(x))
-    l16, g16, _ = run("bf16")
-    keys = list(g32)
-
-    def cos(ga, gb, ks):
-        a = np.concatenate([ga[k].ravel() for k in ks]).astype(np.float64)
-        b = np.concatenate([gb[k].ravel() for k in ks]).astype(np.float64)
-        return float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
-
-    floor = 1.0 - cos(g32r, g32, keys)
-    dev = 1.0 - cos(g16, g32, keys)
-    assert dev <= 3.0 * floor + 0.02, (dev, floor)
-    assert abs(l16 - l32) / l32 <= max(3.0 * abs(l32r - l32) / l32, 2e-3), (l16, l32, l32r)
-    pred = [k for k in keys if "predict/pointwise_kernel" in k or "predict/bias" in k]
-    c16, c32r = cos(g16, g32, pred), cos(g32r, g32, pred)
-    assert c16 > 0.95 and 1.0 - c16 <= 3.0 * (1.0 - c32r) + 0.01, (c16, c32r)
 
 
 def test_training_reduces_loss_bf16():
