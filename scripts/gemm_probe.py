@@ -78,6 +78,9 @@ def main():
         if (not only or only == "fwd bn"):
             res["fwd bn"] = timeit(lambda: L.call("edet_conv1x1_fwd", L.BF16, lz_b.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, so, s))
             kern["fwd bn"] = KERN["last"]
+        if (not only or only == "fwd bn -stats"):
+            res["fwd bn -stats"] = timeit(lambda: L.call("edet_conv1x1_fwd", L.BF16, lz_b.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, None, s))
+            kern["fwd bn -stats"] = KERN["last"]
         if (not only or only == "fwd bn+sw"):
             res["fwd bn+sw"] = timeit(lambda: L.call("edet_conv1x1_fwd", L.BF16, lz_bs.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, so, s))
             kern["fwd bn+sw"] = KERN["last"]

