@@ -415,6 +415,19 @@ def pmc_mfma(kernel, calls_per_step=None):
     return None if k is None else float(k["mfma_busy_frac"])
 
 
+def pmc_limiter(kernel, calls_per_step=None, hbm_frac=None):
+    """What bounds ``kernel`` (profiles/pmc_limiter.json, two PMC passes of wave-time breakdown,
+    instruction mix, LDS conflicts and L2 hits; scripts/pmc_limiter.py): (limiter line, the
+    counter-derived fractions behind it), or (None, None)."""
+    k = _pmc_entry("pmc_limiter.json", kernel, calls_per_step)
+    if k is None:
+        return None, None
+    from scripts.pmc_limiter import limiter_from
+    keep = ("waves_per_simd", "wait_frac", "issue_stall_frac", "active_valu_frac", "active_lds_frac",
+            "active_vmem_frac", "lds_conflict_rate", "l2_hit")
+    return limiter_from(k, hbm_frac), {n: round(float(k[n]), 3) for n in keep if n in k}
+
+
 def _cpu_share():
     """Host cores this process may use: the affinity set, capped by a cgroup CPU quota."""
     n = len(os.sched_getaffinity(0))
@@ -533,6 +546,7 @@ def kernel_tables(step_fn, args, el):
         gbs = a[2] / (a[1] * 1e6) if a[3] and a[1] > 0 else None
         tr = pmc_traffic(k, a[0])
         mf = pmc_mfma(k, a[0])
+        lim, lim_pmc = pmc_limiter(k, a[0], None if gbs is None else gbs / HBM_PEAK_GBS)
         table.append({"kernel": k, "calls": a[0], "ms": round(a[1], 4), "share": round(a[1] / total_ms, 4),
                       "avg_us": round(a[1] * 1e3 / a[0], 2),
                       "bytes_per_launch": round(a[2] / a[0]) if a[3] else None,
@@ -540,6 +554,7 @@ def kernel_tables(step_fn, args, el):
                       "frac": None if gbs is None else round(gbs / HBM_PEAK_GBS, 4),
                       "pmc_traffic_ratio": (round(tr / (a[2] / a[0]), 3) if (tr and a[3] and a[2]) else None),
                       "mfma_frac": None if mf is None else round(mf, 4),
+                      "limiter": lim, "limiter_pmc": lim_pmc,
                       "entry_points": sorted(a[4])})
     known = sum(a[2] for a in kag.values() if a[3])
     step_level = {"algorithmic_bytes": round(known), "ms_per_step": round(el / args.steps * 1e3, 3),

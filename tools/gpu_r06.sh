@@ -29,6 +29,18 @@ for step in ${STEPS:-}; do
     kbench)
       timeout -k 10 400 python scripts/kbench.py --top 400 ${KB_ARGS:-} --out $O/${TAG}_kbench.txt > $O/kbench.log 2>&1
       rc=$?; head -32 $O/${TAG}_kbench.txt 2>/dev/null; tail -3 $O/kbench.log; [ $rc -eq 0 ] || exit $rc ;;
+    limiter)
+      EAGER="python bench.py --steps 3 --warmup 1 --graph 0 --cpu-baseline 0 --kernel-timing 0"
+      rm -rf $O/pmc_lima $O/pmc_limb
+      timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+          SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_lima -o run \
+          --output-format csv -- $EAGER > $O/pmc_lima.log 2>&1 &&
+      timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT \
+          SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_limb -o run \
+          --output-format csv -- $EAGER > $O/pmc_limb.log 2>&1 &&
+      python scripts/pmc_limiter.py --a $O/pmc_lima --b $O/pmc_limb --steps 6 --tag $TAG --out $O/pmc_limiter.json \
+          > $O/${TAG}_pmc_limiter.txt
+      rc=$?; find $O -name "*.db" -delete 2>/dev/null; head -40 $O/${TAG}_pmc_limiter.txt; [ $rc -eq 0 ] || { tail -5 $O/pmc_lima.log $O/pmc_limb.log; exit $rc; } ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
