@@ -55,6 +55,19 @@ enum { EDET_OK = 0, EDET_EINVAL = -1, EDET_EUNSUPPORTED = -2, EDET_EHIP = -3 };
 
 #define EDET_MAX_SEG 5
 
+/* Statistics vectors (ABI 9): the fp64 per-channel BN statistics (edet_bn.sum / .sq,
+ * edet_statout) and BN-backward sums (edet_bngrad64) are stored REPLICATED: channel c of
+ * replica r (r < EDET_STAT_REPLICAS) lives at element
+ *     (c / 16) * 16 * EDET_STAT_REPLICAS + r * 16 + c % 16
+ * and its value is the sum of its replicas (r = 0, 1, 2, 3, in that order, paired (0+1)+(2+3)).
+ * A vector of C channels therefore takes ceil(C / 16) * 16 * EDET_STAT_REPLICAS doubles
+ * (EDET_STAT_LEN(C)); producers add each block's sums into one replica, so an address sees a
+ * quarter of the adders (contended fp64 atomics cost the D0 step ~0.3 ms).  Accumulators are
+ * caller-zeroed as before; a caller that writes a value itself puts it in replica 0 and zeroes
+ * the others. */
+#define EDET_STAT_REPLICAS 4
+#define EDET_STAT_LEN(C) ((((C) + 15) / 16) * 16 * EDET_STAT_REPLICAS)
+
 /* Row layout of a (possibly multi-level) NHWC activation buffer.  Segment s holds
  * batch*H[s]*W[s] rows starting at row_off[s] (a multiple of 128).  A plain tensor
  * is one segment at offset 0.  The feature pyramid P3..P7 is five segments. */

@@ -15,7 +15,7 @@ import torch  # noqa: E402
 
 from tf2mv_amd import _lib as L  # noqa: E402
 from tf2mv_amd.runtime import Pyr, stream, vp  # noqa: E402
-from gpu_util import LazyDesc, make_bn, stat_out, zeros64  # noqa: E402
+from gpu_util import LazyDesc, make_bn, stat_out, stats_out, zeros64  # noqa: E402
 
 
 def timeit(fn, reps):
@@ -43,7 +43,7 @@ def main():
     dy = torch.randn(pout.rows, C, device="cuda").to(torch.bfloat16)
     dx = torch.empty(pin.rows, C, device="cuda", dtype=torch.bfloat16)
     dw = torch.zeros(k * k, C, device="cuda")
-    so = stat_out([(zeros64(C), zeros64(C))])
+    so = stat_out(stats_out(1, C))
     s = stream()
     es = 2
     byt = (pin.rows + pout.rows) * C * es

@@ -13,7 +13,7 @@ import torch  # noqa: E402
 
 from tf2mv_amd import _lib as L  # noqa: E402
 from tf2mv_amd.runtime import Pyr, stream, vp  # noqa: E402
-from gpu_util import LazyDesc, make_bn, stat_out, zeros64  # noqa: E402
+from gpu_util import LazyDesc, make_bn, stat_out, stats_out, zeros64  # noqa: E402
 
 SHAPES = [(32, 256, 256, 32, 3, 1), (32, 256, 256, 96, 3, 2), (32, 128, 128, 144, 3, 1), (32, 128, 128, 144, 5, 2),
           (32, 64, 64, 240, 5, 1), (32, 64, 64, 240, 3, 2), (32, 32, 32, 480, 3, 1), (32, 32, 32, 480, 5, 1),
@@ -48,7 +48,7 @@ def main():
         dy = torch.randn(pout.rows, C, device="cuda").to(torch.bfloat16)
         dx = torch.empty(pin.rows, C, device="cuda", dtype=torch.bfloat16)
         dw = torch.zeros(k * k, C, device="cuda")
-        so = stat_out([(zeros64(C), zeros64(C)) for _ in range(pin.nseg)])
+        so = stat_out(stats_out(pin.nseg, C))
         if which == "fwd":
             f = lambda: L.call("edet_dwconv_fwd", L.BF16, lz.c, pin.c, C, k, st, vp(w), vp(y), pout.c, so, s)
         elif which == "dgrad":

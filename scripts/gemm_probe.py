@@ -17,7 +17,7 @@ import torch  # noqa: E402
 
 from tf2mv_amd import _lib as L  # noqa: E402
 from tf2mv_amd.runtime import Pyr, ensure_workspace, stream, vp  # noqa: E402
-from gpu_util import LazyDesc, make_bn, stat_out, zeros64  # noqa: E402
+from gpu_util import LazyDesc, make_bn, stat_out, stats_out, zeros64  # noqa: E402
 
 
 KERN = {}
@@ -63,7 +63,7 @@ def main():
         lz_b = LazyDesc(x, pyr, K, bn=bn, act=0)
         lz_bs = LazyDesc(x, pyr, K, bn=bn, act=1)
         lz_bsg = LazyDesc(x, pyr, K, bn=bn, act=1, gate=gate)
-        st = [(zeros64(N), zeros64(N))]
+        st = stats_out(1, N)
         so = stat_out(st)
         s = stream()
         es = 2

@@ -15,9 +15,42 @@ import torch  # noqa: F401
 from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
 
 MAX_SEG = 5
-ABI_VERSION = 8  # must equal edet_abi_version() of the loaded library (struct layouts)
+ABI_VERSION = 9  # must equal edet_abi_version() of the loaded library (struct layouts)
 OPT_NORM_BLOCKS = 256  # EDET_OPT_NORM_BLOCKS: edet_opt_norm partial-sum slots per quantity
 F32, BF16 = 0, 1
+# replicated statistics vectors (include/edet.h, ABI 9): channel c of replica r at stat_idx(c, r)
+STAT_REPLICAS = 4
+
+
+def stat_len(C: int) -> int:
+    """doubles of a replicated statistics vector of C channels (EDET_STAT_LEN)"""
+    return (C + 15) // 16 * 16 * STAT_REPLICAS
+
+
+def stat_idx(c, r=0):
+    return (c // 16) * 16 * STAT_REPLICAS + r * 16 + c % 16
+
+
+def stat_fold(t, C: int):
+    """The values of a replicated statistics vector (last dimension stat_len(C)): replicas summed
+    in the library's order, (r0 + r1) + (r2 + r3); a tensor of the leading shape x C."""
+    lead = t.shape[:-1]
+    v = t.reshape(*lead, -1, STAT_REPLICAS, 16)
+    s = (v[..., 0, :] + v[..., 1, :]) + (v[..., 2, :] + v[..., 3, :])
+    return s.reshape(*lead, -1)[..., :C]
+
+
+def stat_unfold(v):
+    """A replicated statistics vector holding the values v (last dimension C) in replica 0."""
+    import torch as _t
+    C = v.shape[-1]
+    lead = v.shape[:-1]
+    out = _t.zeros(*lead, stat_len(C), dtype=v.dtype, device=v.device)
+    o = out.view(*lead, -1, STAT_REPLICAS, 16)
+    pad = _t.zeros(*lead, (C + 15) // 16 * 16, dtype=v.dtype, device=v.device)
+    pad[..., :C] = v
+    o[..., 0, :] = pad.view(*lead, -1, 16)
+    return out
 ACT_NONE, ACT_SWISH = 0, 1
 MODE_SAME, MODE_UPSAMPLE, MODE_MAXPOOL = 0, 1, 2
 
@@ -167,7 +200,9 @@ class _Lib:
             fn.restype = _RESTYPE.get(name, c_int)
             self.fns[name] = fn
         abi = self.fns["edet_abi_version"]()
-        if abi != ABI_VERSION:
+        # same-box timing A/B only: an ABI 8 build (plain statistics vectors) runs in the larger
+        # replicated buffers of ABI 9 without leaving them; its values are not the model's
+        if abi != ABI_VERSION and not (allow_missing and abi == 8):
             raise ImportError(f"{path} implements C-ABI version {abi}, this binding expects {ABI_VERSION}: "
                               f"rebuild it with `make -C tensorflow2-machine-vision_amd`")
         # development builds only (EDET_LIB=.../libedet_dev.so): plan slots for whole-step A/B runs,

@@ -67,52 +67,43 @@ struct LArgs {
   int cslices;  // k_gate_bn_reduce: channel slices of geo.TPR * 8 channels (1 = whole rows)
 };
 
-// per-channel tables in dynamic LDS: af (sc, sh), mr (mean, rstd), gb (dgamma/M, dbeta/M).
-// A thread builds channels tid, tid + blockDim, ... : TU = 2 of them with every statistic
-// load issued before any is used (the plain loop waited for each channel's fp64 loads in turn:
-// C / blockDim dependent L2 round trips per block, 8 for the 1152-channel rows; TU = 4 cost
-// the light apply instances 1-2 waves per SIMD)
-__device__ __forceinline__ void load_tables(const edet_lazy& lz, int seg, float inv, int C, float2* af, float2* mr,
-                                            float2* gb, const edet_bngrad64* acc) {
-  constexpr int TU = 2;
+// per-channel tables in dynamic LDS: af (sc, sh), mr (mean, rstd), gb (dgamma/M, dbeta/M), for
+// channels [c_lo, c_hi) (a block's channel slice) at their channel index.  One channel per
+// thread and trip, its replicas' loads (common.hpp stat_idx: 4 statistics vectors x 4
+// replicas) all issued before any is used -- 32 VGPRs in flight; the two-channel form of round
+// 5 held twice that once the statistics were replicated and cost the apply kernels 1-3 waves
+// per SIMD (r06k: 80-114 -> 138 VGPRs).
+__device__ __forceinline__ void load_tables(const edet_lazy& lz, int seg, float inv, int c_lo, int c_hi, float2* af,
+                                            float2* mr, float2* gb, const edet_bngrad64* acc) {
   const bool bn = lz.bn.enabled;
-  for (int c0 = threadIdx.x; c0 < C; c0 += TU * blockDim.x) {
-    double su[TU], sq[TU], dg[TU], db[TU];
-    float ga[TU], be[TU];
+  for (int c = c_lo + threadIdx.x; c < c_hi; c += blockDim.x) {
+    float2 a = make_float2(1.f, 0.f), b = make_float2(0.f, 1.f), d = make_float2(0.f, 0.f);
+    if (bn) {  // bn_affine / bn_mean_rstd (common.hpp), the same arithmetic
+      double su[SR], sq[SR], dg[SR], db[SR];
+      const int i = stat_idx(c, 0);
 #pragma unroll
-    for (int u = 0; u < TU; ++u) {
-      const int c = min(c0 + u * (int)blockDim.x, C - 1);  // clamped: loads are unconditional
-      su[u] = sq[u] = dg[u] = db[u] = 0.0;
-      ga[u] = 1.f;
-      be[u] = 0.f;
-      if (bn) {
-        su[u] = lz.bn.sum[seg][c];
-        sq[u] = lz.bn.sq[seg][c];
-        ga[u] = lz.bn.gamma[seg][c];
-        be[u] = lz.bn.beta[seg][c];
+      for (int r = 0; r < SR; ++r) {
+        su[r] = lz.bn.sum[seg][i + 16 * r];
+        sq[r] = lz.bn.sq[seg][i + 16 * r];
         if (gb) {
-          dg[u] = acc->dgamma[seg][c];
-          db[u] = acc->dbeta[seg][c];
+          dg[r] = acc->dgamma[seg][i + 16 * r];
+          db[r] = acc->dbeta[seg][i + 16 * r];
         }
       }
+      const float ga = lz.bn.gamma[seg][c], be = lz.bn.beta[seg][c];
+      const double mean = ((su[0] + su[1]) + (su[2] + su[3])) * (double)inv;
+      const double var = fmax(((sq[0] + sq[1]) + (sq[2] + sq[3])) * (double)inv - mean * mean, 0.0);
+      const float r = rsqrtf((float)var + lz.bn.eps);
+      const float sc = ga * r;
+      a = make_float2(sc, be - (float)mean * sc);
+      b = make_float2((float)mean, r);
+      if (gb)
+        d = make_float2((float)(((dg[0] + dg[1]) + (dg[2] + dg[3])) * (double)inv),
+                        (float)(((db[0] + db[1]) + (db[2] + db[3])) * (double)inv));
     }
-#pragma unroll
-    for (int u = 0; u < TU; ++u) {
-      const int c = c0 + u * (int)blockDim.x;
-      if (c >= C) break;
-      float2 a = make_float2(1.f, 0.f), b = make_float2(0.f, 1.f);
-      if (bn) {  // bn_affine / bn_mean_rstd (common.hpp), the same arithmetic
-        const double mean = su[u] * (double)inv;
-        const double var = fmax(sq[u] * (double)inv - mean * mean, 0.0);
-        const float r = rsqrtf((float)var + lz.bn.eps);
-        const float sc = ga[u] * r;
-        a = make_float2(sc, be[u] - (float)mean * sc);
-        b = make_float2((float)mean, r);
-      }
-      af[c] = a;
-      if (mr) mr[c] = b;
-      if (gb) gb[c] = bn ? make_float2((float)(dg[u] * (double)inv), (float)(db[u] * (double)inv)) : make_float2(0.f, 0.f);
-    }
+    af[c] = a;
+    if (mr) mr[c] = b;
+    if (gb) gb[c] = d;
   }
 }
 
@@ -143,8 +134,8 @@ __device__ __forceinline__ void flush_reduce(const LArgs& g, const RowGeom& geo,
   for (int c = tid; c < C; c += blockDim.x) {
     float ss = 0.f, qq = 0.f;
     for (int i = 0; i < geo.R; ++i) { ss += red[i * C + c]; qq += red[(geo.R + i) * C + c]; }
-    stat_add(g.acc.dbeta[seg] + c, (double)ss);
-    stat_add(g.acc.dgamma[seg] + c, (double)qq);
+    stat_put(g.acc.dbeta[seg], c, (double)ss);
+    stat_put(g.acc.dgamma[seg], c, (double)qq);
   }
   __syncthreads();
 }
@@ -198,7 +189,7 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_reduce(LArgs g, int nchunks) {
     const int rows = seg_rows(g.p, seg);
     if (seg != cur_seg) {
       if (cur_seg >= 0) flush_reduce<T>(g, geo, cur_seg, rr, tv, red, s, q);
-      load_tables(g.lz, seg, 1.f / (float)rows, C, af, mr, nullptr, nullptr);
+      load_tables(g.lz, seg, 1.f / (float)rows, 0, C, af, mr, nullptr, nullptr);
       cur_seg = seg;
       __syncthreads();
     }
@@ -269,21 +260,28 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g, int nchunks) {
   const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
   const int NV = C / 8;
   T* DX = (T*)g.dx;
-  int cur_seg = -1;
-  for (int b = blockIdx.x; b < nchunks; b += gridDim.x) {
+  // channel slices (g.cslices > 1, the wide short tensors): work item b = (chunk, slice); a
+  // block builds the tables of its slice only (all C of them per 8-row chunk cost more than the
+  // chunk's rows once the statistics were replicated)
+  const int ns = g.cslices, CSW = ns > 1 ? geo.TPR * 8 : C;
+  int cur_seg = -1, cur_cs = -1;
+  for (int b = blockIdx.x; b < nchunks * ns; b += gridDim.x) {
+    const int cs = b % ns;
     int seg, chunk;
-    chunk_lookup(g.p, geo.CH, b, seg, chunk);
+    chunk_lookup(g.p, geo.CH, b / ns, seg, chunk);
     const int rows = seg_rows(g.p, seg);
-    if (seg != cur_seg) {
-      if (cur_seg >= 0) __syncthreads();  // the previous segment's tables are still being read
-      load_tables(g.lz, seg, 1.f / (float)rows, C, af, mr, gb, &g.acc);
+    const int c_lo = cs * CSW, c_hi = min(C, c_lo + CSW);
+    if (seg != cur_seg || cs != cur_cs) {
+      if (cur_seg >= 0) __syncthreads();  // the previous tables are still being read
+      load_tables(g.lz, seg, 1.f / (float)rows, c_lo, c_hi, af, mr, gb, &g.acc);
       cur_seg = seg;
+      cur_cs = cs;
       __syncthreads();
     }
-    if (g.has_grads && chunk == 0)  // one writer per segment: fp32 parameter gradients
-      for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        g.grads.a[seg][c] += (float)g.acc.dgamma[seg][c];
-        g.grads.b[seg][c] += (float)g.acc.dbeta[seg][c];
+    if (g.has_grads && chunk == 0)  // one writer per segment and channel: fp32 parameter gradients
+      for (int c = c_lo + threadIdx.x; c < c_hi; c += blockDim.x) {
+        g.grads.a[seg][c] += (float)stat_get(g.acc.dgamma[seg], c);
+        g.grads.b[seg][c] += (float)stat_get(g.acc.dbeta[seg], c);
       }
     if (rr >= geo.R) continue;
     const int off = g.p.row_off[seg];
@@ -292,7 +290,7 @@ __global__ __launch_bounds__(256) void k_lazy_bwd_apply(LArgs g, int nchunks) {
     const float* dvsp = g.dv_scale ? g.dv_scale + seg * g.p.batch : nullptr;
 #pragma unroll
     for (int v = 0; v < RVPT; ++v) {
-      const int cv = tv + v * geo.TPR;
+      const int cv = c_lo / 8 + tv + v * geo.TPR;
       if (!(v < geo.VPT && cv < NV)) continue;
       const int c = cv * 8;
       float sc[8], sh[8], kb[8], kc[8];
@@ -359,7 +357,7 @@ __global__ __launch_bounds__(256) void k_img_reduce(LArgs g) {
   const int cs = blockIdx.x % g.cslices, bi = blockIdx.x / g.cslices;
   const int n = bi / g.chunks_per_img, chunk = bi - n * g.chunks_per_img;
   const int cvb = cs * geo.TPR;
-  load_tables(g.lz, 0, 1.f / (float)seg_rows(g.p, 0), C, af, nullptr, nullptr, nullptr);
+  load_tables(g.lz, 0, 1.f / (float)seg_rows(g.p, 0), cvb * 8, min(C, cvb * 8 + CSW), af, nullptr, nullptr, nullptr);
   __syncthreads();
   const int m_begin = n * g.hw + chunk * geo.CH, m_end = min((n + 1) * g.hw, m_begin + geo.CH);
   const int NV = C / 8;
@@ -438,7 +436,7 @@ __global__ __launch_bounds__(256) void k_gate_bn_reduce(LArgs g) {
   const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
   const int cs = blockIdx.x % g.cslices, bi = blockIdx.x / g.cslices;
   const int n = bi / g.chunks_per_img, chunk = bi - n * g.chunks_per_img;
-  load_tables(g.lz, 0, 1.f / (float)seg_rows(g.p, 0), C, af, mr, nullptr, nullptr);
+  load_tables(g.lz, 0, 1.f / (float)seg_rows(g.p, 0), cs * CSW, min(C, cs * CSW + CSW), af, mr, nullptr, nullptr);
   __syncthreads();
   const int m_begin = n * g.hw + chunk * geo.CH, m_end = min((n + 1) * g.hw, m_begin + geo.CH);
   const int c0 = cs * CSW, c = c0 + tv * 8;
@@ -534,9 +532,9 @@ __device__ __forceinline__ void se_bn_combine_body(int B, int C, int blk, const 
     gb += __shfl_xor(gb, o, 64);
     gg += __shfl_xor(gg, o, 64);
   }
-  if (c < C && ln == 0) {
-    dbeta[c] += gb;
-    dgamma[c] += gg;
+  if (c < C && ln == 0) {  // the channel's one writer: replica 0
+    dbeta[stat_idx(c, 0)] += gb;
+    dgamma[stat_idx(c, 0)] += gg;
   }
 }
 
@@ -718,8 +716,8 @@ __global__ __launch_bounds__(256) void k_residual(LArgs g) {
   chunk_lookup(g.p, geo.CH, blockIdx.x, seg, chunk);
   const int rows = seg_rows(g.p, seg);
   const float inv = 1.f / (float)rows;
-  load_tables(g.lz, seg, inv, C, ax, nullptr, nullptr, nullptr);
-  load_tables(g.res, seg, inv, C, ar, nullptr, nullptr, nullptr);
+  load_tables(g.lz, seg, inv, 0, C, ax, nullptr, nullptr, nullptr);
+  load_tables(g.res, seg, inv, 0, C, ar, nullptr, nullptr, nullptr);
   __syncthreads();
   if (rr >= geo.R) return;
   const int off = g.p.row_off[seg];
@@ -757,10 +755,13 @@ __global__ __launch_bounds__(256) void k_materialize(LArgs g) {
   float2* ax = reinterpret_cast<float2*>(smem);
   const RowGeom geo = g.geo;
   const int tid = threadIdx.x, rr = tid / geo.TPR, tv = tid - rr * geo.TPR;
+  // channel slices (as the apply): block = (chunk, slice), tables of the slice only
+  const int ns = g.cslices, CSW = ns > 1 ? geo.TPR * 8 : C, cs = blockIdx.x % ns;
   int seg, chunk;
-  chunk_lookup(g.p, geo.CH, blockIdx.x, seg, chunk);
+  chunk_lookup(g.p, geo.CH, blockIdx.x / ns, seg, chunk);
   const int rows = seg_rows(g.p, seg);
-  load_tables(g.lz, seg, 1.f / (float)rows, C, ax, nullptr, nullptr, nullptr);
+  const int c_lo = cs * CSW;
+  load_tables(g.lz, seg, 1.f / (float)rows, c_lo, min(C, c_lo + CSW), ax, nullptr, nullptr, nullptr);
   __syncthreads();
   if (rr >= geo.R) return;
   const int off = g.p.row_off[seg];
@@ -770,7 +771,7 @@ __global__ __launch_bounds__(256) void k_materialize(LArgs g) {
   T* OUT = (T*)g.dx;
 #pragma unroll
   for (int v = 0; v < RVPT; ++v) {
-    const int cv = tv + v * geo.TPR;
+    const int cv = c_lo / 8 + tv + v * geo.TPR;
     if (!(v < geo.VPT && cv < NV)) continue;
     const int c = cv * 8;
     float2 a8[8];  // the 8 channels' affine in registers
@@ -810,8 +811,8 @@ __global__ void k_bn_update(int64_t n, const double* sum, const double* sq, cons
   if (i >= n) return;
   if (skip && *skip != 0.f) return;
   const double cnt = count[i];
-  const double mean = sum[i] / cnt;
-  const double var = fmax(sq[i] / cnt - mean * mean, 0.0);
+  const double mean = stat_get(sum, (int)i) / cnt;
+  const double var = fmax(stat_get(sq, (int)i) / cnt - mean * mean, 0.0);
   const float unb = (float)(var * cnt / fmax(cnt - 1.0, 1.0));
   mmean[i] -= (mmean[i] - (float)mean) * (1.f - momentum);
   mvar[i] -= (mvar[i] - unb) * (1.f - momentum);
@@ -822,8 +823,8 @@ __global__ void k_bn_infer_stats(int64_t n, const float* mm, const float* mv, co
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double c = count[i], m = mm[i];
-  sum[i] = m * c;
-  sq[i] = ((double)mv[i] + m * m) * c;
+  sum[stat_idx((int)i, 0)] = m * c;  // replica 0; the other three stay zero
+  sq[stat_idx((int)i, 0)] = ((double)mv[i] + m * m) * c;
 }
 
 static int lazy_checks(const edet_lazy* x, const edet_pyramid* p, int C) {
@@ -919,13 +920,23 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
   else if (C >= 672 && M >= 32768) passes = 16;
   else if (C >= 480 && C <= 672 && M <= 8192) passes = 4;  // not D4's 8192 x 960 (15.3 vs 17.6 us)
   g.geo = row_geom(C, dev_knob(8) > 0 ? dev_knob(8) : passes);
+  g.cslices = 1;
+  // wide rows over few of them (C >= 1024, M <= 16384: the 16^2 stage): 64-channel slices, 32 rows
+  // per pass, 4 passes per chunk (development slot 55: 1 = always from C >= 256, 2 = never;
+  // slot 56: passes)
+  const bool sliced = dev_knob(55) == 1 ? C >= 256 : (dev_knob(55) != 2 && C >= 1024 && M <= 16384);
+  if (sliced) {
+    g.geo.TPR = 8; g.geo.R = 32; g.geo.VPT = 1;
+    g.geo.CH = 32 * (dev_knob(56) > 0 ? dev_knob(56) : 4);
+    g.cslices = cdiv(C / 8, 8);
+  }
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 3 * C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {
     // resident blocks per launch: 512 for the long ungated tensors (M >= 524288, C >= 96: 2M x 96
     // 235.6 -> 222.9 us, 524288 x 144 180.5 -> 176.4, r05i sweep), 2048 elsewhere
     const int gcap = dev_knob(9) > 0 ? dev_knob(9) : ((M >= 524288 && C >= 96 && !x->gate) ? 512 : 2048);
-    const int grid = nb > gcap ? gcap : nb;
+    const int grid = nb * g.cslices > gcap ? gcap : nb * g.cslices;
     const int f = (x->bn.enabled ? AF_BN : 0) | (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0) |
                   (dv_scale ? AF_DVS : 0) | (accumulate ? AF_ACC : 0);
     // nontemporal row loads / stores over >= 524288 rows (2M x 96: 222 -> 215 us, 524288 x 144:
@@ -1089,7 +1100,15 @@ int edet_lazy_materialize(int dtype, const edet_lazy* x, const edet_pyramid* p, 
   const int M = pyr_valid_rows(*p);
   const bool mid = C >= 144 && M >= 32768 && M <= 131072;
   g.geo = row_geom(C, dev_knob(13) > 0 ? dev_knob(13) : (C >= 1024 || mid ? 8 : 4));
-  const int nb = total_chunks(*p, g.geo.CH);
+  g.cslices = 1;
+  // C >= 1024 over M <= 16384: 64-channel slices, 32 rows per pass (as edet_lazy_bwd_apply;
+  // development slot 57: 1 = from C >= 256, 2 = never; slot 58: passes)
+  if (dev_knob(57) == 1 ? C >= 256 : (dev_knob(57) != 2 && C >= 1024 && M <= 16384)) {
+    g.geo.TPR = 8; g.geo.R = 32; g.geo.VPT = 1;
+    g.geo.CH = 32 * (dev_knob(58) > 0 ? dev_knob(58) : 2);
+    g.cslices = cdiv(C / 8, 8);
+  }
+  const int nb = total_chunks(*p, g.geo.CH) * g.cslices;
   const size_t lds = C * sizeof(float2);
   EDET_DTYPE_DISPATCH(dtype, T, {
     const hipStream_t st = (hipStream_t)stream;

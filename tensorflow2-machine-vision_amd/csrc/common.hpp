@@ -129,6 +129,27 @@ __device__ __forceinline__ float dswishf_(float x) {
 // fp64 statistics accumulation (one atomic per channel per block; DESIGN.md "Reproducibility")
 __device__ __forceinline__ void stat_add(double* p, double v) { atomicAdd(p, v); }
 
+// Replicated per-channel statistics (ABI 9; include/edet.h "statistics vectors").  Every block
+// of a producer adds its per-channel sums into the same fp64 vector; the adds to one address
+// serialise at the memory-side atomic unit (~20 ns each: 256 adders cost ~5 us per launch, the
+// D0 step ~0.5 ms; r06e/r06g).  The BN batch statistics and the BN-backward sums are therefore
+// kept in EDET_STAT_REPLICAS = 4 replicas: channel c, replica r at stat_idx(c, r) -- 16
+// channels of one replica per 128-B line, so replicas never share a line -- a block adds into
+// the replica its index hashes to, and readers take the value as the fixed-order sum of the
+// four.  A vector of C channels occupies stat_len(C) doubles.
+constexpr int SR = EDET_STAT_REPLICAS;
+static_assert(SR == 4, "stat_get sums four replicas");
+__host__ __device__ __forceinline__ constexpr long stat_len(int C) { return (long)((C + 15) / 16) * 16 * SR; }
+__host__ __device__ __forceinline__ int stat_idx(int c, int r) { return (c >> 4) * (16 * SR) + r * 16 + (c & 15); }
+__device__ __forceinline__ double stat_get(const double* p, int c) {
+  const double* q = p + stat_idx(c, 0);
+  return (q[0] + q[16]) + (q[32] + q[48]);
+}
+// a block's replica: a multiplicative hash of its index (grids whose blocks of one channel group
+// are a fixed stride apart, e.g. the depthwise channel blocks, still spread over all four)
+__device__ __forceinline__ int stat_rep() { return (int)((blockIdx.x * 2654435761u) >> 30); }
+__device__ __forceinline__ void stat_put(double* p, int c, double v) { atomicAdd(p + stat_idx(c, stat_rep()), v); }
+
 // Sum over the four 16-lane rows of a wave (lane bits 4 and 5), result in every lane: the
 // MFMA epilogues reduce a column's 4 row groups this way.  gfx950's v_permlane16/32_swap are
 // plain VALU ops; the __shfl_xor form was two dependent ds_bpermute round trips per value
@@ -240,16 +261,16 @@ __host__ __device__ __forceinline__ int pyr_total_rows(const edet_pyramid& p) {
 // Per-channel affine of the lazy BN for segment `seg`: v = x * sc + sh.
 __device__ __forceinline__ float2 bn_affine(const edet_bn& bn, int seg, int c, float inv_count) {
   if (!bn.enabled) return make_float2(1.f, 0.f);
-  const double mean = bn.sum[seg][c] * (double)inv_count;
-  const double var = fmax(bn.sq[seg][c] * (double)inv_count - mean * mean, 0.0);
+  const double mean = stat_get(bn.sum[seg], c) * (double)inv_count;
+  const double var = fmax(stat_get(bn.sq[seg], c) * (double)inv_count - mean * mean, 0.0);
   const float r = rsqrtf((float)var + bn.eps);
   const float sc = bn.gamma[seg][c] * r;
   return make_float2(sc, bn.beta[seg][c] - (float)mean * sc);
 }
 // mean / rstd (for x-hat in backward)
 __device__ __forceinline__ float2 bn_mean_rstd(const edet_bn& bn, int seg, int c, float inv_count) {
-  const double mean = bn.sum[seg][c] * (double)inv_count;
-  const double var = fmax(bn.sq[seg][c] * (double)inv_count - mean * mean, 0.0);
+  const double mean = stat_get(bn.sum[seg], c) * (double)inv_count;
+  const double var = fmax(stat_get(bn.sq[seg], c) * (double)inv_count - mean * mean, 0.0);
   return make_float2((float)mean, rsqrtf((float)var + bn.eps));
 }
 

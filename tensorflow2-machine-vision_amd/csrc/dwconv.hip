@@ -187,8 +187,8 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
           float ss = 0.f, qq = 0.f;
 #pragma unroll
           for (int i = 0; i < 8; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
-          stat_add(g.stats.sum[cur_seg] + c0 + tid, (double)(ss));
-          stat_add(g.stats.sq[cur_seg] + c0 + tid, (double)(qq));
+          stat_put(g.stats.sum[cur_seg], c0 + tid, (double)(ss));
+          stat_put(g.stats.sq[cur_seg], c0 + tid, (double)(qq));
         }
       }
       s = 0.f;
@@ -258,8 +258,8 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwArgs g) {
       float ss = 0.f, qq = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
-      stat_add(g.stats.sum[cur_seg] + c0 + tid, (double)(ss));
-      stat_add(g.stats.sq[cur_seg] + c0 + tid, (double)(qq));
+      stat_put(g.stats.sum[cur_seg], c0 + tid, (double)(ss));
+      stat_put(g.stats.sq[cur_seg], c0 + tid, (double)(qq));
     }
   }
 }
@@ -592,8 +592,8 @@ __global__ __launch_bounds__(256) void k_dw3(DwArgs g) {
       float ss = 0.f, qq = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) { ss += red[0][i][tid]; qq += red[1][i][tid]; }
-      stat_add(g.stats.sum[seg] + c0 + tid, (double)ss);
-      stat_add(g.stats.sq[seg] + c0 + tid, (double)qq);
+      stat_put(g.stats.sum[seg], c0 + tid, (double)ss);
+      stat_put(g.stats.sq[seg], c0 + tid, (double)qq);
     }
     s = 0.f;
     q = 0.f;
@@ -783,8 +783,8 @@ __global__ __launch_bounds__(256) void k_dw2_fwd(DwArgs g, DwGeom geo) {
       for (int ch = tid; ch < C; ch += blockDim.x) {
         float ss = 0.f, qq = 0.f;
         for (int i = 0; i < geo.R; ++i) { ss += red2[i * C + ch]; qq += red2[(geo.R + i) * C + ch]; }
-        stat_add(g.stats.sum[seg] + ch, (double)ss);
-        stat_add(g.stats.sq[seg] + ch, (double)qq);
+        stat_put(g.stats.sum[seg], ch, (double)ss);
+        stat_put(g.stats.sq[seg], ch, (double)qq);
       }
       __syncthreads();
     }
@@ -1041,8 +1041,8 @@ __global__ __launch_bounds__(256) void k_dw4_dgrad(DwArgs g, DwGeom geo, edet_bn
       for (int ch = tid; ch < CB; ch += blockDim.x) {
         float a = 0.f, b = 0.f;
         for (int i = 0; i < geo.R; ++i) { a += fsum[i * CB + ch]; b += fsum[(geo.R + i) * CB + ch]; }
-        stat_add(fold.dbeta[seg] + cs * CB + ch, (double)a);
-        stat_add(fold.dgamma[seg] + cs * CB + ch, (double)b);
+        stat_put(fold.dbeta[seg], cs * CB + ch, (double)a);
+        stat_put(fold.dgamma[seg], cs * CB + ch, (double)b);
       }
       __syncthreads();
     }
@@ -1440,8 +1440,8 @@ __global__ __launch_bounds__(256) void k_dws(DwArgs g, DwsPlan pl) {
         float ss = 0.f, qq = 0.f;
 #pragma unroll
         for (int k = 0; k < 8; ++k) { ss += red[k * DCB + tid]; qq += red[(8 + k) * DCB + tid]; }
-        stat_add(g.stats.sum[seg] + c0 + tid, (double)ss);
-        stat_add(g.stats.sq[seg] + c0 + tid, (double)qq);
+        stat_put(g.stats.sum[seg], c0 + tid, (double)ss);
+        stat_put(g.stats.sq[seg], c0 + tid, (double)qq);
       }
     }
     if constexpr (SQ) {  // (after the statistics' reads of the scratch: its own rows 16..23)
@@ -1821,7 +1821,7 @@ __global__ __launch_bounds__(256) void k_dwb(DwArgs g, DwsPlan pl, edet_bngrad64
 #pragma unroll
     for (int k = 0; k < 8; ++k) sum += red[(i * 8 + k) * DCB + cc];
     if (i < K * K) atomicAdd(g.dw + (size_t)i * C + c0 + cc, sum);
-    else if constexpr (FOLD) stat_add((i == K * K ? fold.dbeta[seg] : fold.dgamma[seg]) + c0 + cc, (double)sum);
+    else if constexpr (FOLD) stat_put(i == K * K ? fold.dbeta[seg] : fold.dgamma[seg], c0 + cc, (double)sum);
   }
 }
 
@@ -2058,7 +2058,7 @@ __global__ __launch_bounds__(256) void k_dwb2(DwArgs g, DwsPlan pl, edet_bngrad6
 #pragma unroll
     for (int k = 0; k < 8; ++k) sum += red[(i * 8 + k) * DCB + cc];
     if (i < K * K) atomicAdd(g.dw + (size_t)i * C + c0 + cc, sum);
-    else if constexpr (FOLD) stat_add((i == K * K ? fold.dbeta[seg] : fold.dgamma[seg]) + c0 + cc, (double)sum);
+    else if constexpr (FOLD) stat_put(i == K * K ? fold.dbeta[seg] : fold.dgamma[seg], c0 + cc, (double)sum);
   }
 }
 
@@ -2136,13 +2136,14 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
       float4 t = make_float4(1.f, 0.f, 0.f, 0.f);
       if (d.y.bn.enabled) {
         const float2 a = bn_affine(d.y.bn, seg, cc, inv), q = bn_mean_rstd(d.y.bn, seg, cc, inv);
-        const float dgm = (float)(d.acc.dgamma[seg][cc] * (double)inv), dbm = (float)(d.acc.dbeta[seg][cc] * (double)inv);
+        const float dgm = (float)(stat_get(d.acc.dgamma[seg], cc) * (double)inv),
+                    dbm = (float)(stat_get(d.acc.dbeta[seg], cc) * (double)inv);
         const float kb = -a.x * q.y * dgm;
         t = make_float4(a.x, a.y, kb, -a.x * dbm - kb * q.x);
         // one writer per segment and channel: the first chunk's block
         if (n_gin == 0 && chunk == 0 && d.grads.a[seg]) {
-          d.grads.a[seg][cc] += (float)d.acc.dgamma[seg][cc];
-          d.grads.b[seg][cc] += (float)d.acc.dbeta[seg][cc];
+          d.grads.a[seg][cc] += (float)stat_get(d.acc.dgamma[seg], cc);
+          d.grads.b[seg][cc] += (float)stat_get(d.acc.dbeta[seg], cc);
         }
       }
       gtab[tid] = t;
@@ -2376,7 +2377,7 @@ __global__ __launch_bounds__(256) void k_dwt(DwArgs g, DwtPlan pl, edet_bngrad64
     const float v = (red[(0 * NR + i) * DWT_CB + cc] + red[(1 * NR + i) * DWT_CB + cc]) +
                     (red[(2 * NR + i) * DWT_CB + cc] + red[(3 * NR + i) * DWT_CB + cc]);
     if (i < KK) atomicAdd(g.dw + (size_t)i * C + c0 + cc, v);
-    else if constexpr (FOLD) stat_add((i == KK ? fold.dbeta[seg] : fold.dgamma[seg]) + c0 + cc, (double)v);
+    else if constexpr (FOLD) stat_put(i == KK ? fold.dbeta[seg] : fold.dgamma[seg], c0 + cc, (double)v);
   }
 }
 

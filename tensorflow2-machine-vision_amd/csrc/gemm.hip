@@ -506,8 +506,8 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     for (int i = tid; i < BN; i += 256) {
       const int col = col0 + i;
       if (col < g.N) {
-        stat_add(g.stats.sum[seg] + col, (double)(red[0][0][i] + red[0][1][i]));
-        stat_add(g.stats.sq[seg] + col, (double)(red[1][0][i] + red[1][1][i]));
+        stat_put(g.stats.sum[seg], col, (double)(red[0][0][i] + red[0][1][i]));
+        stat_put(g.stats.sq[seg], col, (double)(red[1][0][i] + red[1][1][i]));
       }
     }
   }
@@ -678,8 +678,8 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
     __syncthreads();
     if (cur_seg >= 0 && g.has_stats)
       for (int c = tid; c < ncols; c += 256) {
-        stat_add(g.stats.sum[cur_seg] + cbase + c, (double)(red[c] + red[LDC + c]));
-        stat_add(g.stats.sq[cur_seg] + cbase + c, (double)(red[2 * LDC + c] + red[3 * LDC + c]));
+        stat_put(g.stats.sum[cur_seg], cbase + c, (double)(red[c] + red[LDC + c]));
+        stat_put(g.stats.sq[cur_seg], cbase + c, (double)(red[2 * LDC + c] + red[3 * LDC + c]));
         red[c] = red[LDC + c] = red[2 * LDC + c] = red[3 * LDC + c] = 0.f;
       }
     if constexpr (LAZY) {
@@ -829,8 +829,8 @@ __global__ __launch_bounds__(256) void k_gemm_r(GemmArgs g, int KP, int nsplit, 
   __syncthreads();
   if (cur_seg >= 0 && g.has_stats)
     for (int c = tid; c < ncols; c += 256) {
-      stat_add(g.stats.sum[cur_seg] + cbase + c, (double)(red[c] + red[LDC + c]));
-      stat_add(g.stats.sq[cur_seg] + cbase + c, (double)(red[2 * LDC + c] + red[3 * LDC + c]));
+      stat_put(g.stats.sum[cur_seg], cbase + c, (double)(red[c] + red[LDC + c]));
+      stat_put(g.stats.sq[cur_seg], cbase + c, (double)(red[2 * LDC + c] + red[3 * LDC + c]));
     }
 }
 
@@ -1615,8 +1615,8 @@ __global__ __launch_bounds__(256) void k_pwb(GemmArgs g, PwPlan p) {
         if (col < N && cl < p.NGtot) {
           float& rs = red[(0 * 2 + wm) * p.NGtot + cl];
           float& rq = red[(1 * 2 + wm) * p.NGtot + cl];
-          stat_add(g.stats.sum[seg] + col, (double)rs);
-          stat_add(g.stats.sq[seg] + col, (double)rq);
+          stat_put(g.stats.sum[seg], col, (double)rs);
+          stat_put(g.stats.sq[seg], col, (double)rq);
           rs = 0.f;
           rq = 0.f;
         }
@@ -2027,8 +2027,8 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
     for (int n = threadIdx.x; n < N; n += 256) {
       const float a = (red[sg][0][0][n] + red[sg][0][1][n]) + (red[sg][0][2][n] + red[sg][0][3][n]);
       const float b = (red[sg][1][0][n] + red[sg][1][1][n]) + (red[sg][1][2][n] + red[sg][1][3][n]);
-      stat_add(g.stats.sum[sg] + n, (double)a);
-      stat_add(g.stats.sq[sg] + n, (double)b);
+      stat_put(g.stats.sum[sg], n, (double)a);
+      stat_put(g.stats.sq[sg], n, (double)b);
     }
 }
 

@@ -65,8 +65,8 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const T* x, int B, int H, int 
   }
   __syncthreads();
   if (tid < Cout) {
-    stat_add(sum + tid, (double)((red[0][0][tid] + red[0][1][tid]) + (red[0][2][tid] + red[0][3][tid])));
-    stat_add(sq + tid, (double)((red[1][0][tid] + red[1][1][tid]) + (red[1][2][tid] + red[1][3][tid])));
+    stat_put(sum, tid, (double)((red[0][0][tid] + red[0][1][tid]) + (red[0][2][tid] + red[0][3][tid])));
+    stat_put(sq, tid, (double)((red[1][0][tid] + red[1][1][tid]) + (red[1][2][tid] + red[1][3][tid])));
   }
 }
 
@@ -240,8 +240,8 @@ __global__ __launch_bounds__(256) void k_stem2_fwd(const uint16_t* x, int B, int
     }
   __syncthreads();
   if (tid < Cout) {
-    stat_add(sum + tid, (double)((red[0][0][tid] + red[0][1][tid]) + (red[0][2][tid] + red[0][3][tid])));
-    stat_add(sq + tid, (double)((red[1][0][tid] + red[1][1][tid]) + (red[1][2][tid] + red[1][3][tid])));
+    stat_put(sum, tid, (double)((red[0][0][tid] + red[0][1][tid]) + (red[0][2][tid] + red[0][3][tid])));
+    stat_put(sq, tid, (double)((red[1][0][tid] + red[1][1][tid]) + (red[1][2][tid] + red[1][3][tid])));
   }
 }
 

@@ -234,10 +234,8 @@ class EfficientDetNet:
         if self._count_batch == B:
             return
         host = np.ones(max(self.P.n_bn, 1), np.float32)
-        o = 0
         for bn in self.P.bns:
-            host[o:o + bn.C] = float(B * bn.hw)
-            o += bn.C
+            host[bn.coff:bn.coff + bn.C] = float(B * bn.hw)
         self.P.bn_count.copy_(torch.from_numpy(host))
         self._count_batch = B
 

@@ -67,7 +67,7 @@ def _value_grad_tables(eng: Engine, out: Act, rec: GradRec):
     if out.bns is not None:
         grads = _bn_grads(out.bns)
         # fp64 dgamma/dbeta sums (edet_bngrad64): their order must not reach the rounding of dx
-        acc_t = rec.bn_sums if folded else eng.zeros64(2, len(out.bns), out.C)
+        acc_t = rec.bn_sums if folded else eng.zeros64(2, len(out.bns), L.stat_len(out.C))
         acc = L.BnGrad64()
         for i in range(len(out.bns)):
             acc.dgamma[i], acc.dbeta[i] = acc_t[0, i].data_ptr(), acc_t[1, i].data_ptr()
@@ -123,7 +123,7 @@ def stem(eng: Engine, P: ParamStore, x: torch.Tensor, wname: str, bn: BNParam) -
     if eng.training:
         L.call("edet_stem_fwd", eng.dt, vp(x), B, H, W, vp(P.wcv(wname)), Cout, vp(y), vp(bn.tsum), vp(bn.tsq), stream())
     else:
-        scratch = eng.zeros64(2, Cout)
+        scratch = eng.zeros64(2, L.stat_len(Cout))
         L.call("edet_stem_fwd", eng.dt, vp(x), B, H, W, vp(P.wcv(wname)), Cout, vp(y), vp(scratch[0]),
                vp(scratch[1]), stream())
     out = Act(y, pyr, Cout, [bn], L.ACT_SWISH, training=eng.training, name="stem")
@@ -248,11 +248,11 @@ def _dgrad_fold_kernel_route(k: int, pin: Pyr) -> bool:
 def _fold_dst(eng: Engine, x: Act, acc: int):
     """BN-backward fold destination for x's gradient when the op writing it owns all of it (x has
     one consumer, nothing accumulated yet) and x's value is BN(+act) without an SE gate: zeroed
-    fp64 [2][nseg][C] sums recorded on x's gradient (value_grad_to_raw then skips its reduce pass)
+    fp64 [2][nseg][stat_len(C)] replicated sums recorded on x's gradient (value_grad_to_raw then skips its reduce pass)
     and their edet_bngrad64 descriptor; else None."""
     if not (acc == 0 and x.uses == 1 and x.bns is not None and x.gate is None and x.se is None):
         return None
-    sums = eng.zeros64(2, len(x.bns), x.C)
+    sums = eng.zeros64(2, len(x.bns), L.stat_len(x.C))  # replicated (include/edet.h)
     fold = L.BnGrad64()
     for i in range(len(x.bns)):
         fold.dgamma[i], fold.dbeta[i] = sums[0, i].data_ptr(), sums[1, i].data_ptr()

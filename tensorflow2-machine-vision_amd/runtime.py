@@ -93,8 +93,9 @@ class BNParam:
         self.name, self.C, self.momentum, self.eps = name, C, momentum, eps
         self.gamma = self.beta = self.dgamma = self.dbeta = None
         self.mmean = self.mvar = self.count = None
-        self.tsum = self.tsq = None    # batch statistics (training)
-        self.isum = self.isq = None    # moving statistics as sums (inference)
+        self.tsum = self.tsq = None    # batch statistics (training), replicated (L.stat_len(C))
+        self.isum = self.isq = None    # moving statistics as sums (inference), replicated
+        self.coff = -1                 # channel offset in the BN arenas (a multiple of 16)
 
     def stats(self, training: bool):
         return (self.tsum, self.tsq) if training else (self.isum, self.isq)
@@ -273,24 +274,29 @@ class ParamStore:
         self.wct = torch.empty(max(toff, 1), dtype=compute_dtype, device=device)
         self.t_table = torch.tensor(np.asarray(table, np.int64).reshape(-1, 4), device=device)
         self.t_entries, self.t_max_tiles = len(table), max_tiles
-        # BN arenas
-        nch = sum(bn.C for bn in self.bns)
-        self.n_bn = nch
-        self.bn_mm = torch.zeros(max(nch, 1), device=device)
-        self.bn_mv = torch.ones(max(nch, 1), device=device)
-        self.bn_count = torch.ones(max(nch, 1), device=device)
-        # fp64 statistics arenas (see edet_bn in include/edet.h)
-        self.bn_tstats = torch.zeros(2, max(nch, 1), dtype=torch.float64, device=device)
-        self.bn_istats = torch.zeros(2, max(nch, 1), dtype=torch.float64, device=device)
+        # BN arenas: every BN's channels start on a multiple of 16, so one channel index space
+        # (padding channels: count 1, statistics 0) serves the per-channel arrays and the
+        # replicated fp64 statistics (include/edet.h "Statistics vectors": channel c of the
+        # arena at L.stat_idx(c, r), each BN's vector a contiguous L.stat_len(C) slice)
         o = 0
         for bn in self.bns:
-            sl = slice(o, o + bn.C)
+            bn.coff = o
+            o += round_up(bn.C, 16)
+        nch = max(o, 16)
+        self.n_bn = nch
+        self.bn_mm = torch.zeros(nch, device=device)
+        self.bn_mv = torch.ones(nch, device=device)
+        self.bn_count = torch.ones(nch, device=device)
+        self.bn_tstats = torch.zeros(2, L.stat_len(nch), dtype=torch.float64, device=device)
+        self.bn_istats = torch.zeros(2, L.stat_len(nch), dtype=torch.float64, device=device)
+        for bn in self.bns:
+            sl = slice(bn.coff, bn.coff + bn.C)
+            ssl = slice(bn.coff * L.STAT_REPLICAS, bn.coff * L.STAT_REPLICAS + L.stat_len(bn.C))
             bn.gamma, bn.beta = self.view(bn.name + "/gamma"), self.view(bn.name + "/beta")
             bn.dgamma, bn.dbeta = self.grad(bn.name + "/gamma"), self.grad(bn.name + "/beta")
             bn.mmean, bn.mvar, bn.count = self.bn_mm[sl], self.bn_mv[sl], self.bn_count[sl]
-            bn.tsum, bn.tsq = self.bn_tstats[0, sl], self.bn_tstats[1, sl]
-            bn.isum, bn.isq = self.bn_istats[0, sl], self.bn_istats[1, sl]
-            o += bn.C
+            bn.tsum, bn.tsq = self.bn_tstats[0, ssl], self.bn_tstats[1, ssl]
+            bn.isum, bn.isq = self.bn_istats[0, ssl], self.bn_istats[1, ssl]
         self.finalized = True
         if torch.device(device).type == "cuda":
             ensure_workspace(device)
@@ -335,11 +341,9 @@ class ParamStore:
         out = {n: host[self.specs[n].offset: self.specs[n].offset + self.specs[n].size].reshape(self.specs[n].shape).copy()
                for n in self.order}
         mm, mv = self.bn_mm.cpu().numpy(), self.bn_mv.cpu().numpy()
-        o = 0
         for bn in self.bns:
-            out[bn.name + "/moving_mean"] = mm[o:o + bn.C].copy()
-            out[bn.name + "/moving_variance"] = mv[o:o + bn.C].copy()
-            o += bn.C
+            out[bn.name + "/moving_mean"] = mm[bn.coff:bn.coff + bn.C].copy()
+            out[bn.name + "/moving_variance"] = mv[bn.coff:bn.coff + bn.C].copy()
         return out
 
     def load_state_dict(self, sd: Dict[str, np.ndarray]):
@@ -352,12 +356,10 @@ class ParamStore:
         self.w.copy_(torch.from_numpy(host))
         self.ema.copy_(self.w)
         mm, mv = self.bn_mm.cpu().numpy(), self.bn_mv.cpu().numpy()
-        o = 0
         for bn in self.bns:
             if bn.name + "/moving_mean" in sd:
-                mm[o:o + bn.C] = sd[bn.name + "/moving_mean"]
-                mv[o:o + bn.C] = sd[bn.name + "/moving_variance"]
-            o += bn.C
+                mm[bn.coff:bn.coff + bn.C] = sd[bn.name + "/moving_mean"]
+                mv[bn.coff:bn.coff + bn.C] = sd[bn.name + "/moving_variance"]
         self.bn_mm.copy_(torch.from_numpy(mm))
         self.bn_mv.copy_(torch.from_numpy(mv))
         self.refresh_compute_copy()

@@ -28,11 +28,14 @@ class LazyDesc:
         lz.x = x.data_ptr()
         lz.gate = gate.data_ptr() if gate is not None else None
         lz.ld, lz.act = self.ld, act
+        self._rep = []  # the replicated statistics vectors the descriptor points at (ABI 9)
         if bn:
             lz.bn.enabled = 1
             lz.bn.eps = eps
             for s, (a, b, c, d) in enumerate(bn):
-                lz.bn.sum[s], lz.bn.sq[s], lz.bn.gamma[s], lz.bn.beta[s] = a.data_ptr(), b.data_ptr(), c.data_ptr(), d.data_ptr()
+                ra, rb = rep64(a), rep64(b)
+                self._rep += [ra, rb]
+                lz.bn.sum[s], lz.bn.sq[s], lz.bn.gamma[s], lz.bn.beta[s] = ra.data_ptr(), rb.data_ptr(), c.data_ptr(), d.data_ptr()
         self.c = lz
 
     def cpu_value(self):
@@ -75,6 +78,62 @@ def zeros64(*shape):
     return torch.zeros(shape, dtype=torch.float64, device=DEV)
 
 
+def rep64(v):
+    """A plain fp64 statistics vector (last dim C) in the library's replicated layout (replica 0)."""
+    v = v if isinstance(v, Folded) else torch.as_tensor(v, dtype=torch.float64, device=DEV)
+    return v.raw if isinstance(v, Folded) else L.stat_unfold(v.to(DEV, torch.float64))
+
+
+class Folded:
+    """A replicated fp64 statistics buffer (include/edet.h "Statistics vectors", ABI 9) that the
+    kernels write; indexing / .v read its values (replicas summed in the library's order)."""
+
+    def __init__(self, lead, C):
+        self.C = C
+        self.raw = torch.zeros(*lead, L.stat_len(C), dtype=torch.float64, device=DEV)
+        self.dtype = self.raw.dtype
+
+    def data_ptr(self):
+        return self.raw.data_ptr()
+
+    @property
+    def v(self):
+        return L.stat_fold(self.raw, self.C)
+
+    def __getitem__(self, idx):
+        return self.v[idx]
+
+    def abs(self):
+        return self.v.abs()
+
+    def __len__(self):
+        return self.raw.shape[0]
+
+
+class _Slice:
+    """Folded[i] as a statistics destination (pointer into the raw buffer) and value."""
+
+    def __init__(self, parent, idx):
+        self.parent, self.idx, self.dtype = parent, idx, torch.float64
+
+    def data_ptr(self):
+        return self.parent.raw[self.idx].data_ptr()
+
+    @property
+    def v(self):
+        return self.parent.v[self.idx]
+
+
+def stats_out(nseg, C):
+    """[(sum, sq)] per segment: replicated destinations for a producer's BN statistics."""
+    return [(Folded((), C), Folded((), C)) for _ in range(nseg)]
+
+
+def fv(t):
+    """The values of a Folded (or a plain tensor as is)."""
+    return t.v if isinstance(t, (Folded, _Slice)) else t
+
+
 def stat_out(pairs):
     so = L.StatOut()
     for i, (a, b) in enumerate(pairs):
@@ -84,11 +143,12 @@ def stat_out(pairs):
 
 
 def bngrad64(nseg, C):
-    """fp64 dgamma / dbeta accumulators [2][nseg][C] and their edet_bngrad64 descriptor."""
-    t = torch.zeros((2, nseg, C), dtype=torch.float64, device=DEV)
+    """fp64 dgamma / dbeta accumulators [2][nseg][C] (replicated, a Folded: index it for values)
+    and their edet_bngrad64 descriptor."""
+    t = Folded((2, nseg), C)
     d = L.BnGrad64()
     for i in range(nseg):
-        d.dgamma[i], d.dbeta[i] = t[0, i].data_ptr(), t[1, i].data_ptr()
+        d.dgamma[i], d.dbeta[i] = t.raw[0, i].data_ptr(), t.raw[1, i].data_ptr()
     return t, d
 
 
@@ -104,6 +164,7 @@ def zeros(*shape):
 
 
 def close(a, b, dt, scale=None, **kw):
+    a, b = fv(a), fv(b)
     a = a.double().cpu() if isinstance(a, torch.Tensor) else torch.as_tensor(a, dtype=torch.float64)
     b = b.double().cpu() if isinstance(b, torch.Tensor) else torch.as_tensor(b, dtype=torch.float64)
     tol = dict(TOL[dt])

@@ -34,7 +34,7 @@ def test_struct_layouts_match_header():
 
 def test_error_path_without_gpu():
     lib = _lib.lib()
-    assert lib.fns["edet_abi_version"]() == _lib.ABI_VERSION == 8
+    assert lib.fns["edet_abi_version"]() == _lib.ABI_VERSION == 9
     # argument validation happens before any HIP call
     rc = lib.fns["edet_conv1x1_fwd"](0, None, None, 8, None, 8, None, None, 8, 0, None, None)
     assert rc == -1 and "null" in lib.last_error()
@@ -59,3 +59,19 @@ def test_conv1x1_fwd_rejects_accumulate_with_lazy_a():
     rc = lib.fns["edet_conv1x1_fwd"](0, ctypes.byref(lz), ctypes.byref(pyr), 8, dummy, 8, None, dummy, 8, 1,
                                      None, None)
     assert rc == -1 and "plain A" in lib.last_error()
+
+
+def test_stat_layout_helpers():
+    """include/edet.h "Statistics vectors" (ABI 9): channel c of replica r at
+    (c / 16) * 64 + r * 16 + c % 16; the value is (r0 + r1) + (r2 + r3)."""
+    import torch
+    assert _lib.stat_len(1) == 64 and _lib.stat_len(16) == 64 and _lib.stat_len(17) == 128
+    assert _lib.stat_idx(0, 0) == 0 and _lib.stat_idx(5, 2) == 37 and _lib.stat_idx(17, 3) == 64 + 48 + 1
+    v = torch.arange(1, 21, dtype=torch.float64)
+    t = _lib.stat_unfold(v)
+    assert t.shape == (128,) and float(t.sum()) == float(v.sum())
+    t[_lib.stat_idx(3, 1)] += 0.5
+    t[_lib.stat_idx(3, 0)] -= 0.5
+    assert torch.equal(_lib.stat_fold(t, 20), v)
+    two = _lib.stat_unfold(torch.stack([v, 2 * v]))
+    assert two.shape == (2, 128) and torch.equal(_lib.stat_fold(two, 20)[1], 2 * v)

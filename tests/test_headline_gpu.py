@@ -186,7 +186,7 @@ class ActCapture:
         of the pool windows re-routed through such ties)."""
         from tf2mv_amd import _lib as L
         assert a.pyr.nseg == 1
-        ssum, ssq = a.bns[0].stats(a.training)
+        ssum, ssq = (L.stat_fold(t, a.C) for t in a.bns[0].stats(a.training))  # replicated (ABI 9)
         n = a.pyr.rows
         inv = float(np.float32(1.0 / n))
         mean = ssum.double() * inv

@@ -13,7 +13,7 @@ import torch.nn.functional as Fn
 
 from tf2mv_amd import _lib as L
 from tf2mv_amd.runtime import Pyr, stream, vp
-from gpu_util import DEV, DT, TDT, LazyDesc, bngrad64, close, g, make_bn, seg_out, stat_out, zeros, zeros64
+from gpu_util import DEV, DT, TDT, LazyDesc, bngrad64, close, fv, g, make_bn, rep64, seg_out, stat_out, stats_out, zeros, zeros64
 
 pytestmark = pytest.mark.gpu
 DTS = ["f32", "bf16"]
@@ -67,7 +67,7 @@ def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
     w = g(rnd(rng, N, K, scale=1 / math.sqrt(K)), dt)
     b = g(rnd(rng, N), "f32")
     y = torch.empty(pyr.rows, N, dtype=TDT[dt], device=DEV)
-    st = [(zeros64(N), zeros64(N)) for _ in range(nseg)]
+    st = stats_out(nseg, N)
     L.call("edet_conv1x1_fwd", DT[dt], lz.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, stat_out(st), stream())
     ref = lz.cpu_value() @ w.double().cpu().t() + b.double().cpu()
     for s in range(nseg):
@@ -237,7 +237,7 @@ def test_dwconv_fwd_bwd(dt, k, s, H, W, C, lazy, nseg, workspace_mode):
     lz = LazyDesc(x, pin, C, bn=bn, act=1 if lazy in (1, 3) else 0, gate=gate)
     w = g(rnd(rng, k * k, C, scale=0.3), dt)
     y = torch.empty(pout.rows, C, dtype=TDT[dt], device=DEV)
-    st = [(zeros64(C), zeros64(C)) for _ in range(nseg)]
+    st = stats_out(nseg, C)
     L.call("edet_dwconv_fwd", DT[dt], lz.c, pin.c, C, k, s, vp(w), vp(y), pout.c, stat_out(st), stream())
     v = lz.cpu_value().requires_grad_(True)
     wr = w.double().cpu().requires_grad_(True)
@@ -477,7 +477,7 @@ def test_dwconv_long_blocks(k, s, B, H, C):
     lz = LazyDesc(x, pin, C, bn=make_bn(x, pin, C, rng), act=1, gate=g(torch.rand(B, C), "f32"))
     w = g(rnd(rng, k * k, C, scale=0.3), "bf16")
     y = torch.empty(pout.rows, C, dtype=TDT["bf16"], device=DEV)
-    st = [(zeros64(C), zeros64(C))]
+    st = stats_out(1, C)
     L.call("edet_dwconv_fwd", DT["bf16"], lz.c, pin.c, C, k, s, vp(w), vp(y), pout.c, stat_out(st), stream())
     ref = dw_ref(lz.cpu_value(), pin, k, s, w.double().cpu())
     close(y, ref, "bf16")
@@ -497,7 +497,9 @@ def test_dwconv_long_blocks(k, s, B, H, C):
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("C,act,gate,dsq,scale,nseg", [(40, 0, 0, 0, 0, 1), (96, 1, 1, 1, 0, 1), (64, 1, 0, 0, 1, 2),
                                                         (144, 1, 0, 0, 0, 1), (24, 0, 0, 0, 0, 1), (240, 1, 1, 0, 0, 1),
-                                                        (672, 1, 1, 1, 0, 1), (672, 1, 0, 0, 0, 1)])
+                                                        (672, 1, 1, 1, 0, 1), (672, 1, 0, 0, 0, 1),
+                                                        # the channel-sliced apply (C >= 1024, M <= 16384)
+                                                        (1152, 1, 1, 1, 0, 1), (1152, 1, 0, 0, 1, 2)])
 def test_lazy_backward(dt, C, act, gate, dsq, scale, nseg):
     rng = np.random.default_rng(C + act * 7 + nseg)
     B = 3
@@ -505,6 +507,9 @@ def test_lazy_backward(dt, C, act, gate, dsq, scale, nseg):
     if C == 672:  # M = 32768: the long-chunk plans of the wide layers
         B = 32
         pyr = Pyr(B, [(32, 32)])
+    elif C == 1152 and nseg == 1:  # M = 8192: 18 channel slices x 64 chunks
+        B = 32
+        pyr = Pyr(B, [(16, 16)])
     x = pyr_data(rng, pyr, C, dt, scale=2.0)
     bn = make_bn(x, pyr, C, rng)
     gt = g(torch.rand(B, C) + 0.5, "f32") if gate else None
@@ -773,13 +778,17 @@ def test_bifpn_fuse_stored_pool_taps(dt, pool_in):
 
 
 @pytest.mark.parametrize("dt", DTS)
-@pytest.mark.parametrize("kind", ["gate", "pyramid"])
+@pytest.mark.parametrize("kind", ["gate", "pyramid", "wide", "wide_pyramid"])
 def test_lazy_materialize(dt, kind):
+    """wide: C = 1152 over 16x16 images (the channel-sliced plan, C >= 1024 and M <= 16384)."""
     rng = np.random.default_rng(31)
-    C = 48
-    pyr = Pyr(3, [(5, 7)]) if kind == "gate" else Pyr(2, [(4, 4), (2, 2)])
+    C = 1152 if kind.startswith("wide") else 48
+    pyr = {"gate": Pyr(3, [(5, 7)]), "pyramid": Pyr(2, [(4, 4), (2, 2)]), "wide": Pyr(32, [(16, 16)]),
+           "wide_pyramid": Pyr(2, [(9, 7), (3, 4)])}[kind]
+    if kind == "wide_pyramid":
+        kind = "pyramid"
     x = g(rnd(rng, pyr.rows, C), dt)
-    gate = g(torch.rand(pyr.batch, C), "f32") if kind == "gate" else None
+    gate = g(torch.rand(pyr.batch, C), "f32") if kind in ("gate", "wide") else None
     lz = LazyDesc(x, pyr, C, bn=make_bn(x, pyr, C, rng), act=1, gate=gate)
     out = torch.full((pyr.rows, C), float("nan"), dtype=TDT[dt], device=DEV)
     L.call("edet_lazy_materialize", DT[dt], lz.c, pyr.c, C, vp(out), stream())
@@ -819,8 +828,8 @@ def test_stem(dt, shape, workspace_mode):
     w = g(rnd(rng, 3, 3, 3, Co, scale=0.3), dt)
     OH, OW = (H + 1) // 2, (W + 1) // 2
     y = torch.empty(B * OH * OW, Co, dtype=TDT[dt], device=DEV)
-    su, sq = zeros64(Co), zeros64(Co)
-    L.call("edet_stem_fwd", DT[dt], vp(x), B, H, W, vp(w), Co, vp(y), vp(su), vp(sq), stream())
+    su, sq = stats_out(1, Co)[0]
+    L.call("edet_stem_fwd", DT[dt], vp(x), B, H, W, vp(w), Co, vp(y), vp(su.raw), vp(sq.raw), stream())
     xc = x.double().cpu().permute(0, 3, 1, 2)
     ph, pw = max((OH - 1) * 2 + 3 - H, 0), max((OW - 1) * 2 + 3 - W, 0)
     xp = Fn.pad(xc, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2))
@@ -1018,31 +1027,35 @@ def test_optimizer_skips_nonfinite_step(bad):
 def test_bn_moving_update_and_inference_stats():
     rng = np.random.default_rng(4)
     n = 300
-    su = (rnd(rng, n) * 50).double().to(DEV)  # fp64 statistics arena
+    su = (rnd(rng, n) * 50).double().to(DEV)  # fp64 statistics arena (values)
     sq = (torch.rand(n) * 500 + 2500).double().to(DEV)
+    sur, sqr = rep64(su), rep64(sq)  # the replicated layout the kernels read (ABI 9)
+    # the value split over the four replicas: the kernel must sum them
+    sur[L.stat_idx(5, 2)] += 3.0
+    sur[L.stat_idx(5, 0)] -= 3.0
     cnt = g(torch.full((n,), 100.0))
     mm, mv = g(rnd(rng, n)), g(torch.rand(n) + 0.5)
     MM, MV = mm.double().cpu(), mv.double().cpu()
-    L.call("edet_bn_update_moving", n, vp(su), vp(sq), vp(cnt), 0.99, None, vp(mm), vp(mv), stream())
+    L.call("edet_bn_update_moving", n, vp(sur), vp(sqr), vp(cnt), 0.99, None, vp(mm), vp(mv), stream())
     mean = su.double().cpu() / 100
     var = sq.double().cpu() / 100 - mean ** 2
     close(mm, MM - (MM - mean) * 0.01, "f32", rtol=1e-5)
     close(mv, MV - (MV - var * 100 / 99) * 0.01, "f32", rtol=1e-5)
-    s2, q2 = zeros64(n), zeros64(n)
-    L.call("edet_bn_inference_stats", n, vp(mm), vp(mv), vp(cnt), vp(s2), vp(q2), stream())
-    m2 = s2.double().cpu() / 100
+    s2, q2 = stats_out(1, n)[0]
+    L.call("edet_bn_inference_stats", n, vp(mm), vp(mv), vp(cnt), vp(s2.raw), vp(q2.raw), stream())
+    m2 = s2.v.double().cpu() / 100
     close(m2, mm, "f32", rtol=1e-6)
-    close(q2.double().cpu() / 100 - m2 ** 2, mv, "f32", rtol=1e-3, atol=1e-4)
+    close(q2.v.double().cpu() / 100 - m2 ** 2, mv, "f32", rtol=1e-3, atol=1e-4)
     # the optimizer's skip flag (scalars[6]) set: a skipped step leaves the moving statistics
     # alone, NaN batch sums included; flag clear: the update runs
     skip = g(torch.tensor([1.0]))
-    su[7] = float("nan")
+    sur[L.stat_idx(7, 1)] = float("nan")
     mm0, mv0 = mm.clone(), mv.clone()
-    L.call("edet_bn_update_moving", n, vp(su), vp(sq), vp(cnt), 0.99, vp(skip), vp(mm), vp(mv), stream())
+    L.call("edet_bn_update_moving", n, vp(sur), vp(sqr), vp(cnt), 0.99, vp(skip), vp(mm), vp(mv), stream())
     torch.cuda.synchronize()
     assert torch.equal(mm, mm0) and torch.equal(mv, mv0)
     skip.zero_()
-    L.call("edet_bn_update_moving", n, vp(su), vp(sq), vp(cnt), 0.99, vp(skip), vp(mm), vp(mv), stream())
+    L.call("edet_bn_update_moving", n, vp(sur), vp(sqr), vp(cnt), 0.99, vp(skip), vp(mm), vp(mv), stream())
     torch.cuda.synchronize()
     assert not torch.equal(mm, mm0) and math.isnan(float(mm[7]))
 
@@ -1115,7 +1128,7 @@ def test_gate_bn_reduce_equals_separate_passes(dt, C, HW):
     # with the terms summed (the sliced form sums 32 row groups of H*W / 32 rows)
     torch.testing.assert_close(s5[0], dg, rtol=1e-5, atol=1e-6 * max(1.0, HW / 64))
     scale = float(acc_t.abs().max())
-    torch.testing.assert_close(acc2_t, acc_t, rtol=1e-4, atol=1e-5 * scale)
+    torch.testing.assert_close(acc2_t.v, acc_t.v, rtol=1e-4, atol=1e-5 * scale)
     # edet_se_bwd_bn == edet_se_bwd then edet_se_bn_combine (its dsq): the SE gradients bit for
     # bit, the fp64 BN sums to fp64 rounding (the combine kernel adds the images as a tree)
     R = 8
@@ -1134,7 +1147,7 @@ def test_gate_bn_reduce_equals_separate_passes(dt, C, HW):
             L.call("edet_se_bwd", *args, stream())
             L.call("edet_se_bn_combine", B, C, vp(gt), vp(dsq2), vp(s5), a, stream())
         torch.cuda.synchronize()
-        outs.append([t.cpu() for t in dws] + [dsq2.cpu(), a_t.cpu()])
+        outs.append([t.cpu() for t in dws] + [dsq2.cpu(), a_t.v.cpu()])
     for u, v in zip(outs[0][:-1], outs[1][:-1]):
         assert torch.equal(u, v)
     torch.testing.assert_close(outs[1][-1], outs[0][-1], rtol=1e-12, atol=1e-12 * float(outs[0][-1].abs().max()))

@@ -14,7 +14,7 @@ import torch
 
 from tf2mv_amd import _lib as L
 from tf2mv_amd.runtime import Pyr, stream, vp
-from gpu_util import DEV, DT, TDT, LazyDesc, bngrad64, close, g, make_bn, seg_out, stat_out, zeros, zeros64
+from gpu_util import DEV, DT, TDT, LazyDesc, bngrad64, close, fv, g, make_bn, rep64, seg_out, stat_out, stats_out, zeros, zeros64
 
 pytestmark = pytest.mark.gpu
 DTS = ["f32", "bf16"]
@@ -48,7 +48,7 @@ def test_conv1x1_fwd_large(dt, kind, K, N, lazy):
     ys, sts = [], []
     for _ in range(2):
         y = torch.full((pyr.rows, N), float("nan"), dtype=TDT[dt], device=DEV)
-        st = [(zeros64(N), zeros64(N)) for _ in range(pyr.nseg)]
+        st = stats_out(pyr.nseg, N)
         L.call("edet_conv1x1_fwd", DT[dt], lz.c, pyr.c, K, vp(w), N, vp(b), vp(y), N, 0, stat_out(st), stream())
         ys.append(y)
         sts.append(st)
@@ -122,7 +122,7 @@ def test_dwconv_fwd_large(dt, k, s, kind, C, lazy):
     ys, sts = [], []
     for _ in range(2):
         y = torch.full((pout.rows, C), float("nan"), dtype=TDT[dt], device=DEV)
-        st = [(zeros64(C), zeros64(C)) for _ in range(pin.nseg)]
+        st = stats_out(pin.nseg, C)
         L.call("edet_dwconv_fwd", DT[dt], lz.c, pin.c, C, k, s, vp(w), vp(y), pout.c, stat_out(st), stream())
         ys.append(y)
         sts.append(st)
