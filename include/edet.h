@@ -346,6 +346,33 @@ int edet_bifpn_fuse_bwd(int dtype, int n_in, const edet_fuse_input* ins, const f
                         int B, int H, int W, int C, const void* out, const void* dout,
                         float* dw, edet_stream_t stream);
 
+/* ABI 10: the fusion backward in one pass from the gradient of the node's VALUE
+ * (bifpn.py:59-66 with OpAfterCombine's swish, bifpn.py:26): dv = d act(F) [B*H*W][C], out = the
+ * raw fused F the forward wrote, out_act = act (0 none, 1 swish).  d(raw F) is formed in
+ * registers, so the caller runs no d(value) -> d(raw) pass over the output.  dx of every input as
+ * edet_bifpn_fuse_bwd (accumulate honoured).  The weight gradient leaves as per-block sums in
+ * part[nparts][4] floats (no atomics); edet_bifpn_fuse_fold adds them into dw.
+ * edet_bifpn_fuse_bwd_dv_parts sets *nparts to the number of float4 records the launch writes,
+ * or 0 when the node is not covered (bf16 only; the input-mode combinations of the BiFPN; an
+ * upsampled input must be exactly x2; a max-pooled input needs the forward's pool_arg taps):
+ * the caller then uses edet_bifpn_fuse_bwd. */
+int edet_bifpn_fuse_bwd_dv_parts(int dtype, int n_in, const edet_fuse_input* ins, int B, int H,
+                                 int W, int C, int* nparts);
+int edet_bifpn_fuse_bwd_dv(int dtype, int n_in, const edet_fuse_input* ins, const float* w,
+                           int B, int H, int W, int C, const void* out, const void* dv,
+                           int out_act, float* part, int nparts, edet_stream_t stream);
+
+/* one node's weight-gradient records: dw[i] += (sum_b part[b][i]) / (sum_i w[i] + 1e-4),
+ * i < n_in, the records summed in a fixed order in fp64 (reproducible) */
+typedef struct edet_fuse_fold {
+  const float* part;    /* [nparts][4] from edet_bifpn_fuse_bwd_dv */
+  const float* w;       /* the node's n_in fusion weights */
+  float* dw;            /* their gradient (added to) */
+  int32_t nparts, n_in;
+} edet_fuse_fold;
+#define EDET_FUSE_FOLD_MAX 64  /* items per launch; longer lists take several launches */
+int edet_bifpn_fuse_fold(int n, const edet_fuse_fold* items, edet_stream_t stream);
+
 /* ---- detection loss (focal + Huber), forward and backward in one pass ----
  * cls: [rows][ldc] logits (A*NC used), box: [rows][ldb] (A*4 used).
  * cls_t [rows][A] class index, box_t [rows][A][4], npos_sum = sum of positive masks

@@ -15,7 +15,7 @@ import torch  # noqa: F401
 from ctypes import POINTER, c_char_p, c_float, c_int, c_int32, c_int64, c_size_t, c_uint64, c_void_p
 
 MAX_SEG = 5
-ABI_VERSION = 9  # must equal edet_abi_version() of the loaded library (struct layouts)
+ABI_VERSION = 10  # must equal edet_abi_version() of the loaded library (struct layouts)
 OPT_NORM_BLOCKS = 256  # EDET_OPT_NORM_BLOCKS: edet_opt_norm partial-sum slots per quantity
 F32, BF16 = 0, 1
 # replicated statistics vectors (include/edet.h, ABI 9): channel c of replica r at stat_idx(c, r)
@@ -99,6 +99,14 @@ class FuseInput(ctypes.Structure):
                 ("mode", c_int32), ("accumulate", c_int32), ("pool_arg", c_void_p)]
 
 
+class FuseFold(ctypes.Structure):
+    """edet_fuse_fold: one BiFPN node's weight-gradient records (ABI 10)."""
+    _fields_ = [("part", c_void_p), ("w", c_void_p), ("dw", c_void_p), ("nparts", c_int32), ("n_in", c_int32)]
+
+
+FUSE_FOLD_MAX = 64  # EDET_FUSE_FOLD_MAX
+
+
 class Sched(ctypes.Structure):
     _fields_ = [("adjusted_lr", c_float), ("warmup_init", c_float), ("warmup_steps", c_int32),
                 ("total_steps", c_int32), ("momentum", c_float), ("ema_decay", c_float),
@@ -159,6 +167,9 @@ SIGNATURES = {
     "edet_maxpool_bwd": [c_int, PLazy, c_int, c_int, c_int, c_int, P, P, c_int, P],
     "edet_bifpn_fuse_fwd": [c_int, c_int, PFuse, P, c_int, c_int, c_int, c_int, P, P],
     "edet_bifpn_fuse_bwd": [c_int, c_int, PFuse, P, c_int, c_int, c_int, c_int, P, P, P, P],
+    "edet_bifpn_fuse_bwd_dv_parts": [c_int, c_int, PFuse, c_int, c_int, c_int, c_int, POINTER(c_int)],
+    "edet_bifpn_fuse_bwd_dv": [c_int, c_int, PFuse, P, c_int, c_int, c_int, c_int, P, P, c_int, P, c_int, P],
+    "edet_bifpn_fuse_fold": [c_int, POINTER(FuseFold), P],
     "edet_detection_loss": [c_int, P, c_int, P, c_int, PPyr, c_int, c_int, P, P, P, c_float,
                             c_float, c_float, c_float, c_float, P, P, P, P, P],
     "edet_count_positives": [P, c_int64, P, P],
@@ -200,9 +211,10 @@ class _Lib:
             fn.restype = _RESTYPE.get(name, c_int)
             self.fns[name] = fn
         abi = self.fns["edet_abi_version"]()
-        # same-box timing A/B only: an ABI 8 build (plain statistics vectors) runs in the larger
-        # replicated buffers of ABI 9 without leaving them; its values are not the model's
-        if abi != ABI_VERSION and not (allow_missing and abi == 8):
+        # same-box timing A/B only: an ABI 9 build lacks the ABI 10 entry points (the callers
+        # check has()); an ABI 8 build (plain statistics vectors) runs in the larger replicated
+        # buffers of ABI 9 without leaving them, its values are not the model's
+        if abi != ABI_VERSION and not (allow_missing and abi in (8, 9)):
             raise ImportError(f"{path} implements C-ABI version {abi}, this binding expects {ABI_VERSION}: "
                               f"rebuild it with `make -C tensorflow2-machine-vision_amd`")
         # development builds only (EDET_LIB=.../libedet_dev.so): plan slots for whole-step A/B runs,
@@ -214,6 +226,9 @@ class _Lib:
                 raise ImportError(f"EDET_DEV_SLOTS needs a development build (make dev): {path}")
             if rc != 0:
                 raise ImportError(f"EDET_DEV_SLOTS: {self.last_error()}")
+
+    def has(self, name: str) -> bool:
+        return name in self.fns
 
     def last_error(self) -> str:
         return self.fns["edet_last_error"]().decode(errors="replace")
@@ -237,6 +252,10 @@ def lib() -> _Lib:
 
 def call(name: str, *args):
     return lib().call(name, *args)
+
+
+def has(name: str) -> bool:
+    return lib().has(name)
 
 
 def launched_kernels() -> list:

@@ -958,6 +958,252 @@ __global__ __launch_bounds__(256) void k_fuse_bwd_m(FuseArgs g) {
   if (tid < NIN) atomicAdd(g.dw + tid, red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3]);
 }
 
+// ------------------------------------------------------------------ fusion backward from d(value) (ABI 10)
+// One pass over the node (bifpn.py:59-66 + OpAfterCombine's swish, :26) from the gradient of
+// its VALUE dv = d act(F): dF = dv * act'(F) is formed in registers, so the separate
+// d(value) -> d(raw) pass over the output and its re-reads by the dx and weight-gradient blocks
+// are gone.  Two kinds of blocks:
+//  * quad blocks: a thread owns a 2x2 output quad x 8 channels.  It loads dv and F of the quad,
+//    every same-size input's raw vectors and the exact-x2 upsampled input's one source vector
+//    (the quad's nearest source), writes the same-size inputs' dx (4 vectors each) and the
+//    upsampled input's dx (the quad's sum, 1 vector), and adds dF * (v_i - F) per element.
+//  * pool blocks (first, the heavier ones): a thread owns one pixel x 8 channels of the
+//    max-pooled input; with the forward's recorded taps it gathers dF from the <= 2x2 windows
+//    holding the pixel (dv and F loaded with the taps) and, for every window whose tap picks the
+//    pixel, adds dF * (x(pixel) - F(window)): each output counted once, at its argmax.
+// The weight gradient leaves as one float4 of per-input sums per block (fixed order, no
+// atomics); edet_bifpn_fuse_fold sums them per node and divides by (sum w + 1e-4).
+struct FuseDvArgs {
+  edet_fuse_input in[3];
+  const float* w;
+  const void* fused;  // raw F [B*H*W][C]
+  const void* dv;     // d(value) [B*H*W][C]
+  float4* part;       // [blocks]
+  int B, H, W, C, QH, QW;
+  int nb_pool;  // pool blocks (the first ones); 0 without a max-pooled input
+};
+
+template <int OACT>
+__device__ __forceinline__ void fuse_df(const uint4& dq, const uint4& fq, float* F, float* d) {
+  unpack_bf8(fq, F);
+  unpack_bf8(dq, d);
+  if constexpr (OACT == 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] *= dswishf_(F[j]);
+  }
+}
+
+template <int M0, int M1, int M2, int ACT, int OACT>
+__global__ __launch_bounds__(256) void k_fuse_bwd_dv(FuseDvArgs g) {
+  using T = uint16_t;
+  constexpr int NIN = 2 + (M2 >= 0);
+  constexpr int MODE[3] = {M0, M1, M2};
+  constexpr int PI = M2 == EDET_MODE_MAXPOOL ? 2 : (M1 == EDET_MODE_MAXPOOL ? 1 : -1);
+  extern __shared__ float2 aft[];  // [n_in][C]
+  __shared__ float red[3][4];
+  for (int i = 0; i < NIN; ++i)
+    load_affine(g.in[i].v, g.C, 1.f / (float)(g.B * g.in[i].H * g.in[i].W), aft + i * g.C);
+  __syncthreads();
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = g.C, nv = C / 8;
+  const float den = fuse_denom(g.w, NIN);
+  float wn[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) wn[i] = i < NIN ? g.w[i] / den : 0.f;
+  float part[3] = {0.f, 0.f, 0.f};
+  const T* Fp = (const T*)g.fused;
+  const T* Dp = (const T*)g.dv;
+  const int b = blockIdx.x;
+  if constexpr (PI >= 0) {
+    if (b < g.nb_pool) {
+      const edet_fuse_input& fi = g.in[PI];
+      const int Hi = fi.H, Wi = fi.W;
+      const long idx = (long)b * 256 + tid;
+      if (idx < (long)g.B * Hi * Wi * nv) {
+        const int cv = (int)(idx % nv), c = cv * 8;
+        const long pix = idx / nv;
+        const int n = (int)(pix / ((long)Hi * Wi));
+        const int rem = (int)(pix - (long)n * Hi * Wi);
+        const int iy = rem / Wi, ix = rem - iy * Wi;
+        const int pt = same_pad(Hi, 3, 2), pl = same_pad(Wi, 3, 2);
+        const int oy_lo = max(0, fdiv(iy + pt - 1, 2)), oy_hi = min(g.H - 1, fdiv(iy + pt, 2));
+        const int ox_lo = max(0, fdiv(ix + pl - 1, 2)), ox_hi = min(g.W - 1, fdiv(ix + pl, 2));
+        const size_t o0 = (size_t)n * g.H * g.W;
+        uint2 tq[4];
+        uint4 dq[4], fq[4];
+        bool okk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int oy = oy_lo + (k >> 1), ox = ox_lo + (k & 1);
+          okk[k] = oy <= oy_hi && ox <= ox_hi;
+          const size_t o = (o0 + (okk[k] ? (size_t)oy * g.W + ox : 0)) * C + c;
+          tq[k] = *reinterpret_cast<const uint2*>(fi.pool_arg + o);
+          dq[k] = gld16(Dp + o);
+          fq[k] = gld16(Fp + o);
+        }
+        const uint4 xq = gld16((const T*)fi.v.x + (size_t)pix * C + c);
+        float xv[8], d[8];
+        {
+          float2 af[8];
+          affine8_lds(aft + PI * C, c, af);
+          unpack_bf8(xq, xv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { xv[j] = fuse_act<ACT>(xv[j], af[j], fi.v.act); d[j] = 0.f; }
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (!okk[k]) continue;
+          const int oy = oy_lo + (k >> 1), ox = ox_lo + (k & 1);
+          const int kme = (iy - (oy * 2 - pt)) * 3 + (ix - (ox * 2 - pl));
+          float F[8], dd[8];
+          fuse_df<OACT>(dq[k], fq[k], F, dd);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int tap = (int)(((j < 4 ? tq[k].x : tq[k].y) >> (8 * (j & 3))) & 0xffu);
+            if (tap == kme) {
+              d[j] += dd[j];
+              s += dd[j] * (xv[j] - F[j]);
+            }
+          }
+        }
+        part[PI] = s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] *= wn[PI];
+        acc8m((T*)fi.dx + (size_t)pix * C + c, 8, d, fi.accumulate);
+      }
+    }
+  }
+  if (PI < 0 || b >= g.nb_pool) {
+    const long q = (long)(b - g.nb_pool) * 256 + tid;
+    if (q < (long)g.B * g.QH * g.QW * nv) {
+      const int cv = (int)(q % nv), c = cv * 8;
+      long r = q / nv;
+      const int qx = (int)(r % g.QW);
+      r /= g.QW;
+      const int qy = (int)(r % g.QH), n = (int)(r / g.QH);
+      const size_t o0 = (size_t)n * g.H * g.W;
+      bool ok[4];
+      size_t po[4];  // element offset of the quad's pixel p (invalid ones alias pixel 0)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int y = 2 * qy + (p >> 1), x = 2 * qx + (p & 1);
+        ok[p] = y < g.H && x < g.W;
+        po[p] = (o0 + (size_t)(ok[p] ? y : 2 * qy) * g.W + (ok[p] ? x : 2 * qx)) * C + c;
+      }
+      uint4 dq[4], fq[4], sq[3][4], uq[3];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        dq[p] = gld16(Dp + po[p]);
+        fq[p] = gld16(Fp + po[p]);
+      }
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) {
+        const T* X = (const T*)g.in[i].v.x;
+        if (MODE[i] == EDET_MODE_SAME) {
+#pragma unroll
+          for (int p = 0; p < 4; ++p) sq[i][p] = gld16(X + po[p]);
+        } else if (MODE[i] == EDET_MODE_UPSAMPLE) {
+          uq[i] = gld16(X + (((size_t)n * g.in[i].H + qy) * g.in[i].W + qx) * C + c);
+        }
+      }
+      float vu[8], du[8];
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) {
+        if (MODE[i] == EDET_MODE_UPSAMPLE) {
+          float2 af[8];
+          affine8_lds(aft + i * C, c, af);
+          unpack_bf8(uq[i], vu);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { vu[j] = fuse_act<ACT>(vu[j], af[j], g.in[i].v.act); du[j] = 0.f; }
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (!ok[p]) continue;
+        float F[8], d[8];
+        fuse_df<OACT>(dq[p], fq[p], F, d);
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) {
+          if (MODE[i] == EDET_MODE_SAME) {
+            float2 af[8];
+            affine8_lds(aft + i * C, c, af);
+            float v[8], o[8], s = 0.f;
+            unpack_bf8(sq[i][p], v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              s += d[j] * (fuse_act<ACT>(v[j], af[j], g.in[i].v.act) - F[j]);
+              o[j] = d[j] * wn[i];
+            }
+            part[i] += s;
+            acc8m((T*)g.in[i].dx + po[p], 8, o, g.in[i].accumulate);
+          } else if (MODE[i] == EDET_MODE_UPSAMPLE) {
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              s += d[j] * (vu[j] - F[j]);
+              du[j] += d[j];
+            }
+            part[i] += s;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) {
+        if (MODE[i] == EDET_MODE_UPSAMPLE) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) du[j] *= wn[i];
+          acc8m((T*)g.in[i].dx + (((size_t)n * g.in[i].H + qy) * g.in[i].W + qx) * C + c, 8, du,
+                g.in[i].accumulate);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float s = wave_sum(part[i]);
+    if (lane == 0) red[i][wave] = s;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float4 o;
+    o.x = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    o.y = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    o.z = (red[2][0] + red[2][1]) + (red[2][2] + red[2][3]);
+    o.w = 0.f;
+    g.part[b] = o;
+  }
+}
+
+// dw[i] += (sum over the node's blocks of part[.][i]) / (sum w + 1e-4), per node; the blocks'
+// sums added in a fixed order (fp64), so the result does not depend on scheduling
+struct FuseFoldArgs {
+  edet_fuse_fold it[EDET_FUSE_FOLD_MAX];
+};
+__global__ __launch_bounds__(256) void k_fuse_fold(FuseFoldArgs a) {
+  __shared__ double red[3][4];
+  const edet_fuse_fold f = a.it[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float4* P = (const float4*)f.part;
+  double s[3] = {0.0, 0.0, 0.0};
+  for (int b = tid; b < f.nparts; b += 256) {
+    const float4 p = P[b];
+    s[0] += p.x; s[1] += p.y; s[2] += p.z;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    double v = s[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[i][wave] = v;
+  }
+  __syncthreads();
+  if (tid < f.n_in) {
+    const double t = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
+    f.dw[tid] += (float)(t / (double)fuse_denom(f.w, f.n_in));
+  }
+}
+
 }  // namespace edet
 
 using namespace edet;
@@ -1176,6 +1422,99 @@ int edet_bifpn_fuse_bwd(int dtype, int n_in, const edet_fuse_input* ins, const f
     if (nb) EDET_LAUNCH(k_fuse_bwd<T>, dim3(nb), dim3(256), n_in * C * sizeof(float2), (hipStream_t)stream, g);
     return check_launch("edet bifpn_fuse_bwd");
   });
+}
+
+// the one-pass backward's plan: 0 blocks = this node is not covered (dtype, input-mode
+// combination, an upsample that is not exactly x2, a max-pooled input without recorded taps)
+static long fuse_dv_plan(int dtype, int n_in, const edet_fuse_input* ins, int B, int H, int W, int C,
+                         int* nb_pool) {
+  *nb_pool = 0;
+  if (dtype != EDET_BF16 || n_in < 2 || n_in > 3 || C % 8 || dev_knob(34) == 2) return 0;
+  const int m0 = ins[0].mode, m1 = ins[1].mode, m2 = n_in == 3 ? ins[2].mode : -1;
+  constexpr int S_ = EDET_MODE_SAME, U_ = EDET_MODE_UPSAMPLE, P_ = EDET_MODE_MAXPOOL;
+  const bool combo = (m0 == S_ && m1 == U_ && m2 == -1) || (m0 == S_ && m1 == S_ && m2 == P_) ||
+                     (m0 == S_ && m1 == P_ && m2 == -1) || (m0 == S_ && m1 == S_ && m2 == U_) ||
+                     (m0 == S_ && m1 == S_ && m2 == -1);
+  if (!combo) return 0;
+  const int nv = C / 8;
+  for (int i = 0; i < n_in; ++i) {
+    const edet_fuse_input& f = ins[i];
+    if (f.mode == U_ && (H != 2 * f.H || W != 2 * f.W)) return 0;
+    if (f.mode == P_) {
+      if (!f.pool_arg) return 0;
+      *nb_pool = (int)(((long)B * f.H * f.W * nv + 255) / 256);
+    }
+  }
+  return *nb_pool + ((long)B * cdiv(H, 2) * cdiv(W, 2) * nv + 255) / 256;
+}
+
+int edet_bifpn_fuse_bwd_dv_parts(int dtype, int n_in, const edet_fuse_input* ins, int B, int H, int W, int C,
+                                 int* nparts) {
+  EDET_REQUIRE(nparts && (n_in == 0 || ins), "bifpn_fuse_bwd_dv_parts: null argument");
+  int nbp;
+  const long nb = fuse_dv_plan(dtype, n_in, ins, B, H, W, C, &nbp);
+  EDET_REQUIRE(nb < (1L << 31), "bifpn_fuse_bwd_dv_parts: too many blocks");
+  *nparts = (int)nb;
+  return EDET_OK;
+}
+
+int edet_bifpn_fuse_bwd_dv(int dtype, int n_in, const edet_fuse_input* ins, const float* w, int B, int H, int W,
+                           int C, const void* out, const void* dv, int out_act, float* part, int nparts,
+                           edet_stream_t stream) {
+  FuseDvArgs g{};
+  FuseArgs s{};
+  int rc = fuse_setup(s, n_in, ins, w, B, H, W, C);
+  if (rc) return rc;
+  EDET_REQUIRE(out && dv && part, "bifpn_fuse_bwd_dv: null argument");
+  EDET_REQUIRE(out_act == 0 || out_act == 1, "bifpn_fuse_bwd_dv: out_act must be 0 or 1");
+  for (int i = 0; i < n_in; ++i) EDET_REQUIRE(ins[i].dx, "bifpn_fuse_bwd_dv: input %d has no dx", i);
+  int nbp;
+  const long nb = fuse_dv_plan(dtype, n_in, ins, B, H, W, C, &nbp);
+  EDET_REQUIRE(nb > 0, "bifpn_fuse_bwd_dv: node not covered (edet_bifpn_fuse_bwd_dv_parts returned 0)");
+  EDET_REQUIRE(nparts == nb, "bifpn_fuse_bwd_dv: nparts %d, the plan has %ld", nparts, nb);
+  for (int i = 0; i < n_in; ++i) g.in[i] = ins[i];
+  g.w = w; g.fused = out; g.dv = dv; g.part = (float4*)part;
+  g.B = B; g.H = H; g.W = W; g.C = C; g.QH = cdiv(H, 2); g.QW = cdiv(W, 2);
+  g.nb_pool = nbp;
+  const size_t lds = n_in * C * sizeof(float2);
+  const int m0 = ins[0].mode, m1 = ins[1].mode, m2 = n_in == 3 ? ins[2].mode : -1;
+  constexpr int S_ = EDET_MODE_SAME, U_ = EDET_MODE_UPSAMPLE, P_ = EDET_MODE_MAXPOOL;
+  hipStream_t st = (hipStream_t)stream;
+  const int act = fuse_common_act(n_in, ins);
+#define EDET_FUSE_DV(A, B_, C_, OA)                                                                       \
+  do {                                                                                                   \
+    if (act == 0) EDET_LAUNCH((k_fuse_bwd_dv<A, B_, C_, 0, OA>), dim3(nb), dim3(256), lds, st, g);       \
+    else if (act == 1) EDET_LAUNCH((k_fuse_bwd_dv<A, B_, C_, 1, OA>), dim3(nb), dim3(256), lds, st, g);  \
+    else EDET_LAUNCH((k_fuse_bwd_dv<A, B_, C_, -1, OA>), dim3(nb), dim3(256), lds, st, g);               \
+  } while (0)
+#define EDET_FUSE_DV2(A, B_, C_)                   \
+  do {                                             \
+    if (out_act) EDET_FUSE_DV(A, B_, C_, 1);       \
+    else EDET_FUSE_DV(A, B_, C_, 0);               \
+  } while (0)
+  if (m0 == S_ && m1 == U_ && m2 == -1) EDET_FUSE_DV2(S_, U_, -1);
+  else if (m0 == S_ && m1 == S_ && m2 == P_) EDET_FUSE_DV2(S_, S_, P_);
+  else if (m0 == S_ && m1 == P_ && m2 == -1) EDET_FUSE_DV2(S_, P_, -1);
+  else if (m0 == S_ && m1 == S_ && m2 == U_) EDET_FUSE_DV2(S_, S_, U_);
+  else EDET_FUSE_DV2(S_, S_, -1);
+#undef EDET_FUSE_DV2
+#undef EDET_FUSE_DV
+  return check_launch("edet bifpn_fuse_bwd_dv");
+}
+
+int edet_bifpn_fuse_fold(int n, const edet_fuse_fold* items, edet_stream_t stream) {
+  EDET_REQUIRE(n >= 0 && (n == 0 || items), "bifpn_fuse_fold: bad arguments");
+  for (int i = 0; i < n; ++i)
+    EDET_REQUIRE(items[i].part && items[i].w && items[i].dw && items[i].nparts >= 0 && items[i].n_in >= 1 &&
+                     items[i].n_in <= 3,
+                 "bifpn_fuse_fold: bad item %d", i);
+  for (int i0 = 0; i0 < n; i0 += EDET_FUSE_FOLD_MAX) {
+    const int m = std::min(n - i0, EDET_FUSE_FOLD_MAX);
+    FuseFoldArgs a{};
+    for (int i = 0; i < m; ++i) a.it[i] = items[i0 + i];
+    EDET_LAUNCH(k_fuse_fold, dim3(m), dim3(256), 0, (hipStream_t)stream, a);
+  }
+  return check_launch("edet bifpn_fuse_fold");
 }
 
 }  // extern "C"

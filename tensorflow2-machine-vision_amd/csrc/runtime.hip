@@ -104,7 +104,7 @@ extern "C" {
 
 const char* edet_last_error(void) { return edet::g_err; }
 
-int edet_abi_version(void) { return 9; }  // 3: edet_fuse_input.pool_arg; 4: opt norm partials; 5: dwconv_bwd; 6: dwconv_fwd_squeeze; 7: skip_nonfinite + opt_apply step; 8: bn_update_moving skip flag; 9: replicated statistics vectors
+int edet_abi_version(void) { return 10; }  // 3: edet_fuse_input.pool_arg; 4: opt norm partials; 5: dwconv_bwd; 6: dwconv_fwd_squeeze; 7: skip_nonfinite + opt_apply step; 8: bn_update_moving skip flag; 9: replicated statistics vectors; 10: one-pass fusion backward + fold
 
 int edet_launched_kernels(char* buf, size_t size) {
   EDET_REQUIRE(buf && size > 0, "launched_kernels: null buffer");

@@ -16,6 +16,7 @@ Reference call sites replaced (AIServer/ai_api/ai_models/...):
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import List, Optional, Sequence, Tuple
 
@@ -383,6 +384,20 @@ def maxpool(eng: Engine, x: Act, name: str = "") -> Act:
     return out
 
 
+# EDET_FUSE_DV=0: the two-pass fusion backward (d(value) -> d(raw) apply, then
+# edet_bifpn_fuse_bwd) for same-box A/B against the one-pass edet_bifpn_fuse_bwd_dv
+FUSE_DV = os.environ.get("EDET_FUSE_DV", "1") != "0"
+
+
+def _fuse_fold(items):
+    """One launch adding every node's weight-gradient records into its gradient view."""
+    arr = (L.FuseFold * len(items))()
+    for k, (part, wvec, grad, nparts, n) in enumerate(items):
+        arr[k].part, arr[k].w, arr[k].dw = part.data_ptr(), wvec.data_ptr(), grad.data_ptr()
+        arr[k].nparts, arr[k].n_in = nparts, n
+    L.call("edet_bifpn_fuse_fold", len(items), arr, stream())
+
+
 def bifpn_fuse(eng: Engine, P: ParamStore, inputs: Sequence[Tuple[Act, int]], wnames: Sequence[str],
                H: int, W: int, name: str = "") -> Act:
     """sum_i R_i(v_i) * w_i / (sum w + 1e-4); returned lazily as swish(sum) (OpAfterCombine)."""
@@ -411,17 +426,32 @@ def bifpn_fuse(eng: Engine, P: ParamStore, inputs: Sequence[Tuple[Act, int]], wn
         rec = eng.tape.take(out)
         if rec is None:
             return
-        dF, _ = value_grad_to_raw(eng, out, rec)
         fb = (L.FuseInput * n)()
         for i, (a, mode) in enumerate(inputs):
-            dx, acc = eng.tape.dst(a)
             fb[i].v = a.lazy()
             fb[i].H, fb[i].W, fb[i].mode = a.pyr.H, a.pyr.W, mode
+            fb[i].pool_arg = taps[i].data_ptr() if taps[i] is not None else None
+        # one pass from d(value) (ABI 10) where the library covers the node: d(raw) formed in
+        # registers, the weight gradient as per-block records folded once after the backward
+        nparts = ctypes.c_int(0)
+        if (FUSE_DV and rec.scale is None and rec.ld == C and out.bns is None and out.gate is None
+                and L.has("edet_bifpn_fuse_bwd_dv")):
+            L.call("edet_bifpn_fuse_bwd_dv_parts", eng.dt, n, fb, B, H, W, C, ctypes.byref(nparts))
+        dF = None
+        if nparts.value == 0:
+            dF, _ = value_grad_to_raw(eng, out, rec)
+        for i, (a, _) in enumerate(inputs):
+            dx, acc = eng.tape.dst(a)
             fb[i].dx = dx.data_ptr()
             fb[i].accumulate = acc
-            fb[i].pool_arg = taps[i].data_ptr() if taps[i] is not None else None
-        L.call("edet_bifpn_fuse_bwd", eng.dt, n, fb, vp(wvec), B, H, W, C, vp(y), vp(dF),
-               vp(P.grad(wnames[0])), stream())
+        if dF is not None:
+            L.call("edet_bifpn_fuse_bwd", eng.dt, n, fb, vp(wvec), B, H, W, C, vp(y), vp(dF),
+                   vp(P.grad(wnames[0])), stream())
+            return
+        part = torch.empty(nparts.value * 4, dtype=torch.float32, device=eng.device)
+        L.call("edet_bifpn_fuse_bwd_dv", eng.dt, n, fb, vp(wvec), B, H, W, C, vp(y), vp(rec.t),
+               1 if out.act == L.ACT_SWISH else 0, vp(part), nparts.value, stream())
+        eng.tape.collect("bifpn_fuse_fold", _fuse_fold, (part, wvec, P.grad(wnames[0]), nparts.value, n))
 
     eng.record(bwd)
     return out

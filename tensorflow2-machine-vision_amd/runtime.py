@@ -414,6 +414,9 @@ class Tape:
         self.entries: List = []
         self.g: Dict[Act, GradRec] = {}
         self.trace = trace  # debug: list receiving (act name, fp32 copy of d(value)) per take()
+        # work gathered over the backward and launched once after the last closure:
+        # key -> (fn(items), items) (the BiFPN fusion weight-gradient fold, ops.bifpn_fuse)
+        self.finals: Dict[str, Tuple] = {}
 
     def record(self, fn):
         self.entries.append(fn)
@@ -443,10 +446,17 @@ class Tape:
             self.trace.append((act.name, torch.cat(rows, 0).clone(), None if rec.scale is None else rec.scale.clone()))
         return rec
 
+    def collect(self, key: str, fn, item):
+        """Add `item` to the list `fn` receives once, after every backward closure has run."""
+        self.finals.setdefault(key, (fn, []))[1].append(item)
+
     def backward(self):
         entries, self.entries = self.entries, []
         for fn in reversed(entries):
             fn()
+        finals, self.finals = self.finals, {}
+        for fn, items in finals.values():
+            fn(items)
         self.g.clear()
         self.eng.join_side()
 

@@ -34,7 +34,7 @@ def test_struct_layouts_match_header():
 
 def test_error_path_without_gpu():
     lib = _lib.lib()
-    assert lib.fns["edet_abi_version"]() == _lib.ABI_VERSION == 9
+    assert lib.fns["edet_abi_version"]() == _lib.ABI_VERSION == 10
     # argument validation happens before any HIP call
     rc = lib.fns["edet_conv1x1_fwd"](0, None, None, 8, None, 8, None, None, 8, 0, None, None)
     assert rc == -1 and "null" in lib.last_error()

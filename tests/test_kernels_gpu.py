@@ -4,6 +4,7 @@ fp32 storage must match to ~1e-5; bf16 storage to bf16 rounding (3e-2 relative o
 values).  Shapes include ragged sizes, odd spatial extents (TF SAME asymmetric padding),
 channel counts that are not tile multiples and 2-segment pyramids with padding rows.
 """
+import ctypes
 import math
 
 import numpy as np
@@ -775,6 +776,157 @@ def test_bifpn_fuse_stored_pool_taps(dt, pool_in):
     for a, b in zip(d0, d1):
         assert torch.equal(a, b)
     assert torch.allclose(w0, w1, rtol=1e-5, atol=1e-6)
+
+
+_FMODE = {"S": L.MODE_SAME, "U": L.MODE_UPSAMPLE, "P": L.MODE_MAXPOOL}
+
+
+def _fuse_node(rng, B, C, H, W, modes, act_in, pool_odd):
+    descs = []
+    for m in modes:
+        h, w = {"S": (H, W), "U": (H // 2, W // 2),
+                "P": (2 * H - 1, 2 * W - 1) if pool_odd else (2 * H, 2 * W)}[m]
+        pyr = Pyr(B, [(h, w)])
+        x = pyr_data(rng, pyr, C, "bf16", scale=2.0)
+        descs.append((LazyDesc(x, pyr, C, bn=make_bn(x, pyr, C, rng), act=act_in), pyr, h, w, _FMODE[m]))
+    return descs
+
+
+def _fuse_inputs(descs, taps, prefill, C=64):
+    fi = (L.FuseInput * len(descs))()
+    dxs = []
+    for i, (d, pyr, h, w, mode) in enumerate(descs):
+        fi[i].v, fi[i].H, fi[i].W, fi[i].mode = d.c, h, w, mode
+        dx = torch.full((pyr.rows, C), 0.5 if prefill[i] else 0.0, dtype=torch.bfloat16, device=DEV)
+        dxs.append(dx)
+        fi[i].dx, fi[i].accumulate = dx.data_ptr(), int(prefill[i])
+        fi[i].pool_arg = taps.data_ptr() if mode == L.MODE_MAXPOOL else None
+    return fi, dxs
+
+
+@pytest.mark.parametrize("modes,H,W,act_in,out_act,pool_odd", [
+    ("SU", 8, 8, 1, 1, False), ("SU", 64, 64, 0, 1, False), ("SSP", 8, 6, 1, 1, False),
+    ("SSP", 7, 5, 1, 0, True), ("SP", 16, 16, 1, 1, False), ("SP", 5, 3, 0, 1, True),
+    ("SSU", 32, 32, 1, 1, False), ("SSU", 4, 6, 1, 0, False), ("SS", 9, 7, 1, 1, False),
+    ("SS", 33, 31, 0, 0, False)])
+def test_bifpn_fuse_bwd_dv(modes, H, W, act_in, out_act, pool_odd):
+    """The one-pass fusion backward from d(value) (edet_bifpn_fuse_bwd_dv + edet_bifpn_fuse_fold,
+    ABI 10) against the two-pass one it replaces (d(raw) = dv * act'(F) formed here, then
+    edet_bifpn_fuse_bwd, whose own parity is test_bifpn_fuse) on the same forward and the same
+    recorded pool taps, and the weight gradient against the fp64 autograd of bifpn.py:59-66.
+    Covers every BiFPN input-mode combination, odd extents (partial output quads), odd max-pool
+    inputs, accumulation into an existing dx, and both output activations."""
+    rng = np.random.default_rng(H * 31 + W + len(modes))
+    B, C = 2, 64
+    n = len(modes)
+    descs = _fuse_node(rng, B, C, H, W, modes, act_in, pool_odd)
+    wv = g(torch.tensor([1.0, 0.7, 1.3][:n]))
+    taps = torch.full((B * H * W, C), 77, dtype=torch.uint8, device=DEV)
+    prefill = [i == 0 for i in range(n)]
+    fi, _ = _fuse_inputs(descs, taps, prefill)
+    out = torch.empty(B * H * W, C, dtype=torch.bfloat16, device=DEV)
+    L.call("edet_bifpn_fuse_fwd", L.BF16, n, fi, vp(wv), B, H, W, C, vp(out), stream())
+    dv = g(rnd(rng, B * H * W, C), "bf16")
+    F = out.float()
+    dF = (dv.float() * (torch.sigmoid(F) * (1 + F * (1 - torch.sigmoid(F)))) if out_act else dv.float())
+    # two-pass reference path
+    fa, dxa = _fuse_inputs(descs, taps, prefill)
+    dwa = zeros(n)
+    L.call("edet_bifpn_fuse_bwd", L.BF16, n, fa, vp(wv), B, H, W, C, vp(out), vp(dF.to(torch.bfloat16)),
+           vp(dwa), stream())
+    # one pass
+    fb, dxb = _fuse_inputs(descs, taps, prefill)
+    nparts = ctypes.c_int(-1)
+    L.call("edet_bifpn_fuse_bwd_dv_parts", L.BF16, n, fb, B, H, W, C, ctypes.byref(nparts))
+    assert nparts.value > 0
+    part = torch.full((nparts.value * 4,), float("nan"), dtype=torch.float32, device=DEV)
+    L.call("edet_bifpn_fuse_bwd_dv", L.BF16, n, fb, vp(wv), B, H, W, C, vp(out), vp(dv), out_act, vp(part),
+           nparts.value, stream())
+    dwb = g(torch.full((n,), 0.25))
+    item = (L.FuseFold * 1)()
+    item[0].part, item[0].w, item[0].dw, item[0].nparts, item[0].n_in = part.data_ptr(), wv.data_ptr(), \
+        dwb.data_ptr(), nparts.value, n
+    L.call("edet_bifpn_fuse_fold", 1, item, stream())
+    torch.cuda.synchronize()
+    for a, b in zip(dxa, dxb):
+        close(b, a, "bf16", rtol=2e-2, atol=2e-2)
+    # weight gradient: fp64 autograd over the stored inputs with the kernel's own pool taps
+    wr = wv.double().cpu().requires_grad_(True)
+    den = wr.sum() + 1e-4
+    vs = [d.cpu_value() for d, *_ in descs]
+    Fr = 0
+    tcpu = taps.long().cpu()
+    for i, (d, pyr, h, w, mode) in enumerate(descs):
+        v = vs[i].view(B, h, w, C)
+        if mode == L.MODE_SAME:
+            r = v
+        elif mode == L.MODE_UPSAMPLE:
+            r = v[:, torch.arange(H) // 2][:, :, torch.arange(W) // 2]
+        else:
+            pt, pl = max((H - 1) * 2 + 3 - h, 0) // 2, max((W - 1) * 2 + 3 - w, 0) // 2
+            t = tcpu.view(B, H, W, C)
+            iy = (torch.arange(H).view(1, H, 1, 1) * 2 - pt + t // 3).clamp(0, h - 1)
+            ix = (torch.arange(W).view(1, 1, W, 1) * 2 - pl + t % 3).clamp(0, w - 1)
+            bi = torch.arange(B).view(B, 1, 1, 1).expand(B, H, W, C)
+            ci = torch.arange(C).view(1, 1, 1, C).expand(B, H, W, C)
+            r = v[bi, iy, ix, ci]
+        Fr = Fr + r.reshape(-1, C) * wr[i] / den
+    Fd = Fr.detach()
+    dFr = dv.double().cpu() * ((torch.sigmoid(Fd) * (1 + Fd * (1 - torch.sigmoid(Fd)))) if out_act else 1.0)
+    (Fr * dFr).sum().backward()
+    close(dwb - 0.25, wr.grad, "bf16", scale=30)
+    close(dwb - 0.25, dwa, "bf16", scale=30)
+
+
+def test_bifpn_fuse_fold_many_items():
+    """edet_bifpn_fuse_fold over more items than one launch takes (EDET_FUSE_FOLD_MAX): every
+    node's records summed in fp64 and divided by its (sum w + 1e-4), added into dw."""
+    rng = np.random.default_rng(5)
+    n_items = L.FUSE_FOLD_MAX + 9
+    arr = (L.FuseFold * n_items)()
+    keep, expect = [], []
+    for k in range(n_items):
+        n_in = 2 + k % 2
+        nparts = int(rng.integers(1, 700))
+        p = rng.standard_normal((nparts, 4)).astype(np.float32)
+        w = rng.uniform(0.1, 2.0, n_in).astype(np.float32)
+        pt, wt, dw = g(torch.tensor(p.reshape(-1))), g(torch.tensor(w)), g(torch.full((n_in,), 1.0))
+        keep += [pt, wt, dw]
+        arr[k].part, arr[k].w, arr[k].dw, arr[k].nparts, arr[k].n_in = pt.data_ptr(), wt.data_ptr(), \
+            dw.data_ptr(), nparts, n_in
+        den = float(np.float32(w.sum(dtype=np.float32) + np.float32(1e-4)))
+        expect.append((dw, 1.0 + p[:, :n_in].astype(np.float64).sum(0) / den))
+    L.call("edet_bifpn_fuse_fold", n_items, arr, stream())
+    torch.cuda.synchronize()
+    for dw, e in expect:
+        np.testing.assert_allclose(dw.cpu().numpy(), e, rtol=1e-5, atol=1e-5)
+
+
+def test_bifpn_fuse_bwd_dv_coverage():
+    """edet_bifpn_fuse_bwd_dv_parts reports 0 (caller falls back) for fp32, a max-pooled input
+    without recorded taps and an upsample that is not exactly x2; the launch refuses them."""
+    B, C, H, W = 2, 64, 8, 8
+    x = torch.zeros(B * 16 * 16, C, dtype=torch.bfloat16, device=DEV)
+    fi = (L.FuseInput * 2)()
+    for i, (h, w, mode) in enumerate([(H, W, L.MODE_SAME), (2 * H, 2 * W, L.MODE_MAXPOOL)]):
+        fi[i].v.x, fi[i].v.ld, fi[i].H, fi[i].W, fi[i].mode = x.data_ptr(), C, h, w, mode
+        fi[i].dx = x.data_ptr()
+    nparts = ctypes.c_int(-1)
+    L.call("edet_bifpn_fuse_bwd_dv_parts", L.BF16, 2, fi, B, H, W, C, ctypes.byref(nparts))
+    assert nparts.value == 0  # no pool taps
+    fi[1].pool_arg = x.data_ptr()
+    L.call("edet_bifpn_fuse_bwd_dv_parts", L.BF16, 2, fi, B, H, W, C, ctypes.byref(nparts))
+    assert nparts.value > 0
+    L.call("edet_bifpn_fuse_bwd_dv_parts", L.F32, 2, fi, B, H, W, C, ctypes.byref(nparts))
+    assert nparts.value == 0
+    fi[1].H, fi[1].W, fi[1].mode, fi[1].pool_arg = 3, 3, L.MODE_UPSAMPLE, None  # 3 -> 8 is not x2
+    L.call("edet_bifpn_fuse_bwd_dv_parts", L.BF16, 2, fi, B, H, W, C, ctypes.byref(nparts))
+    assert nparts.value == 0
+    wv = g(torch.tensor([1.0, 1.0]))
+    part = torch.zeros(64, dtype=torch.float32, device=DEV)
+    with pytest.raises(L.EdetError, match="not covered"):
+        L.call("edet_bifpn_fuse_bwd_dv", L.BF16, 2, fi, vp(wv), B, H, W, C, vp(x), vp(x), 1, vp(part), 16,
+               stream())
 
 
 @pytest.mark.parametrize("dt", DTS)
