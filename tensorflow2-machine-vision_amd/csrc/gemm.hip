@@ -33,6 +33,7 @@ struct GemmArgs {
   int accumulate, has_stats, ntm, ntn;
   double* se5;         // FOLD == 2: [5][se_batch][N] per-image SE / BN-backward sums (k_gate_bn_reduce's)
   int se_batch;
+  int ncs;             // k_gemm_s: column slices of 16 NF columns (0 / 1: one, the whole N)
 };
 
 // BN-backward fold (dgrad epilogues): the output y = d(value) of a lazy value v = act(bn(x)) is
@@ -172,6 +173,41 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   const int tm = t / g.ntn, tn = t - tm * g.ntn;
   const int row0 = tm * BM, col0 = tn * BN;
 
+  const T* A = (const T*)g.a;
+  const T* B = (const T*)g.b;
+  struct Chunk {
+    V ra[AV][VW], rb[BV][VW];
+  };
+  // global -> registers (raw), branch-free: an element outside the operand reads zeros
+  // (buf_ld16).  Loads under branches left the compiler's wait-count merge pessimistic: every
+  // commit waited for the chunks in flight behind it (s_waitcnt vmcnt(0)).
+  // (range-checked loads over the block's A rows / B rows: rows past M or N read zeros, a
+  // chunk column past K takes an out-of-range offset)
+  const auto ra_ = buf_rsrc(A + (size_t)row0 * g.lda, (long)min(BM, g.M - row0) * g.lda * (long)sizeof(T));
+  const auto rb_ = buf_rsrc(B + (size_t)col0 * g.ldb, (long)min(BN, g.N - col0) * g.ldb * (long)sizeof(T));
+  auto fetch = [&](Chunk& R, int k0) {
+#pragma unroll
+    for (int u = 0; u < AV; ++u) {
+      const int v = tid + u * 256;
+      const int r = v / KV, kv = (v % KV) * 8;
+      const uint32_t off = buf_off(v < BM * KV && k0 + kv < g.K, (uint32_t)((r * g.lda + k0 + kv) * (int)sizeof(T)));
+#pragma unroll
+      for (int w = 0; w < VW; ++w) R.ra[u][w] = __builtin_bit_cast(V, buf_ld16(ra_, off + 16 * w));
+    }
+#pragma unroll
+    for (int u = 0; u < BV; ++u) {
+      const int v = tid + u * 256;
+      const int n = v / KV, kv = (v % KV) * 8;
+      const uint32_t off = buf_off(v < BN * KV && k0 + kv < g.K, (uint32_t)((n * g.ldb + k0 + kv) * (int)sizeof(T)));
+#pragma unroll
+      for (int w = 0; w < VW; ++w) R.rb[u][w] = __builtin_bit_cast(V, buf_ld16(rb_, off + 16 * w));
+    }
+  };
+  // chunk 0 is requested before the per-block tables (lazy affine, gate rows, fold table) are
+  // built: its round trip overlaps theirs instead of following the barrier
+  Chunk R0, R1;
+  fetch(R0, 0);
+
   int seg = 0;
   if (LAZY || g.has_stats) seg = seg_of_row(g.pyr, row0);
   const int seg_off = g.pyr.row_off[seg];
@@ -200,8 +236,6 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   }
   __syncthreads();
 
-  const T* A = (const T*)g.a;
-  const T* B = (const T*)g.b;
   // FOLD: the folded value's x tile is requested here, its latency hidden by the whole K loop,
   // and parked in LDS next to the staged C tile after it
   constexpr int VPR = BN / 8;  // 8-element vectors per tile row
@@ -219,9 +253,6 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
       for (int w = 0; w < VW; ++w) xr[u][w] = ok ? src[w] : V{};
     }
   }
-  struct Chunk {
-    V ra[AV][VW], rb[BV][VW];
-  };
   // per-thread A rows are fixed across chunks: resolve their staged gate rows once
   int goff[AV];
 #pragma unroll
@@ -229,31 +260,6 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     const int grow = min(row0 + (tid + u * 256) / KV, g.M - 1);
     goff[u] = has_gate ? ((grow - seg_off) / hw - n_lo) * g.K : 0;
   }
-  // global -> registers (raw), branch-free: an element outside the operand reads zeros
-  // (buf_ld16).  Loads under branches left the compiler's wait-count merge pessimistic: every
-  // commit waited for the chunks in flight behind it (s_waitcnt vmcnt(0)).
-  // (range-checked loads over the block's A rows / B rows: rows past M or N read zeros, a
-  // chunk column past K takes an out-of-range offset)
-  const auto ra_ = buf_rsrc(A + (size_t)row0 * g.lda, (long)min(BM, g.M - row0) * g.lda * (long)sizeof(T));
-  const auto rb_ = buf_rsrc(B + (size_t)col0 * g.ldb, (long)min(BN, g.N - col0) * g.ldb * (long)sizeof(T));
-  auto fetch = [&](Chunk& R, int k0) {
-#pragma unroll
-    for (int u = 0; u < AV; ++u) {
-      const int v = tid + u * 256;
-      const int r = v / KV, kv = (v % KV) * 8;
-      const uint32_t off = buf_off(v < BM * KV && k0 + kv < g.K, (uint32_t)((r * g.lda + k0 + kv) * (int)sizeof(T)));
-#pragma unroll
-      for (int w = 0; w < VW; ++w) R.ra[u][w] = __builtin_bit_cast(V, buf_ld16(ra_, off + 16 * w));
-    }
-#pragma unroll
-    for (int u = 0; u < BV; ++u) {
-      const int v = tid + u * 256;
-      const int n = v / KV, kv = (v % KV) * 8;
-      const uint32_t off = buf_off(v < BN * KV && k0 + kv < g.K, (uint32_t)((n * g.ldb + k0 + kv) * (int)sizeof(T)));
-#pragma unroll
-      for (int w = 0; w < VW; ++w) R.rb[u][w] = __builtin_bit_cast(V, buf_ld16(rb_, off + 16 * w));
-    }
-  };
   // registers -> LDS buffer, lazy transform of A on the way: branch-free per element (the
   // activation and the gate are block-uniform choices, taken once around the whole chunk)
   auto lazy_a = [&](auto act_c, auto gate_c, const Chunk& R, int buf, int k0) {
@@ -322,8 +328,6 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   // Two register chunks in flight: chunk k+1 was fetched two iterations before its commit (one
   // chunk ahead left every 32-wide K step waiting a memory round trip behind a handful of MFMAs)
   const int nk = cdiv(g.K, KC);
-  Chunk R0, R1;
-  fetch(R0, 0);
   commit(R0, 0, 0);
   fetch(R0, KC);  // (past K: every element is outside, committed as zeros or not at all)
   fetch(R1, 2 * KC);
@@ -1812,7 +1816,13 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint16_t* cw = stg[wave];
   const int kq = 8 * (lane >> 4);  // this lane's 8 k values
-  const int K = g.K, N = g.N, M = g.M;
+  // column slices (g.ncs > 1, the wide expand convs): block = (row range, slice of 16 NF
+  // columns starting at nb0); every slice re-reads its rows' A (L2 hits: the slices of a row
+  // range are neighbouring blocks)
+  const int ncs = g.ncs > 1 ? g.ncs : 1;
+  const int cs = blockIdx.x % ncs, rb = blockIdx.x / ncs, nrb = gridDim.x / ncs;
+  const int nb0 = cs * NF * 16;
+  const int K = g.K, N = min(g.N - nb0, NF * 16), M = g.M;
   const T* A = (const T*)g.a;
   const T* Wt = (const T*)g.b;
   T* Y = (T*)g.c;
@@ -1824,21 +1834,30 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
     for (int f = 0; f < NF; ++f) {
       const int n = 16 * f + (lane & 15), k = 32 * ks + kq;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (n < N && k < K) v = *reinterpret_cast<const uint4*>(Wt + (size_t)n * g.ldb + k);
+      if (n < N && k < K) v = *reinterpret_cast<const uint4*>(Wt + (size_t)(nb0 + n) * g.ldb + k);
       wf[ks][f] = __builtin_bit_cast(bf16x8_t, v);
     }
   // bias in LDS (4 * NF registers per lane held it: at NF = 9 the difference between one and
   // two waves per SIMD)
   __shared__ __attribute__((aligned(16))) float bias_s[NF * 16];
-  for (int n = threadIdx.x; n < NF * 16; n += 256) bias_s[n] = (g.bias && n < N) ? g.bias[n] : 0.f;
-  float2 af[KS][8];
+  for (int n = threadIdx.x; n < NF * 16; n += 256) bias_s[n] = (g.bias && n < N) ? g.bias[nb0 + n] : 0.f;
+  // the lazy BN affine of this lane's k values: registers for KS <= 2, LDS beyond (KS * 16
+  // registers would cost the deep-K sliced forms their second wave per SIMD)
+  constexpr bool AFR = KS <= 2;
+  float2 af[AFR ? KS : 1][8];
+  __shared__ float2 af_s[AFR ? 1 : KS * 32];
   if constexpr (LAZY) {
     const float inv = 1.f / (float)M;
+    if constexpr (AFR) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
+      for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        af[ks][j] = 32 * ks + kq + j < K ? bn_affine(g.lz.bn, 0, 32 * ks + kq + j, inv) : make_float2(1.f, 0.f);
+        for (int j = 0; j < 8; ++j)
+          af[ks][j] = 32 * ks + kq + j < K ? bn_affine(g.lz.bn, 0, 32 * ks + kq + j, inv) : make_float2(1.f, 0.f);
+    } else {
+      for (int k = threadIdx.x; k < KS * 32; k += 256)
+        af_s[k] = k < K ? bn_affine(g.lz.bn, 0, k, inv) : make_float2(1.f, 0.f);
+    }
   }
   const int hw = g.pyr.H[0] * g.pyr.W[0];
   float ss[NF][4], sq[NF][4];
@@ -1851,7 +1870,7 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   if constexpr (FOLD) {
     const float inv = 1.f / (float)seg_rows(g.pyr, 0);
     for (int c = threadIdx.x; c < NF * 16; c += 256)
-      ftab[c] = c < N ? fold_table(g.fx.bn, 0, c, inv) : make_float4(0.f, 0.f, 0.f, 0.f);
+      ftab[c] = c < N ? fold_table(g.fx.bn, 0, nb0 + c, inv) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   int cur_seg = -1, seg_end = g.has_stats ? 0 : M;
   // lanes sharing (lane >> 4) hold the same 4 channels of 16 different rows
@@ -1876,8 +1895,8 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   // a block meets one pyramid level, rarely two: per-wave flushes and the block's fp64
   // atomics cover only the levels it touched (a grid-strided wave met a new level about once
   // per group and every block flushed all five)
-  const int ngroups = (M + 15) / 16, gpb = (ngroups + gridDim.x - 1) / gridDim.x;
-  const int g_begin = blockIdx.x * gpb, g_end = min(ngroups, g_begin + gpb);
+  const int ngroups = (M + 15) / 16, gpb = (ngroups + nrb - 1) / nrb;
+  const int g_begin = rb * gpb, g_end = min(ngroups, g_begin + gpb);
   // the next groups' A rows are fetched before this group's stores are issued (vmcnt
   // counts loads and stores in order: a load issued after the stores would wait for them)
   // FOLD: the folded value's raw x at this lane's output positions (row, 4 channels per
@@ -1888,9 +1907,12 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
   // the group come with its A rows (a gate load at the use waited for every load in flight).
   const auto rs_a = buf_rsrc(A + (size_t)g_begin * 16 * g.lda,
                              (long)(min(g_end * 16, M) - g_begin * 16) * g.lda * (long)sizeof(T));
-  const bool has_gate = LAZY && g.lz.gate != nullptr;
-  const auto rs_g = buf_rsrc(LAZY ? g.lz.gate : nullptr, has_gate ? (long)g.pyr.batch * K * 4 : 0);
-  constexpr int NG = LAZY ? KS : 1;
+  // (the SE-gated form for KS <= 2 only: its per-group gate vectors cost 16 KS registers; the
+  // host routes a gated A with a deeper K elsewhere)
+  constexpr bool GT = LAZY && KS <= 2;
+  const bool has_gate = GT && g.lz.gate != nullptr;
+  const auto rs_g = buf_rsrc(GT ? g.lz.gate : nullptr, has_gate ? (long)g.pyr.batch * K * 4 : 0);
+  constexpr int NG = GT ? KS : 1;
   auto fetch = [&](int grp, uint4* v, float4 (*gv)[2], uint2* xv) {
     const int rl = (grp - g_begin) * 16 + (lane & 15), row = grp * 16 + (lane & 15);
     const bool gok = grp < g_end;
@@ -1899,7 +1921,7 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
       const int k = 32 * ks + kq;
       const uint32_t off = buf_off(k < K && gok, (uint32_t)((rl * g.lda + k) * (int)sizeof(T)));
       v[ks] = buf_ld16(rs_a, off);
-      if constexpr (LAZY) {
+      if constexpr (GT) {
         const uint32_t go = buf_off(k < K && gok && row < M, (uint32_t)(((row / hw) * K + k) * 4));
         gv[ks][0] = __builtin_bit_cast(float4, buf_ld16(rs_g, go));
         gv[ks][1] = __builtin_bit_cast(float4, buf_ld16(rs_g, go + 16));
@@ -1910,7 +1932,7 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
       for (int f = 0; f < NF; ++f) {
         const int n0 = 16 * f + 4 * (lane >> 4);
         const bool ok = n0 < N && grp < g_end && row < M;
-        const uint2 t = *reinterpret_cast<const uint2*>(X + (ok ? (size_t)row * g.fx.ld + n0 : 0));
+        const uint2 t = *reinterpret_cast<const uint2*>(X + (ok ? (size_t)row * g.fx.ld + nb0 + n0 : 0));
         xv[f] = ok ? t : make_uint2(0, 0);
       }
     }
@@ -1945,12 +1967,14 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
           x[2 * i] = __uint_as_float(w4[i] << 16);
           x[2 * i + 1] = __uint_as_float(w4[i] & 0xffff0000u);
         }
-        const float gt[8] = {pg[ks][0].x, pg[ks][0].y, pg[ks][0].z, pg[ks][0].w,
-                             pg[ks][1].x, pg[ks][1].y, pg[ks][1].z, pg[ks][1].w};
+        const int kg = GT ? ks : 0;
+        const float gt[8] = {pg[kg][0].x, pg[kg][0].y, pg[kg][0].z, pg[kg][0].w,
+                             pg[kg][1].x, pg[kg][1].y, pg[kg][1].z, pg[kg][1].w};
         uint16_t o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float u = x[j] * af[ks][j].x + af[ks][j].y;
+          const float2 a = AFR ? af[AFR ? ks : 0][j] : af_s[32 * ks + kq + j];
+          float u = x[j] * a.x + a.y;
           if constexpr (ACT == 1) u = swishf_(u);
           if (has_gate) u *= gt[j];
           o[j] = k0 + j < K ? f2bf(u) : (uint16_t)0;
@@ -2000,7 +2024,7 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
       const int e = lane + 64 * i;
       const int rl = e / vpr, c8 = (e - rl * vpr) * 8;
       if (e < 16 * vpr && row0 + rl < M)
-        *reinterpret_cast<uint4*>(Y + (size_t)(row0 + rl) * g.ldc + c8) = *reinterpret_cast<const uint4*>(cw + rl * LDW + c8);
+        *reinterpret_cast<uint4*>(Y + (size_t)(row0 + rl) * g.ldc + nb0 + c8) = *reinterpret_cast<const uint4*>(cw + rl * LDW + c8);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -2027,8 +2051,8 @@ __global__ __launch_bounds__(256) void k_gemm_s(GemmArgs g) {
     for (int n = threadIdx.x; n < N; n += 256) {
       const float a = (red[sg][0][0][n] + red[sg][0][1][n]) + (red[sg][0][2][n] + red[sg][0][3][n]);
       const float b = (red[sg][1][0][n] + red[sg][1][1][n]) + (red[sg][1][2][n] + red[sg][1][3][n]);
-      stat_put(g.stats.sum[sg], n, (double)a);
-      stat_put(g.stats.sq[sg], n, (double)b);
+      stat_put(g.stats.sum[sg], nb0 + n, (double)a);
+      stat_put(g.stats.sq[sg], nb0 + n, (double)b);
     }
 }
 
@@ -2042,7 +2066,9 @@ static int launch_gemm_s(const GemmArgs& g, hipStream_t s) {
   if (g.has_stats && g.N <= 64 && g.K >= 64 && g.M <= 262144) cap = 256;
   else if (g.M >= (1 << 21)) cap = 1024;
   if (dev_knob(7) > 0) cap = dev_knob(7);
-  const int grid = std::max(1, std::min(cdiv(ngroups, 4), cap));
+  if (g.ncs > 1 && dev_knob(61) > 0) cap = dev_knob(61);
+  const int ncs = g.ncs > 1 ? g.ncs : 1;
+  const int grid = std::max(1, std::min(cdiv(ngroups, 4), std::max(1, cap / ncs))) * ncs;
   if constexpr (LAZY) {
     if (g.lz.act) EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY, FOLD, 1>), dim3(grid), dim3(256), 0, s, g);
     else EDET_LAUNCH((k_gemm_s<T, NF, KS, LAZY, FOLD, 0>), dim3(grid), dim3(256), 0, s, g);
@@ -2117,6 +2143,44 @@ static int dispatch_gemm_s(const GemmArgs& g, hipStream_t s, bool& done) {
     }
   }
   return EDET_OK;
+}
+
+// Column-sliced wave streaming for the wide expand convs (K <= 192 into N > 160: 32768 x 112 ->
+// 672, 8192 x 192 -> 1152, 131072 x 40 -> 240, 32768 x 80 -> 480).  The K-loop tiles ran these
+// write-heavy products at 0.9-1.8 TB/s: each 64 x 128 tile block lived through a short K loop
+// and its own epilogue, one round trip after another.  Here a wave keeps 16 NF columns of W in
+// registers and streams its row groups (the A rows are re-read per slice, from L2).
+// Development slot 59: 1 = wherever it applies, 2 = never; slot 60: NF; slot 61: blocks.
+template <typename T, bool LAZY>
+static int dispatch_gemm_s_sliced(GemmArgs g, hipStream_t s, bool& done) {
+  done = false;
+  const int route = dev_knob(59);
+  if (route == 2 || sizeof(T) != 2) return EDET_OK;
+  if (g.K % 8 || g.N % 8 || g.accumulate || g.ldc % 8 || g.lda % 8 || g.ldb % 8 || g.K > 192 || g.N <= 160)
+    return EDET_OK;
+  if (LAZY && (g.pyr.nseg != 1 || (g.lz.gate != nullptr && g.K > 64))) return EDET_OK;
+  // Not a production route: in isolated replays a lazy A with K <= 128 over >= 32768 rows gained
+  // (kbench r06q / r06r: 131072 x 40 -> 240 43.0 -> 35.5 us, 32768 x 112 -> 672 36.8 -> 33.6,
+  // 32768 x 80 -> 480 24.7 -> 23.5; the 8192-row K = 192 expand lost, 24.1 -> 37.6), but the
+  // same-box whole-step A/B did not move (12.074 vs 12.073 ms, profiles/r06/r06r_*): kept
+  // behind slot 59 for the next study of these write-heavy products
+  if (route != 1) return EDET_OK;
+  const int KS = cdiv(g.K, 32);
+  const int nf = dev_knob(60) > 0 ? dev_knob(60) : (KS <= 4 ? 4 : 2);
+  g.ncs = cdiv(g.N, 16 * nf);
+  done = true;
+  auto go = [&](auto ks_c) -> int {
+    constexpr int KSC = decltype(ks_c)::value;
+    return nf == 2 ? launch_gemm_s<T, LAZY, 2, KSC>(g, s) : launch_gemm_s<T, LAZY, 4, KSC>(g, s);
+  };
+  switch (KS) {
+    case 1: return go(std::integral_constant<int, 1>{});
+    case 2: return go(std::integral_constant<int, 2>{});
+    case 3: return go(std::integral_constant<int, 3>{});
+    case 4: return go(std::integral_constant<int, 4>{});
+    case 5: return go(std::integral_constant<int, 5>{});
+    default: return go(std::integral_constant<int, 6>{});
+  }
 }
 
 // ------------------------------------------------------------------ launch helpers
@@ -2302,6 +2366,11 @@ static int dispatch_gemm(GemmArgs g, hipStream_t s) {
   // with K > 64 into 192 < N <= 320 (D4 32768 x 160 -> 224: 95 -> 59 us); the A-resident form
   // wins K = 224 into N >= 192 with statistics at M <= 8192 (8192 x 224 -> 224: 33 -> 24 us);
   // the B-resident form wins the D0 class predict (174592 x 64 -> 729: 114 -> 93 us)
+  {
+    bool done = false;
+    const int rc = dispatch_gemm_s_sliced<T, LAZY>(g, s, done);
+    if (done || rc) return rc;
+  }
   if constexpr (sizeof(T) == 2) {
     // Round-5 K-loop tile sweep over the mid-size D0 products (8192 / 32768 rows: the 16^2 and
     // 32^2 stages, 0.4-1.6 TB/s; tools/gpu_r05l.sh, profiles/r05/r05l_gemm_tiles.txt): 64-column

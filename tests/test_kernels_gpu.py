@@ -55,7 +55,12 @@ def pyr_data(rng, pyr, C, dt, scale=1.0):
                                             # rows), lazy into N > 320 64 x 128, lazy with
                                             # statistics into 64 columns 64 x 64 / 128 x 64
                                             (8192, 1152, 192, 0, 1), (32768, 480, 112, 0, 1),
-                                            (8192, 192, 1152, 1, 1), (8192, 320, 64, 3, 1), (32768, 112, 64, 2, 1)])
+                                            (8192, 192, 1152, 1, 1), (8192, 320, 64, 3, 1), (32768, 112, 64, 2, 1),
+                                            # round 6: the column-sliced wave-streaming form (lazy A,
+                                            # K <= 128 into N > 160 over >= 32768 rows; a gated
+                                            # K > 64 stays on the K loop)
+                                            (32768, 112, 672, 3, 1), (32768, 40, 240, 2, 1), (32768, 80, 480, 1, 1),
+                                            (32768, 24, 168, 1, 1)])
 def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
     """conv1x1 forward with BN statistics (and without them for plain inputs: the stats-free
     route) against fp64."""
