@@ -172,6 +172,15 @@ int edet_memcpy_async(void* dst, const void* src, size_t bytes, edet_stream_t st
  * kernels that may use it are queued; NULL unregisters (atomics fallback).  Not thread-safe:
  * one registered workspace per process. */
 int edet_set_workspace(void* ptr, size_t bytes);
+/* ABI 10: deferred split sums.  Between edet_partials_defer and edet_partials_flush, every
+ * weight-gradient split reduction (1x1 wgrad partials, wave-streaming wgrad, stem wgrad) writes
+ * its partials into a fresh region of `arena` (256-B aligned bump allocation) and its fixed-order
+ * sum into dW / db is recorded instead of launched; edet_partials_flush launches every recorded
+ * sum (one launch per 40 jobs) and closes the window.  The gradients those sums complete must not
+ * be read before the flush.  A region that does not fit falls back to the ordinary workspace and
+ * an immediate sum; *needed (nullable) receives the arena size the window would have used. */
+int edet_partials_defer(void* arena, size_t bytes);
+int edet_partials_flush(size_t* needed, edet_stream_t stream);
 /* launch-duration probe (measurement): end = 0 stores the wall clock in slot[0]; end = 1 adds
  * (now - slot[0]) to slot[1] and 1 to slot[2].  Capturable in HIP graphs. */
 int edet_probe(uint64_t* slot, int end, edet_stream_t stream);

@@ -134,6 +134,8 @@ SIGNATURES = {
     "edet_memset_async": [P, c_int, c_size_t, P],
     "edet_memcpy_async": [P, P, c_size_t, P],
     "edet_set_workspace": [P, c_size_t],
+    "edet_partials_defer": [P, c_size_t],
+    "edet_partials_flush": [POINTER(c_size_t), P],
     "edet_probe": [P, c_int, P],
     "edet_wall_clock_khz": [P],
     "edet_launched_kernels": [c_char_p, c_size_t],

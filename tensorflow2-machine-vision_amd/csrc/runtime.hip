@@ -4,6 +4,9 @@
 #include <stdio.h>
 #include "common.hpp"
 
+#include <algorithm>
+#include <vector>
+
 namespace edet {
 
 static thread_local char g_err[512] = "";
@@ -42,7 +45,37 @@ int dev_knob(int slot) { return (slot >= 0 && slot < 64) ? g_dev[slot] : 0; }
 // allocates nothing; without a (large enough) workspace the kernels fall back to atomics.
 static void* g_ws = nullptr;
 static size_t g_ws_bytes = 0;
+
+// Deferred split sums (ABI 10, edet_partials_defer / edet_partials_flush): inside a deferral
+// window every split reduction takes a fresh region of the caller's deferral arena and its sum is
+// recorded instead of launched; the flush sums every recorded job in one launch.  The weight
+// gradients are read by nothing before the optimizer, and the D0 backward's 28 sum launches
+// (~4.7 us each, mostly launch and drain) become one.  A region that does not fit falls back to
+// the ordinary workspace and an immediate sum.
+struct PartJob {
+  const float* part;
+  float* out;
+  float* out2;
+  long n, n2;
+  int S, nblk;  // nblk: blocks of this job in the flush grid (x chunks)
+  int atomic;   // another job adds into the same output: fp32 atomics
+};
+constexpr int PJ_MAX = 40;  // jobs per flush launch (kernel arguments)
+static char* g_def = nullptr;
+static size_t g_def_bytes = 0, g_def_used = 0, g_def_hw = 0;
+static std::vector<PartJob> g_jobs;
+
 float* workspace_f32(size_t n_floats) {
+  if (g_def) {
+    const size_t bytes = (n_floats * sizeof(float) + 255) & ~(size_t)255;
+    if (g_def_used + bytes <= g_def_bytes) {
+      float* p = (float*)(g_def + g_def_used);
+      g_def_used += bytes;
+      g_def_hw = std::max(g_def_hw, g_def_used);
+      return p;
+    }
+    g_def_hw = std::max(g_def_hw, g_def_used + bytes);  // (reported: the arena the caller should give)
+  }
   return (g_ws && n_floats * sizeof(float) <= g_ws_bytes) ? (float*)g_ws : nullptr;
 }
 
@@ -76,9 +109,53 @@ __global__ __launch_bounds__(256) void k_sum_partials(const float* part, int S, 
   else atomicAdd(out + i, t);
 }
 
+constexpr int SUM_CHUNK_DEF = SUM_CHUNK;
+struct PartJobs {
+  PartJob j[PJ_MAX];
+  int n;
+};
+// the recorded sums, one launch: block b belongs to the job whose block range holds it (a scan
+// over at most PJ_MAX kernel-argument entries), then k_sum_partials' loop
+__global__ __launch_bounds__(256) void k_sum_partials_jobs(PartJobs a) {
+  int b = blockIdx.x, j = 0;
+  while (j < a.n - 1 && b >= a.j[j].nblk) b -= a.j[j++].nblk;
+  const PartJob& J = a.j[j];
+  const long nt = J.n + J.n2;
+  const long bx = (nt + 255) / 256;
+  const int chunk = (int)(b / bx);
+  long i = (b - (long)chunk * bx) * 256 + threadIdx.x;
+  if (i >= nt) return;
+  const float* part = J.part;
+  float* out = J.out;
+  long n = J.n;
+  if (i >= n) {
+    part += (size_t)J.S * n;
+    i -= n;
+    n = J.n2;
+    out = J.out2;
+  }
+  const int s0 = chunk * SUM_CHUNK_DEF, s1 = min(J.S, s0 + SUM_CHUNK_DEF);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int s = s0;
+  for (; s + 8 <= s1; s += 8)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += part[(size_t)(s + u) * n + i];
+  for (; s < s1; ++s) acc[0] += part[(size_t)s * n + i];
+  const float t = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  if (!J.atomic && J.nblk == bx) out[i] += t;
+  else atomicAdd(out + i, t);
+}
+
 int sum_partials(const float* part, int S, long n, float* out, hipStream_t st, long n2, float* out2) {
   if (!out2) n2 = 0;
   if (n + n2 <= 0) return EDET_OK;
+  if (g_def && (const char*)part >= g_def && (const char*)part < g_def + g_def_bytes) {
+    PartJob j{};
+    j.part = part; j.out = out; j.out2 = out2; j.n = n; j.n2 = n2; j.S = S;
+    j.nblk = (int)(((n + n2 + 255) / 256) * ((S + SUM_CHUNK - 1) / SUM_CHUNK));
+    g_jobs.push_back(j);
+    return EDET_OK;
+  }
   const unsigned chunks = (unsigned)((S + SUM_CHUNK - 1) / SUM_CHUNK);
   EDET_LAUNCH(k_sum_partials, dim3((unsigned)((n + n2 + 255) / 256), chunks), dim3(256), 0, st, part, S, n, out, n2,
               out2);
@@ -135,6 +212,44 @@ int edet_dev_set(int slot, int value) {
   edet::set_error("edet_dev_set: development slots exist only in the EDET_DEV build (make dev)");
   return EDET_EUNSUPPORTED;
 #endif
+}
+
+int edet_partials_defer(void* arena, size_t bytes) {
+  EDET_REQUIRE(arena && bytes > 0, "partials_defer: null arena");
+  EDET_REQUIRE(!edet::g_def, "partials_defer: a deferral window is already open (edet_partials_flush first)");
+  edet::g_def = (char*)arena;
+  edet::g_def_bytes = bytes;
+  edet::g_def_used = 0;
+  edet::g_def_hw = 0;
+  edet::g_jobs.clear();
+  return EDET_OK;
+}
+
+int edet_partials_flush(size_t* needed, edet_stream_t stream) {
+  EDET_REQUIRE(edet::g_def, "partials_flush: no deferral window open");
+  using namespace edet;
+  if (needed) *needed = g_def_hw;
+  // outputs two jobs add into take atomics (the flush blocks of different jobs run concurrently)
+  for (size_t a = 0; a < g_jobs.size(); ++a)
+    for (size_t b = 0; b < g_jobs.size(); ++b)
+      if (a != b && (g_jobs[a].out == g_jobs[b].out || (g_jobs[a].out2 && g_jobs[a].out2 == g_jobs[b].out2)))
+        g_jobs[a].atomic = 1;
+  int rc = EDET_OK;
+  for (size_t j0 = 0; j0 < g_jobs.size() && rc == EDET_OK; j0 += PJ_MAX) {
+    PartJobs a{};
+    a.n = (int)std::min(g_jobs.size() - j0, (size_t)PJ_MAX);
+    long nb = 0;
+    for (int i = 0; i < a.n; ++i) {
+      a.j[i] = g_jobs[j0 + i];
+      nb += a.j[i].nblk;
+    }
+    EDET_LAUNCH(k_sum_partials_jobs, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, a);
+    rc = check_launch("edet partials_flush");
+  }
+  g_jobs.clear();
+  g_def = nullptr;
+  g_def_bytes = g_def_used = 0;
+  return rc;
 }
 
 int edet_set_workspace(void* ptr, size_t bytes) {

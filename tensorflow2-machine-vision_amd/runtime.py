@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -452,16 +453,30 @@ class Tape:
 
     def backward(self):
         entries, self.entries = self.entries, []
-        for fn in reversed(entries):
-            fn()
-        finals, self.finals = self.finals, {}
-        for fn, items in finals.values():
-            fn(items)
-        self.g.clear()
-        self.eng.join_side()
+        # the weight-gradient split sums are deferred to one launch after the last closure
+        # (edet_partials_defer / _flush): nothing reads a weight gradient before the optimizer
+        arena = self.eng.partials_arena()
+        if arena is not None:
+            L.call("edet_partials_defer", _vp(arena), arena.numel())
+        try:
+            for fn in reversed(entries):
+                fn()
+            finals, self.finals = self.finals, {}
+            for fn, items in finals.values():
+                fn(items)
+            self.g.clear()
+            self.eng.join_side()
+        finally:
+            if arena is not None:
+                need = ctypes.c_size_t(0)
+                L.call("edet_partials_flush", ctypes.byref(need), stream())
+                self.eng.note_partials(need.value)
 
 
 # --------------------------------------------------------------------------- engine
+# EDET_DEFER_PARTIALS=0: every weight-gradient split sum launched right after its kernel (the
+# round-5 behaviour), for same-box A/B
+DEFER_PARTIALS = os.environ.get("EDET_DEFER_PARTIALS", "1") != "0"
 _WORKSPACE = {}
 WORKSPACE_BYTES = 64 << 20
 
@@ -514,6 +529,24 @@ class Engine:
         self._side = None
         self._side_used = False
         self._side_keep: list = []
+        self._parts: Optional[torch.Tensor] = None
+        self._parts_need = 256 << 20
+
+    def partials_arena(self) -> Optional[torch.Tensor]:
+        """Arena of the deferred weight-gradient split partials (edet_partials_defer), sized by
+        the previous backward's need (256 MB to start; D0 B = 32 uses ~0.1 GB).  None: deferral
+        off (EDET_DEFER_PARTIALS=0, or a library without it)."""
+        if not DEFER_PARTIALS or self.device.type != "cuda" or not L.has("edet_partials_defer"):
+            return None
+        if self._parts is None or self._parts.numel() < self._parts_need:
+            self._parts = torch.empty(self._parts_need, dtype=torch.uint8, device=self.device)
+        return self._parts
+
+    def note_partials(self, needed: int):
+        """The arena a backward would have used: grow for the next one (this one fell back to
+        immediate sums past the arena's end)."""
+        if needed > self._parts_need:
+            self._parts_need = round_up(int(needed * 1.25), 1 << 20)
 
     def empty(self, rows: int, C: int, dtype=None) -> torch.Tensor:
         return torch.empty((rows, C), dtype=dtype or self.tdtype, device=self.device)

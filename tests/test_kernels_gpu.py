@@ -203,6 +203,52 @@ def test_conv1x1_wgrad(dt, K, N, lazy, nseg):
     close(db, refb, dt, scale=pyr.rows ** 0.5 * 2)
 
 
+@pytest.mark.parametrize("arena_mb", [256, 1])
+def test_partials_deferred_flush(arena_mb):
+    """edet_partials_defer / edet_partials_flush (ABI 10): the weight-gradient split sums of a
+    backward recorded and launched once give the immediate sums (to the order of the fp32
+    atomics that add chunk sums, and of two jobs adding into the same dW: a weight used twice)
+    for the 1x1 split partials (one 64 x 64 tile over a long M),
+    the wave-streaming form (2M x 16 -> 96) and the stem.  A 1 MB arena overflows: the calls
+    that do not fit sum immediately and the flush reports the arena they needed."""
+    rng = np.random.default_rng(3)
+    M = 1 << 21
+    jobs = []
+    for (m, K, N) in [(174592, 64, 64), (M, 16, 96), (174592, 64, 64)]:
+        pyr = Pyr(1, [(m, 1)])
+        jobs.append((pyr, K, N, g(rnd(rng, m, K), "bf16"), g(rnd(rng, m, N), "bf16")))
+    xs = g(rnd(rng, 4 * 64 * 64, 3), "bf16")
+    dys = g(rnd(rng, 4 * 32 * 32, 32), "bf16")
+
+    def run(defer):
+        outs = [zeros(N, K) for (_, K, N, _, _) in jobs[:2]]
+        dbs = [zeros(N) for (_, K, N, _, _) in jobs[:2]]
+        dstem = zeros(27 * 32)
+        arena = torch.empty(arena_mb << 20, dtype=torch.uint8, device=DEV)
+        if defer:
+            L.call("edet_partials_defer", vp(arena), arena.numel())
+        for i, (pyr, K, N, x, dy) in enumerate(jobs):
+            o = 0 if i == 2 else i  # the third adds into the first's dW / db
+            L.call("edet_conv1x1_wgrad", L.BF16, LazyDesc(x, pyr, K).c, pyr.c, K, vp(dy), N, N, vp(outs[o]),
+                   vp(dbs[o]), stream())
+        L.call("edet_stem_wgrad", L.BF16, vp(xs), 4, 64, 64, vp(dys), 32, vp(dstem), stream())
+        need = ctypes.c_size_t(0)
+        if defer:
+            L.call("edet_partials_flush", ctypes.byref(need), stream())
+        torch.cuda.synchronize()
+        return outs, dbs, dstem, need.value
+
+    (o0, b0, s0, _), (o1, b1, s1, need) = run(False), run(True)
+    # (sums of more than 32 splits add their chunk sums with fp32 atomics in both paths)
+    for a, b in zip(o1 + b1 + [s1], o0 + b0 + [s0]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-3)
+    assert need > 0
+    if arena_mb == 1:
+        assert need > (1 << 20)
+    with pytest.raises(L.EdetError, match="no deferral window"):
+        L.call("edet_partials_flush", None, stream())
+
+
 # ----------------------------------------------------------------- depthwise
 def dw_ref(v, pyr_in, k, s, w):  # v: fp64 [rows, C] values; returns [rows_out, C]
     outs = []
