@@ -131,7 +131,9 @@ def algorithmic_bytes(name, args, es):
     if name == "edet_maxpool_bwd":  # (dtype, lz, B, H, W, C, dy, dx, acc, s)
         B, H, W, C, acc = args[2], args[3], args[4], args[5], args[8]
         return B * (H * W * (2 + acc) + ((H + 1) // 2) * ((W + 1) // 2)) * C * es
-    if name in ("edet_bifpn_fuse_fwd", "edet_bifpn_fuse_bwd"):  # (dtype, n, fi, w, B, H, W, C, ...)
+    # (dtype, n, fi, w, B, H, W, C, ...); the one-pass backward (_dv, ABI 10) reads the raw F and
+    # the value gradient where the two-pass form read y and dF: the same bytes
+    if name in ("edet_bifpn_fuse_fwd", "edet_bifpn_fuse_bwd", "edet_bifpn_fuse_bwd_dv"):
         n, fi, B, H, W, C = args[1], obj(args[2]), args[4], args[5], args[6], args[7]
         ins = sum(B * fi[i].H * fi[i].W for i in range(n)) * C * es
         out = B * H * W * C * es

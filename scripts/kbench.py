@@ -52,6 +52,10 @@ def main():
     model = EfficientDetNetTrain(efficientnet_b0_blocks(), cfg, anchors, dtype="bf16", device=dev, seed=0,
                                  lr_schedule={"warmup_steps": 100, "total_steps": 10000})
     model.eng.overlap = False  # isolated replays
+    # every weight-gradient call replayed with its own split sum: a deferral window
+    # (edet_partials_defer) would record one sum per replay and flush them all at the end
+    from tf2mv_amd import runtime as R
+    R.DEFER_PARTIALS = False
     x, t = bench.synthetic_batch(anchors, B, S, 1000, dev, model.eng.tdtype)
     model.train_step((x, t))
     torch.cuda.synchronize()
