@@ -877,15 +877,19 @@ int edet_lazy_bwd_reduce(int dtype, const edet_lazy* x, const edet_pyramid* p, i
   // Round 3 (profiles/r03ad_bn_plan_sweep.txt): short rows want shorter chunks, 8 passes for
   // C <= 64 and 16 for C >= 144 at M <= 8192 (8192 x 192: 36.2 -> 29.9 us per step, the BiFPN
   // 2048 x 64: 43.3 -> 37.1), and the narrow C <= 24 tensors 256 blocks (2M x 16: 31.5 -> 28.0)
+  // Round 6 (replicated statistics, profiles/r06/r06v_plan_resweep.txt): the single tensors up to
+  // 32768 rows want 8 passes (32768 x 64: 57.0 -> 48.2 us, 8192 x 192: 28.8 -> 23.5, 32768 x 112:
+  // 22.6 -> 20.6), and the narrow C <= 24 tensors up to 524288 rows 1024 blocks (28.1 -> 25.7)
   const int M = pyr_valid_rows(*p);
   int passes = C >= 144 && p->nseg == 1 ? 32 : 16;
   if (M <= 8192 && C < 1024) passes = C <= 64 ? 8 : 16;  // D4's 8192 x 2688 keeps 32 (46.6 vs 64.0 us)
+  if (p->nseg == 1 && M <= 32768 && C < 1024) passes = 8;
   g.geo = row_geom(C, dev_knob(10) > 0 ? dev_knob(10) : passes);
   const int nb = total_chunks(*p, g.geo.CH);
   const size_t lds = 2 * C * sizeof(float2) + 2 * (size_t)g.geo.R * C * sizeof(float);
   EDET_DTYPE_DISPATCH(dtype, T, {
     // persistent blocks (r01h sweep: 1.51 -> 1.43 ms/step against 1024)
-    const int rcap = dev_knob(11) > 0 ? dev_knob(11) : (C <= 24 ? 256 : 512);
+    const int rcap = dev_knob(11) > 0 ? dev_knob(11) : (C <= 24 ? (M <= 524288 ? 1024 : 256) : 512);
     const int grid = nb < rcap ? nb : rcap;
     const int f = (x->act ? AF_ACT : 0) | (x->gate ? AF_GATE : 0) | (dsq ? AF_DSQ : 0) | (dv_scale ? AF_DVS : 0);
     if (nb) launch_reduce<T>(f, dim3(grid), row_block(g.geo), lds, (hipStream_t)stream, g, nb);

@@ -74,14 +74,20 @@ __device__ __forceinline__ void focal_elem(float x, float y, float alpha, float 
 //   fl  = at q^1.5 ce
 //   dfl = at (y ? -1 : 1) sqrt(q) (1.5 p (1-p) ce + q^2)
 // kpos / kneg fold at * sign * (1 / normaliser) for y = 1 / y = 0.
+// Three transcendentals per logit instead of four (round 6): with h = exp(-|x|/2) and
+// s = rsqrt(1 + h^2), z = h^2, r = s^2, sqrt(r) = s, sqrt(z r) = h s and log(1+z) = -2 log(s),
+// so the sigmoid's reciprocal and the modulating square root come from one v_rsq_f32
 __device__ __forceinline__ void focal_elem15(float x, bool y, float apos, float aneg, float kpos, float kneg,
                                              float& fl, float& dfl) {
-  const float z = __expf(-fabsf(x));
-  const float r = __builtin_amdgcn_rcpf(1.f + z);
+  const float h = __builtin_amdgcn_exp2f(fabsf(x) * -0.72134752044448170f);  // exp(-|x|/2)
+  const float z = h * h;
+  const float s = __builtin_amdgcn_rsqf(1.f + z);
+  const float r = s * s;
   const float zr = z * r;
-  const float q = ((x >= 0.f) != y) ? r : zr;
-  const float sq = __builtin_amdgcn_sqrtf(q);
-  const float ce = __logf(1.f + z) + fmaxf(y ? -x : x, 0.f);
+  const bool flip = (x >= 0.f) != y;
+  const float q = flip ? r : zr;
+  const float sq = flip ? s : h * s;
+  const float ce = fmaf(-1.3862943611198906f, __builtin_amdgcn_logf(s), fmaxf(y ? -x : x, 0.f));
   fl = (y ? apos : aneg) * q * sq * ce;
   dfl = (y ? kpos : kneg) * sq * fmaf(1.5f * zr * r, ce, q * q);
 }

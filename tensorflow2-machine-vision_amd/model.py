@@ -21,6 +21,7 @@ Inputs are NHWC torch tensors on the GPU, values in [0, 1] like the reference's 
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -35,6 +36,11 @@ from .runtime import Act, BNParam, Engine, ParamStore, Pyr, Tape, memset0, round
 
 CLS_LD_PAD = 8  # class / box logits row stride padded to a multiple of 8 in training
 
+
+
+# the SE-gated depthwise output is materialised for project convs of at least this many output
+# channels (0 = all); narrower ones read it lazily (EDET_MATERIALIZE_SE_MIN_N, same-box A/B)
+MATERIALIZE_SE_MIN_N = int(os.environ.get("EDET_MATERIALIZE_SE_MIN_N", "0"))
 
 class EfficientDetNet:
     def __init__(self, blocks_args=None, global_params: Optional[Config] = None, name: str = "",
@@ -270,7 +276,7 @@ class EfficientDetNet:
         # weight gradient) read it plain.  Also in inference, where BN + swish + gate could ride in
         # the GEMM's A staging: that lengthened the GEMMs' latency-bound K loops more than the
         # pass costs (config 2: 40.5k -> 31.2k images/s, r04k)
-        if self.materialize_se:
+        if self.materialize_se and (MATERIALIZE_SE_MIN_N <= 0 or sp.output_filters >= MATERIALIZE_SE_MIN_N):
             d = ops.materialize(eng, d, name=f"{pre}/se_out")
         return ops.conv1x1(eng, P, d, b["project_w"], sp.output_filters, bns=[b["bn2"]], name=f"{pre}/project")
 

@@ -145,7 +145,7 @@ def stem(eng: Engine, P: ParamStore, x: torch.Tensor, wname: str, bn: BNParam) -
 # --------------------------------------------------------------------------- 1x1 conv
 # output width from which the weight gradient reads a materialized copy of a lazy A operand
 # (scripts/kbench.py)
-WGRAD_MATERIALIZE_N = 64
+WGRAD_MATERIALIZE_N = int(os.environ.get("EDET_WGRAD_MATERIALIZE_N", "64"))
 
 
 def conv1x1(eng: Engine, P: ParamStore, x: Act, wname: str, N: int, bname: Optional[str] = None,
