@@ -218,11 +218,26 @@ class _StoreDither(torch.autograd.Function):
         return _dither_round(g, ctx.gen, ctx.frac), None, None, None
 
 
+class _OperandDither(torch.autograd.Function):
+    """Forward rounding only: a matrix-core operand the product rounds to bf16 while staging it
+    (gradient untouched -- the gradient of that value is rounded where it is stored)."""
+
+    @staticmethod
+    def forward(ctx, x, gen, frac):
+        return _dither_round(x, gen, frac)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None, None
+
+
 def bf16_dither_hooks(seed, frac=0.25):
-    """(store, gstore) for RefEfficientDet: bf16 storage emulated in both directions with a
-    seeded sub-ulp dither before each rounding (see _dither_round)."""
+    """(store, gstore, ostore) for RefEfficientDet: bf16 storage emulated in both directions with a
+    seeded sub-ulp dither before each rounding (see _dither_round), and the bf16 rounding of the
+    1x1 convolutions' lazily transformed A operands (ostore, forward only)."""
     gen = None if seed is None else torch.Generator().manual_seed(seed)
-    return (lambda t: _StoreDither.apply(t, gen, frac, True), lambda t: _StoreDither.apply(t, gen, frac, False))
+    return (lambda t: _StoreDither.apply(t, gen, frac, True), lambda t: _StoreDither.apply(t, gen, frac, False),
+            lambda t: _OperandDither.apply(t, gen, frac))
 
 
 def bf16_grad(t):
@@ -258,6 +273,9 @@ class RefEfficientDet:
         self.route_stats = {}
         self.store = None  # storage rounding of every tensor the product keeps in HBM (bf16 emulation)
         self.gstore = None  # gradient rounding at every conv / resample input (the stored dv)
+        # forward rounding of a 1x1 conv's A operand that the product transforms lazily (BN /
+        # swish applied while staging) and rounds to bf16 for the matrix cores
+        self.ostore = None
         self._names = {}
         self.p = {}
         if params is not None:
@@ -288,6 +306,12 @@ class RefEfficientDet:
         if id(x) in self._names:  # keep the pool routing's name on the wrapped value
             self._names[id(y)] = self._names[id(x)]
         return y
+
+    def _op(self, x):
+        """The A operand of a 1x1 conv (expand, resample): the product stages bf16(v(x)) for the
+        MFMA, so its value is rounded by ``ostore`` when emulating bf16 (a stored operand -- the
+        SE output, a depthwise output -- is already rounded and not wrapped)."""
+        return x if self.ostore is None or self.recording is not None else self.ostore(x)
 
     def _pool(self, x, stored):
         route = None
@@ -351,7 +375,7 @@ class RefEfficientDet:
         cin, e = b["cin"], b["cin"] * b["e"]
         if b["e"] != 1:
             n = conv_name()
-            x = self._st(Fn.conv2d(self._gin(x), self.w1x1(f"{pre}/{n}/kernel", e, cin, _cki(1, 1, e))))
+            x = self._st(Fn.conv2d(self._op(self._gin(x)), self.w1x1(f"{pre}/{n}/kernel", e, cin, _cki(1, 1, e))))
             x = self._t(f"{pre}/expand", swish(self.bn(x, f"{pre}/{bn_name()}", training, st)))
         k = b["k"]
         x = self._st(conv_same(self._gin(x), self.wdw(f"{pre}/depthwise_conv2d/depthwise_kernel", k, e, _cki(k, k, 1)), b["s"],
@@ -376,7 +400,7 @@ class RefEfficientDet:
         C = x.shape[1]
         x = self._gin(x)
         if C != F:
-            x = self._st(Fn.conv2d(x, self.w1x1(f"{prefix}/conv2d/kernel", F, C, ("glorot", C, F)),
+            x = self._st(Fn.conv2d(self._op(x), self.w1x1(f"{prefix}/conv2d/kernel", F, C, ("glorot", C, F)),
                                    self.w(f"{prefix}/conv2d/bias", (F,), ("const", 0.0))))
             x = self._t(prefix, self.bn(x, f"{prefix}/bn", training, st))
         if x.shape[2] > level_size:

@@ -207,7 +207,9 @@ def oracle_step(cfg, sd, x, masks, targets, routes, dtype=torch.float64, hooks=N
     every conv / resample input's gradient -- the dv the product's dgrads store -- rounded too)."""
     ref = RefEfficientDet(cfg, sd, dtype=dtype)
     if hooks is not None:
-        ref.store, ref.gstore = hooks
+        ref.store, ref.gstore = hooks[:2]
+        if len(hooks) > 2:
+            ref.ostore = hooks[2]
     ref.routes = routes
     keys = [k for k in ref.p if not k.endswith(("/moving_mean", "/moving_variance"))]
     for k in keys:
@@ -423,6 +425,7 @@ def test_d0_512_nc81_forward_bf16(training):
     ref = RefEfficientDet(cfg, m.state_dict())
     emu = RefEfficientDet(cfg, m.state_dict())
     emu.store = lambda t: t.to(torch.bfloat16).to(t.dtype)
+    emu.ostore = emu.store  # the 1x1 convs' lazily transformed A operands, rounded for the MFMA
     with torch.no_grad():
         rb, rc = ref.forward(xr.float().numpy(), training, om)
         eb, ec = emu.forward(xr.float().numpy(), training, om)
@@ -486,6 +489,7 @@ def test_d4_1024_forward_bf16():
     ref = RefEfficientDet(cfg, m.state_dict())
     emu = RefEfficientDet(cfg, m.state_dict())
     emu.store = lambda t: t.to(torch.bfloat16).to(t.dtype)
+    emu.ostore = emu.store  # the 1x1 convs' lazily transformed A operands, rounded for the MFMA
     with torch.no_grad():
         rb, rc = ref.forward(xr.float().numpy(), False)
         eb, ec = emu.forward(xr.float().numpy(), False)
@@ -565,6 +569,7 @@ def test_b0_224_b64_backbone_bf16_inference():
     ref = RefEfficientDet(cfg, m.state_dict())
     emu = RefEfficientDet(cfg, m.state_dict())
     emu.store = bf16_store
+    emu.ostore = bf16_store  # the expand convs' lazily transformed A operands, rounded for the MFMA
     with torch.no_grad():
         rs = ref.backbone(xs, False)
         es = [bf16_store(t) for t in emu.backbone(xs, False)]
