@@ -956,6 +956,10 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
   });
 }
 
+// the per-image reductions (SE squeeze, SE-fused BN reduce) shorten their chunks until a launch
+// holds at least this many blocks (two per CU)
+constexpr long FILL_BLOCKS = 512;
+
 static int img_reduce(int dtype, bool gategrad, const edet_lazy* x, int B, int HW, int C,
                       const void* dv, double* out64, hipStream_t s) {
   EDET_REQUIRE(x && out64 && x->x && (!gategrad || dv), "se reduce: null argument");
@@ -964,7 +968,12 @@ static int img_reduce(int dtype, bool gategrad, const edet_lazy* x, int B, int H
   g.lz = *x; g.lz.gate = nullptr;  // the pre-gate value
   g.p.nseg = 1; g.p.batch = B; g.p.row_off[0] = 0; g.p.H[0] = HW; g.p.W[0] = 1;
   g.dv = dv; g.out64 = out64; g.C = C; g.hw = HW;
-  g.geo = row_geom(C, 16);  // long chunks: each block ends in C fp64 atomics
+  // long chunks: each block ends in C fp64 atomics; round 6: halved (down to 4 passes) while the
+  // launch would hold fewer than FILL_BLOCKS blocks (the 32^2 / 64^2 stages ran 128-320 blocks)
+  int passes = dev_knob(44) > 0 ? dev_knob(44) : 16;
+  if (dev_knob(44) == 0)
+    while (passes > 4 && (long)B * cdiv(HW, row_geom(C, passes).CH) < FILL_BLOCKS) passes /= 2;
+  g.geo = row_geom(C, passes);
   g.cslices = 1;
   // C >= 480 over H*W <= 4096: a block per (image, 64-channel slice) over the whole image, as
   // edet_gate_bn_reduce (development slot 46 = 2: off)
@@ -1005,7 +1014,12 @@ int edet_gate_bn_reduce(int dtype, const edet_lazy* x, int B, int HW, int C, con
   g.dv = dv; g.out64 = sums5; g.C = C; g.hw = HW;
   // long chunks: every block ends in 5C fp64 atomics (0.69 -> 0.54 ms/step at 16 passes vs ~8;
   // 32 passes: 0.58 in round 1, 0.45 against 0.48 in the round-2 sweep after the table hoists)
-  g.geo = row_geom(C, dev_knob(12) > 0 ? dev_knob(12) : 32);
+  // (round 6: halved, down to 4 passes, while the launch would hold fewer than FILL_BLOCKS
+  // blocks: 32768 x 240 ran 128 blocks)
+  int passes = dev_knob(12) > 0 ? dev_knob(12) : 32;
+  if (dev_knob(12) == 0)
+    while (passes > 4 && (long)B * cdiv(HW, row_geom(C, passes).CH) < FILL_BLOCKS) passes /= 2;
+  g.geo = row_geom(C, passes);
   g.cslices = 1;
   // wide rows over short images (C >= 480, H*W <= 4096: the 16^2 / 32^2 / 64^2 stages): a block
   // per (image, 64-channel slice) walks the whole image, 32 rows per pass, and owns its outputs

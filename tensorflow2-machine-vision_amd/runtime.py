@@ -477,6 +477,8 @@ class Tape:
 # EDET_DEFER_PARTIALS=0: every weight-gradient split sum launched right after its kernel (the
 # round-5 behaviour), for same-box A/B
 DEFER_PARTIALS = os.environ.get("EDET_DEFER_PARTIALS", "1") != "0"
+# EDET_OVERLAP=1: weight gradients on the side stream (Engine.overlap), for same-box A/B
+OVERLAP = os.environ.get("EDET_OVERLAP", "0") == "1"
 _WORKSPACE = {}
 WORKSPACE_BYTES = 64 << 20
 
@@ -525,7 +527,7 @@ class Engine:
         # hand their memory to a main-stream op while a side kernel may still read it.  Off by
         # default: measured 1351 vs 1388 img/s (D0 b32) -- the wide side kernels take the CUs
         # the main chain needs instead of filling idle ones.
-        self.overlap = False
+        self.overlap = OVERLAP
         self._side = None
         self._side_used = False
         self._side_keep: list = []
