@@ -923,6 +923,11 @@ int edet_lazy_bwd_apply(int dtype, const edet_lazy* x, const edet_pyramid* p, in
   else if (x->gate && C >= 96 && C < 480) passes = 8;
   else if (C >= 672 && M >= 32768) passes = 16;
   else if (C >= 480 && C <= 672 && M <= 8192) passes = 4;  // not D4's 8192 x 960 (15.3 vs 17.6 us)
+  // round 6 (profiles/r06/r06ae_apply_materialize_sweep.txt): 8 passes for the ungated mid-width
+  // tensors up to 131072 rows (131072 x 240: 68.3 -> 64.5 us, 32768 x 112: 27.6 -> 22.2) and the
+  // C = 64 head pyramids (174592 x 64: 96.0 -> 89.9)
+  if (!x->gate && C >= 96 && C < 480 && M > 8192 && M <= 131072) passes = 8;
+  else if (p->nseg > 1 && C <= 64) passes = 8;
   g.geo = row_geom(C, dev_knob(8) > 0 ? dev_knob(8) : passes);
   g.cslices = 1;
   // wide rows over few of them (C >= 1024, M <= 16384: the 16^2 stage): 64-channel slices, 32 rows
@@ -1116,7 +1121,8 @@ int edet_lazy_materialize(int dtype, const edet_lazy* x, const edet_pyramid* p, 
   // and 8 for 144 <= C over 32768 <= M <= 131072 (32768 x 480: 42.4 -> 40.5 us per step,
   // profiles/r03ad_bn_plan_sweep.txt)
   const int M = pyr_valid_rows(*p);
-  const bool mid = C >= 144 && M >= 32768 && M <= 131072;
+  // (round 6, r06ae: 8 also for C >= 144 over >= 524288 rows, 524288 x 144: 58.5 -> 55.8 us)
+  const bool mid = C >= 144 && M >= 32768 && (M <= 131072 || M >= 524288);
   g.geo = row_geom(C, dev_knob(13) > 0 ? dev_knob(13) : (C >= 1024 || mid ? 8 : 4));
   g.cslices = 1;
   // C >= 1024 over M <= 16384: 64-channel slices, 32 rows per pass (as edet_lazy_bwd_apply;
