@@ -131,6 +131,12 @@ def algorithmic_bytes(name, args, es):
     if name == "edet_maxpool_bwd":  # (dtype, lz, B, H, W, C, dy, dx, acc, s)
         B, H, W, C, acc = args[2], args[3], args[4], args[5], args[8]
         return B * (H * W * (2 + acc) + ((H + 1) // 2) * ((W + 1) // 2)) * C * es
+    if name == "edet_maxpool_fwd_taps":  # (dtype, lz, B, H, W, C, y, taps, s): + one tap byte per output
+        B, H, W, C = args[2], args[3], args[4], args[5]
+        return B * (H * W * es + ((H + 1) // 2) * ((W + 1) // 2) * (es + 1)) * C
+    if name == "edet_maxpool_bwd_taps":  # (dtype, B, H, W, C, taps, dy, dx, acc, s): taps + dy, dx
+        B, H, W, C, acc = args[1], args[2], args[3], args[4], args[8]
+        return B * (H * W * (1 + acc) * es + ((H + 1) // 2) * ((W + 1) // 2) * (es + 1)) * C
     # (dtype, n, fi, w, B, H, W, C, ...); the one-pass backward (_dv, ABI 10) reads the raw F and
     # the value gradient where the two-pass form read y and dF: the same bytes
     if name in ("edet_bifpn_fuse_fwd", "edet_bifpn_fuse_bwd", "edet_bifpn_fuse_bwd_dv"):

@@ -349,6 +349,13 @@ int edet_maxpool_fwd(int dtype, const edet_lazy* x, int B, int H, int W, int C, 
                      edet_stream_t stream);
 int edet_maxpool_bwd(int dtype, const edet_lazy* x, int B, int H, int W, int C,
                      const void* dy, void* dx, int accumulate, edet_stream_t stream);
+/* round 6: the forward records each output's window tap (0..8, row-major) per channel in
+ * taps [B*ceil(H/2)*ceil(W/2)][C] (uint8); the backward then routes dy by the taps alone -- no
+ * input values, no BN tables, no window re-evaluation.  Same results as edet_maxpool_bwd. */
+int edet_maxpool_fwd_taps(int dtype, const edet_lazy* x, int B, int H, int W, int C, void* y,
+                          uint8_t* taps, edet_stream_t stream);
+int edet_maxpool_bwd_taps(int dtype, int B, int H, int W, int C, const uint8_t* taps,
+                          const void* dy, void* dx, int accumulate, edet_stream_t stream);
 int edet_bifpn_fuse_fwd(int dtype, int n_in, const edet_fuse_input* ins, const float* w,
                         int B, int H, int W, int C, void* out, edet_stream_t stream);
 int edet_bifpn_fuse_bwd(int dtype, int n_in, const edet_fuse_input* ins, const float* w,

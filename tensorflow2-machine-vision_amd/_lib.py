@@ -167,6 +167,8 @@ SIGNATURES = {
     "edet_lazy_materialize": [c_int, PLazy, PPyr, c_int, P, P],
     "edet_maxpool_fwd": [c_int, PLazy, c_int, c_int, c_int, c_int, P, P],
     "edet_maxpool_bwd": [c_int, PLazy, c_int, c_int, c_int, c_int, P, P, c_int, P],
+    "edet_maxpool_fwd_taps": [c_int, PLazy, c_int, c_int, c_int, c_int, P, P, P],
+    "edet_maxpool_bwd_taps": [c_int, c_int, c_int, c_int, c_int, P, P, P, c_int, P],
     "edet_bifpn_fuse_fwd": [c_int, c_int, PFuse, P, c_int, c_int, c_int, c_int, P, P],
     "edet_bifpn_fuse_bwd": [c_int, c_int, PFuse, P, c_int, c_int, c_int, c_int, P, P, P, P],
     "edet_bifpn_fuse_bwd_dv_parts": [c_int, c_int, PFuse, c_int, c_int, c_int, c_int, POINTER(c_int)],

@@ -428,7 +428,8 @@ __device__ __forceinline__ void affine8(const edet_lazy& lz, int c, int C, float
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void k_maxpool_fwd(edet_lazy lz, int B, int H, int W, int C, T* y) {
+__global__ __launch_bounds__(256) void k_maxpool_fwd(edet_lazy lz, int B, int H, int W, int C, T* y,
+                                                     uint8_t* taps) {
   extern __shared__ float2 aft[];  // [C]
   load_affine(lz, C, 1.f / (float)(B * H * W), aft);
   __syncthreads();
@@ -443,9 +444,58 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd(edet_lazy lz, int B, int H,
   float2 af[8];
   affine8_lds(aft, cv * 8, af);
   float best[8];
-  int arg[8];
-  pool_window<T>(lz, af, (size_t)n * H * W, H, W, same_pad(H, 3, 2), same_pad(W, 3, 2), oy, ox, cv * 8, 8, best, arg);
+  int arg[8], tap[8];
+  pool_window<T>(lz, af, (size_t)n * H * W, H, W, same_pad(H, 3, 2), same_pad(W, 3, 2), oy, ox, cv * 8, 8, best, arg,
+                 tap);
   st8(y + (size_t)pix * C + cv * 8, best);
+  if (taps) store_taps(taps + (size_t)pix * C + cv * 8, tap);
+}
+
+// max-pool backward from the forward's recorded window taps (edet_maxpool_bwd_taps, round 6):
+// an input pixel's <= 2 x 2 covering windows are read at once -- taps and dy, no input values,
+// no BN tables -- instead of re-evaluating up to four 3 x 3 windows one after another
+// (resample_p6/p7: 16 -> a few us per call)
+template <typename T>
+__global__ __launch_bounds__(256) void k_maxpool_bwd_taps(int B, int H, int W, int C, const uint8_t* taps,
+                                                          const T* dy, T* dx, int accumulate) {
+  const int OH = cdiv(H, 2), OW = cdiv(W, 2), nv = C / 8;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)B * H * W * nv) return;
+  const int cv = (int)(idx % nv), c = cv * 8;
+  const long pix = idx / nv;
+  const int n = (int)(pix / ((long)H * W));
+  const int rem = (int)(pix - (long)n * H * W);
+  const int iy = rem / W, ix = rem - iy * W;
+  const int pt = same_pad(H, 3, 2), pl = same_pad(W, 3, 2);
+  const int oy_lo = max(0, fdiv(iy + pt - 1, 2)), oy_hi = min(OH - 1, fdiv(iy + pt, 2));
+  const int ox_lo = max(0, fdiv(ix + pl - 1, 2)), ox_hi = min(OW - 1, fdiv(ix + pl, 2));
+  const size_t o0 = (size_t)n * OH * OW;
+  uint2 tq[4];
+  float g[4][8];
+  bool ok[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // every window's loads issued before any is used
+    const int oy = oy_lo + (k >> 1), ox = ox_lo + (k & 1);
+    ok[k] = oy <= oy_hi && ox <= ox_hi;
+    const size_t o = (o0 + (ok[k] ? (size_t)oy * OW + ox : 0)) * C + c;
+    tq[k] = *reinterpret_cast<const uint2*>(taps + o);
+    ld8(dy + o, g[k]);
+  }
+  float d[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // windows in row-major order (the recompute path's order)
+    if (!ok[k]) continue;
+    const int oy = oy_lo + (k >> 1), ox = ox_lo + (k & 1);
+    const int kme = (iy - (oy * 2 - pt)) * 3 + (ix - (ox * 2 - pl));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int tap = (int)(((j < 4 ? tq[k].x : tq[k].y) >> (8 * (j & 3))) & 0xffu);
+      if (tap == kme) d[j] += g[k][j];
+    }
+  }
+  acc8m(dx + (size_t)pix * C + c, 8, d, accumulate);
 }
 
 // gather form of the max-pool backward: input pixel collects dy of every window whose
@@ -1292,8 +1342,38 @@ int edet_maxpool_fwd(int dtype, const edet_lazy* x, int B, int H, int W, int C, 
   const long n = (long)B * cdiv(H, 2) * cdiv(W, 2) * (C / 8);
   const int nb = (int)((n + 255) / 256);
   EDET_DTYPE_DISPATCH(dtype, T, {
-    if (nb) EDET_LAUNCH(k_maxpool_fwd<T>, dim3(nb), dim3(256), C * sizeof(float2), (hipStream_t)stream, *x, B, H, W, C, (T*)y);
+    if (nb)
+      EDET_LAUNCH(k_maxpool_fwd<T>, dim3(nb), dim3(256), C * sizeof(float2), (hipStream_t)stream, *x, B, H, W, C, (T*)y,
+                  (uint8_t*)nullptr);
     return check_launch("edet maxpool_fwd");
+  });
+}
+
+int edet_maxpool_fwd_taps(int dtype, const edet_lazy* x, int B, int H, int W, int C, void* y, uint8_t* taps,
+                          edet_stream_t stream) {
+  EDET_REQUIRE(x && x->x && y && taps, "maxpool_fwd_taps: null argument");
+  EDET_REQUIRE(C % 8 == 0 && x->ld % 8 == 0 && x->gate == nullptr, "maxpool_fwd_taps: need C%%8==0, no gate");
+  const long n = (long)B * cdiv(H, 2) * cdiv(W, 2) * (C / 8);
+  const int nb = (int)((n + 255) / 256);
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    if (nb)
+      EDET_LAUNCH(k_maxpool_fwd<T>, dim3(nb), dim3(256), C * sizeof(float2), (hipStream_t)stream, *x, B, H, W, C, (T*)y,
+                  taps);
+    return check_launch("edet maxpool_fwd_taps");
+  });
+}
+
+int edet_maxpool_bwd_taps(int dtype, int B, int H, int W, int C, const uint8_t* taps, const void* dy, void* dx,
+                          int accumulate, edet_stream_t stream) {
+  EDET_REQUIRE(taps && dy && dx, "maxpool_bwd_taps: null argument");
+  EDET_REQUIRE(C % 8 == 0 && B > 0 && H > 0 && W > 0, "maxpool_bwd_taps: need C%%8==0 and a non-empty plane");
+  const long n = (long)B * H * W * (C / 8);
+  const int nb = (int)((n + 255) / 256);
+  EDET_DTYPE_DISPATCH(dtype, T, {
+    if (nb)
+      EDET_LAUNCH(k_maxpool_bwd_taps<T>, dim3(nb), dim3(256), 0, (hipStream_t)stream, B, H, W, C, taps, (const T*)dy,
+                  (T*)dx, accumulate);
+    return check_launch("edet maxpool_bwd_taps");
   });
 }
 

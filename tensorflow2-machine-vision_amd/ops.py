@@ -370,15 +370,25 @@ def maxpool(eng: Engine, x: Act, name: str = "") -> Act:
     B, H, W, C = x.pyr.batch, x.pyr.H, x.pyr.W, x.C
     pout = x.pyr.strided(2)
     y = eng.empty(pout.rows, C)
-    L.call("edet_maxpool_fwd", eng.dt, x.lazy(), B, H, W, C, vp(y), stream())
+    # training: the forward records its window taps, the backward routes dy by them
+    taps = (torch.empty((pout.rows, C), dtype=torch.uint8, device=eng.device)
+            if eng.training and L.has("edet_maxpool_fwd_taps") else None)
+    if taps is not None:
+        L.call("edet_maxpool_fwd_taps", eng.dt, x.lazy(), B, H, W, C, vp(y), vp(taps), stream())
+    else:
+        L.call("edet_maxpool_fwd", eng.dt, x.lazy(), B, H, W, C, vp(y), stream())
     out = Act(y, pout, C, training=eng.training, name=name)
 
     def bwd():
         rec = eng.tape.take(out)
         if rec is None:
             return
+        assert rec.ld == C
         dx, acc = eng.tape.dst(x)
-        L.call("edet_maxpool_bwd", eng.dt, x.lazy(), B, H, W, C, vp(rec.t), vp(dx), acc, stream())
+        if taps is not None:
+            L.call("edet_maxpool_bwd_taps", eng.dt, B, H, W, C, vp(taps), vp(rec.t), vp(dx), acc, stream())
+        else:
+            L.call("edet_maxpool_bwd", eng.dt, x.lazy(), B, H, W, C, vp(rec.t), vp(dx), acc, stream())
 
     eng.record(bwd)
     return out

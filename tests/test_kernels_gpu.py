@@ -745,6 +745,39 @@ def test_maxpool_bwd_bf16_exact(H, W):
 
 
 @pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("H,W", [(16, 16), (9, 7), (8, 8), (3, 5), (64, 64)])
+@pytest.mark.parametrize("acc", [0, 1])
+def test_maxpool_taps_equal_recompute(dt, H, W, acc):
+    """edet_maxpool_fwd_taps / _bwd_taps (the training route of ops.maxpool, resample_p6/p7)
+    against edet_maxpool_fwd / _bwd, which re-evaluate the windows: the same pooled values and,
+    bit for bit, the same dx (the taps record the forward's own argmax, ties included -- bf16
+    inputs with many ties), accumulating into dx or not."""
+    rng = np.random.default_rng(3 * H + W + acc)
+    B, C = 3, 64
+    pyr = Pyr(B, [(H, W)])
+    x = pyr_data(rng, pyr, C, dt)
+    if dt == "bf16":  # coarse values: many exact ties inside the windows
+        x = (x.float() * 4).round().to(torch.bfloat16) / 4
+    bn = make_bn(x, pyr, C, rng)
+    lz = LazyDesc(x, pyr, C, bn=bn)
+    OH, OW = (H + 1) // 2, (W + 1) // 2
+    y0 = torch.empty(B * OH * OW, C, dtype=TDT[dt], device=DEV)
+    y1 = torch.empty_like(y0)
+    taps = torch.full((B * OH * OW, C), 255, dtype=torch.uint8, device=DEV)
+    L.call("edet_maxpool_fwd", DT[dt], lz.c, B, H, W, C, vp(y0), stream())
+    L.call("edet_maxpool_fwd_taps", DT[dt], lz.c, B, H, W, C, vp(y1), vp(taps), stream())
+    dy = g(rnd(rng, B * OH * OW, C), dt)
+    base = g(rnd(rng, B * H * W, C), dt)
+    dx0, dx1 = base.clone(), base.clone()
+    L.call("edet_maxpool_bwd", DT[dt], lz.c, B, H, W, C, vp(dy), vp(dx0), acc, stream())
+    L.call("edet_maxpool_bwd_taps", DT[dt], B, H, W, C, vp(taps), vp(dy), vp(dx1), acc, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    assert int(taps.max()) <= 8
+    assert torch.equal(dx0, dx1)
+
+
+@pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("B,H,W", [(2, 8, 8), (4, 136, 136)])  # the second exceeds the forward's 2048-block grid
 def test_bifpn_fuse(dt, B, H, W):
     rng = np.random.default_rng(11)

@@ -14,7 +14,7 @@ if [ -n "${TESTS_K:-}" ]; then
   rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ -n "${KB_FILTER:-}" ]; then
-  TAG=$TAG/abk OLD=$L/libedet_base.so NEW=$L/libedet.so REPS=2 HEADN=${HEADN:-40} KB_ARGS="--filter $KB_FILTER" \
+  TAG=$TAG/abk OLD=$L/libedet_base.so NEW=$L/libedet.so OLDENV="EDET_ALLOW_MISSING=1" REPS=2 HEADN=${HEADN:-40} KB_ARGS="--filter $KB_FILTER" \
       bash tools/ab_kbench.sh || exit 1
 fi
-STEPS=30 TAG=$TAG/ab VARIANTS="old:EDET_LIB=$L/libedet_base.so new:EDET_LIB=$L/libedet.so" REPS=${ABREPS:-3} bash tools/ab_bench.sh
+STEPS=30 TAG=$TAG/ab VARIANTS="old:EDET_LIB=$L/libedet_base.so,EDET_ALLOW_MISSING=1 new:EDET_LIB=$L/libedet.so" REPS=${ABREPS:-3} bash tools/ab_bench.sh
