@@ -279,14 +279,24 @@ __global__ __launch_bounds__(256) void k_loss(LossArgs g) {
 __global__ void k_count_pos(const uint8_t* mask, int64_t n, float* out) {
   __shared__ float red[4];
   float s = 0.f;
-  const int64_t nv = n / 16;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (int64_t)gridDim.x * 256) {
-    const uint4 v = reinterpret_cast<const uint4*>(mask)[i];
-    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+  const int64_t nv = n / 16, stride = (int64_t)gridDim.x * 256;
+  // four 16-byte vectors per trip, all requested before any is counted (the 64-block grid
+  // walked ~6 dependent loads per thread: 14.9 us for D0's 1.6 MB of masks)
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < nv; i0 += 4 * stride) {
+    uint4 v[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride;
+      v[u] = i < nv ? reinterpret_cast<const uint4*>(mask)[i] : make_uint4(0u, 0u, 0u, 0u);
+    }
 #pragma unroll
-      for (int b = 0; b < 4; ++b) s += ((w4[k] >> (8 * b)) & 0xffu) ? 1.f : 0.f;
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) s += ((w4[k] >> (8 * b)) & 0xffu) ? 1.f : 0.f;
+    }
   }
   for (int64_t i = nv * 16 + (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     s += mask[i] ? 1.f : 0.f;
@@ -336,8 +346,10 @@ int edet_count_positives(const uint8_t* mask, int64_t n, float* out, edet_stream
   EDET_REQUIRE(mask && out, "count_positives: null argument");
   if (n <= 0) return EDET_OK;
   EDET_REQUIRE(((uintptr_t)mask & 15) == 0, "count_positives: mask must be 16-byte aligned");
-  int nb = (int)((n / 16 + 255) / 256);
-  if (nb > 64) nb = 64;
+  // one trip of four vectors per thread where that takes at most 128 blocks (each block ends
+  // in one fp32 atomic on the same address: integer counts, exact in any order)
+  int nb = (int)((n / 16 + 1023) / 1024);
+  if (nb > 128) nb = 128;
   if (nb < 1) nb = 1;
   EDET_LAUNCH(k_count_pos, dim3(nb), dim3(256), 0, (hipStream_t)stream, mask, n, out);
   return check_launch("edet count_positives");
