@@ -167,6 +167,10 @@ const char* edet_last_error(void);
 int edet_abi_version(void);
 int edet_memset_async(void* p, int value, size_t bytes, edet_stream_t stream);
 int edet_memcpy_async(void* dst, const void* src, size_t bytes, edet_stream_t stream);
+/* round 6: zero up to EDET_ZERO_MAX 16-byte aligned device ranges in one launch (the step's
+ * per-step accumulators: gradients, BN statistics, loss scalars) */
+#define EDET_ZERO_MAX 8
+int edet_zero_ranges(int n, void* const* ptrs, const size_t* bytes, edet_stream_t stream);
 /* Register device scratch used by split reductions (weight gradients write per-split partials
  * and sum them in a fixed order instead of issuing atomics).  The buffer must stay valid while
  * kernels that may use it are queued; NULL unregisters (atomics fallback).  Not thread-safe:

@@ -133,6 +133,7 @@ SIGNATURES = {
     "edet_abi_version": [],
     "edet_memset_async": [P, c_int, c_size_t, P],
     "edet_memcpy_async": [P, P, c_size_t, P],
+    "edet_zero_ranges": [c_int, P, P, P],
     "edet_set_workspace": [P, c_size_t],
     "edet_partials_defer": [P, c_size_t],
     "edet_partials_flush": [POINTER(c_size_t), P],

@@ -79,6 +79,29 @@ float* workspace_f32(size_t n_floats) {
   return (g_ws && n_floats * sizeof(float) <= g_ws_bytes) ? (float*)g_ws : nullptr;
 }
 
+// several zero fills in one launch (edet_zero_ranges): the step's per-step accumulators were
+// one fill kernel each.  Chunk k of the concatenated ranges is 16 bytes of range i, first[i] <=
+// k < first[i + 1]; a range's partial last chunk is written byte by byte
+struct ZeroArgs {
+  char* p[EDET_ZERO_MAX];
+  long bytes[EDET_ZERO_MAX];
+  long first[EDET_ZERO_MAX + 1];
+  int n;
+};
+__global__ __launch_bounds__(256) void k_zero_ranges(ZeroArgs a) {
+  const long total = a.first[a.n];
+  for (long k = (long)blockIdx.x * 256 + threadIdx.x; k < total; k += (long)gridDim.x * 256) {
+    int i = 0;
+    while (i + 1 < a.n && k >= a.first[i + 1]) ++i;
+    const long off = (k - a.first[i]) * 16;
+    if (off + 16 <= a.bytes[i]) {
+      *reinterpret_cast<uint4*>(a.p[i] + off) = make_uint4(0u, 0u, 0u, 0u);
+    } else {
+      for (long b = off; b < a.bytes[i]; ++b) a.p[i][b] = 0;
+    }
+  }
+}
+
 // out[i] += sum_{s < S} part[s * n + i]: one thread per output and chunk of at most
 // SUM_CHUNK partials (8 independent loads in flight).  A single chunk adds in a fixed order;
 // more chunks (grid.y) spread the splits over the chip and add their sums with fp32 atomics
@@ -285,6 +308,26 @@ int edet_memset_async(void* p, int value, size_t bytes, edet_stream_t stream) {
     return EDET_EHIP;
   }
   return EDET_OK;
+}
+
+int edet_zero_ranges(int n, void* const* ptrs, const size_t* bytes, edet_stream_t stream) {
+  EDET_REQUIRE(n >= 0 && n <= EDET_ZERO_MAX && (n == 0 || (ptrs && bytes)), "zero_ranges: 0..%d ranges", EDET_ZERO_MAX);
+  edet::ZeroArgs a{};
+  long chunks = 0;
+  for (int i = 0; i < n; ++i) {
+    EDET_REQUIRE(ptrs[i] != nullptr || bytes[i] == 0, "zero_ranges: null range %d", i);
+    EDET_REQUIRE(((uintptr_t)ptrs[i] & 15) == 0, "zero_ranges: range %d not 16-byte aligned", i);
+    a.p[a.n] = (char*)ptrs[i];
+    a.bytes[a.n] = (long)bytes[i];
+    a.first[a.n] = chunks;
+    chunks += (long)((bytes[i] + 15) / 16);
+    if (bytes[i]) ++a.n;
+  }
+  a.first[a.n] = chunks;
+  if (chunks == 0) return EDET_OK;
+  const int grid = (int)std::min<long>(1024, (chunks + 255) / 256);
+  EDET_LAUNCH(edet::k_zero_ranges, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+  return edet::check_launch("edet zero_ranges");
 }
 
 int edet_memcpy_async(void* dst, const void* src, size_t bytes, edet_stream_t stream) {

@@ -32,7 +32,7 @@ from . import ops
 from .anchors import Anchors, Targets
 from .config import (BlockSpec, Config, efficientnet_b0_blocks, expand_blocks, get_efficientdet_config,
                      get_feat_sizes, round_filters)
-from .runtime import Act, BNParam, Engine, ParamStore, Pyr, Tape, memset0, round_up, stream, vp
+from .runtime import Act, BNParam, Engine, ParamStore, Pyr, Tape, memset0, memset0_many, round_up, stream, vp
 
 CLS_LD_PAD = 8  # class / box logits row stride padded to a multiple of 8 in training
 
@@ -520,10 +520,7 @@ class EfficientDetNetTrain(EfficientDetNet):
         x = data[0]
         B = x.shape[0]
         s = stream()
-        memset0(P.g)
-        memset0(P.bn_tstats)
-        memset0(self.scalars)
-        memset0(self.level_parts)
+        memset0_many([P.g, P.bn_tstats, self.scalars, self.level_parts])
         pyr = Pyr(B, [self.level_hw[l] for l in self.levels])
         t = self._targets(data, pyr)
         # N+ = sum(masks) + 1 (the +1 is added by the loss kernel); padding rows are never read

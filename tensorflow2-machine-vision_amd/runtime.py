@@ -607,6 +607,20 @@ class Engine:
         self._side_keep.clear()
 
 
+def memset0_many(ts):
+    """Zero several device tensors in one launch (edet_zero_ranges), or one fill each with a
+    library that lacks it."""
+    ts = [t for t in ts if t.numel()]
+    if not L.has("edet_zero_ranges") or len(ts) > 8 or any(t.data_ptr() % 16 for t in ts):
+        for t in ts:
+            memset0(t)
+        return
+    n = len(ts)
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+    sizes = (ctypes.c_size_t * n)(*[t.numel() * t.element_size() for t in ts])
+    L.call("edet_zero_ranges", n, ptrs, sizes, stream())
+
+
 def memset0(t: torch.Tensor):
     L.call("edet_memset_async", _vp(t), 0, t.numel() * t.element_size(), stream())
 

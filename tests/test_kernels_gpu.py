@@ -744,6 +744,23 @@ def test_maxpool_bwd_bf16_exact(H, W):
     assert torch.equal(dx.double().cpu(), v.grad)
 
 
+def test_zero_ranges():
+    """edet_zero_ranges (the train step's per-step accumulators in one launch): ranges of odd
+    byte counts inside one guarded buffer are zeroed exactly, their neighbours untouched."""
+    buf = torch.full((1 << 22,), 7, dtype=torch.uint8, device=DEV)
+    spans = [(0, 40), (256, 1 << 20), (2 << 20, 17), (3 << 20, 16), (3 << 20 | 4096, 15 * 16 + 9), (4000000, 0)]
+    ptrs = (ctypes.c_void_p * len(spans))(*[buf.data_ptr() + o for o, _ in spans])
+    sizes = (ctypes.c_size_t * len(spans))(*[n for _, n in spans])
+    L.call("edet_zero_ranges", len(spans), ptrs, sizes, stream())
+    torch.cuda.synchronize()
+    want = torch.full((1 << 22,), 7, dtype=torch.uint8)
+    for o, n in spans:
+        want[o:o + n] = 0
+    assert torch.equal(buf.cpu(), want)
+    with pytest.raises(L.EdetError):  # a misaligned range is refused
+        L.call("edet_zero_ranges", 1, (ctypes.c_void_p * 1)(buf.data_ptr() + 8), (ctypes.c_size_t * 1)(16), stream())
+
+
 @pytest.mark.parametrize("dt", DTS)
 @pytest.mark.parametrize("H,W", [(16, 16), (9, 7), (8, 8), (3, 5), (64, 64)])
 @pytest.mark.parametrize("acc", [0, 1])
