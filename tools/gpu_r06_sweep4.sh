@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-6 re-sweep of the tiled depthwise backward's launch plan (development build, kbench
+# replays): slot 30 = block floor, slot 31 = tiles per block.  (libedet_dev.so un-ignored)
+set -u -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-r06ak}; mkdir -p $O
+export EDET_LIB=tensorflow2-machine-vision_amd/lib/libedet_dev.so EDET_ALLOW_MISSING=1
+run() {  # variant dev
+  for rep in 1 2; do
+    D=""; [ -n "$2" ] && D="--dev $2"
+    timeout -k 10 300 python scripts/kbench.py --top 600 --reps 5 --filter edet_dwconv_bwd $D --out $O/kb_$1_$rep.txt > $O/kb_$1.log 2>&1 \
+      || { tail -5 $O/kb_$1.log; return 1; }
+  done
+}
+run base ""
+run f384 30=384
+run f1536 30=1536
+run f3072 30=3072
+run t1 31=1
+run t2 31=2
+run t4 31=4
+python tools/sweep_table.py $O base x 0.0 > $O/sweep.txt
+head -40 $O/sweep.txt
