@@ -13,12 +13,19 @@ run() {  # variant dev
       || { tail -5 $O/kb_$1.log; return 1; }
   done
 }
-run base ""
-run f384 30=384
-run f1536 30=1536
-run f3072 30=3072
-run t1 31=1
-run t2 31=2
-run t4 31=4
+if [ "${SWEEP:-plan}" = form ]; then
+  run base ""
+  run rows 29=2
+  run rows512 29=2,16=512
+  run rows2048 29=2,16=2048
+else
+  run base ""
+  run f384 30=384
+  run f1536 30=1536
+  run f3072 30=3072
+  run t1 31=1
+  run t2 31=2
+  run t4 31=4
+fi
 python tools/sweep_table.py $O base x 0.0 > $O/sweep.txt
 head -40 $O/sweep.txt
