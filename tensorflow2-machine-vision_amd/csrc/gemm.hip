@@ -2265,6 +2265,17 @@ static int dispatch_gemm_kloop(GemmArgs g, hipStream_t s) {
     }
   }
 #endif
+  // Round-6 tile sweep of the plain, statistics-free products (the 1x1 dgrads; development slots
+  // 42 / 43, profiles/r06/r06ap_gemm_tile_sweep.txt): a short K loop into a wide output wants
+  // column tiles -- more blocks, A re-read per tile from L2 -- (131072 x 40 -> 240: 33.5 -> 22.3
+  // us, 32768 x 80 -> 240: 12.9 -> 10.3), and the class head's deep dgrad 128-row tiles
+  // (174592 x 729 -> 64: 66.0 -> 59.5)
+  if constexpr (FOLD == 0 && !LAZY && sizeof(T) == 2) {
+    if (!g.has_stats && g.M >= 131072 && g.K <= 64 && NP > 64) return launch_gemm<T, 64, 64, LAZY, 32, FOLD>(g, s);
+    if (!g.has_stats && g.M >= 131072 && g.K > 512 && NP <= 64) return launch_gemm<T, 128, 64, LAZY, 32, FOLD>(g, s);
+    if (!g.has_stats && g.M >= 32768 && g.M < 131072 && g.K <= 128 && NP > 128 && NP <= 320)
+      return launch_gemm<T, 64, 128, LAZY, 32, FOLD>(g, s);
+  }
   if (only32 || cdiv(g.M, 64) < 512) {
     if (NP <= 64) return launch_gemm<T, 32, 64, LAZY, 32, FOLD>(g, s);
     if (NP <= 96) return launch_gemm<T, 32, 96, LAZY, 32, FOLD>(g, s);

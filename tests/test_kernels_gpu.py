@@ -92,7 +92,11 @@ def test_conv1x1_fwd(dt, M, K, N, lazy, nseg):
                                        (500, 320, 1152, 320), (300, 36, 64, 40), (1000, 224, 224, 224),
                                        (600, 729, 224, 736), (2000, 96, 16, 96), (1500, 144, 24, 144),
                                        # round-5 K-loop tiles at 8192 rows: 128 x 64 / 64 x 64
-                                       (8192, 320, 1152, 320), (8192, 1152, 192, 1152)])
+                                       (8192, 320, 1152, 320), (8192, 1152, 192, 1152),
+                                       # round-6 tiles: short K into wide dx (64 x 64 / 64 x 128),
+                                       # the class head's deep dgrad (128 x 64)
+                                       (131072, 40, 240, 40), (32768, 80, 240, 80),
+                                       (131200, 729, 64, 736)])
 def test_conv1x1_dgrad(dt, M, N, K, ldy):
     rng = np.random.default_rng(M * 7 + N)
     pyr = Pyr(1, [(M, 1)])

@@ -13,7 +13,19 @@ run() {  # variant dev
       || { tail -5 $O/kb_$1.log; return 1; }
   done
 }
-if [ "${SWEEP:-plan}" = form ]; then
+if [ "${SWEEP:-plan}" = gemm ]; then
+  F=edet_conv1x1_fwd,edet_conv1x1_dgrad
+  runf() { for rep in 1 2; do D=""; [ -n "$2" ] && D="--dev $2"
+    timeout -k 10 300 python scripts/kbench.py --top 600 --reps 5 --filter $F $D --out $O/kb_$1_$rep.txt > $O/kb_$1.log 2>&1 \
+      || { tail -5 $O/kb_$1.log; return 1; }; done; }
+  runf base ""
+  runf m64n64 42=64,43=64
+  runf m128n64 42=128,43=64
+  runf m64n128 42=64,43=128
+  runf m32n64 42=32,43=64
+  runf m32n128 42=32,43=128
+  runf m128n128 42=128,43=128
+elif [ "${SWEEP:-plan}" = form ]; then
   run base ""
   run rows 29=2
   run rows512 29=2,16=512
