@@ -25,6 +25,15 @@ if [ "${SWEEP:-plan}" = gemm ]; then
   runf m32n64 42=32,43=64
   runf m32n128 42=32,43=128
   runf m128n128 42=128,43=128
+elif [ "${SWEEP:-plan}" = dwform ]; then
+  F=edet_dwconv_fwd,edet_dwconv_wgrad
+  runf() { for rep in 1 2; do D=""; [ -n "$2" ] && D="--dev $2"
+    timeout -k 10 300 python scripts/kbench.py --top 600 --reps 5 --filter $F $D --out $O/kb_$1_$rep.txt > $O/kb_$1.log 2>&1 \
+      || { tail -5 $O/kb_$1.log; return 1; }; done; }
+  runf base ""
+  runf tile 27=1
+  runf dw3 27=2
+  runf rows 27=5
 elif [ "${SWEEP:-plan}" = form ]; then
   run base ""
   run rows 29=2
